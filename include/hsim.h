@@ -1,0 +1,120 @@
+/* hsim -- MI355X-native batched humanoid simulation: the drop-in C ABI.
+ *
+ * This is the boundary the reference's Python env would bind instead of the `mujoco`
+ * pybind11 module + SB3's SubprocVecEnv.  Each entry point names the reference interface it
+ * replaces (paths relative to the reference repo):
+ *
+ *   hs_model_load        <- mujoco.MjModel.from_xml_path(model_path)      custom_env.py:53
+ *   hs_model_field       <- MjModel attribute reads (nq, nv, nu, body_mass, ...) custom_env.py:87,59-61
+ *   hs_batch_create      <- mujoco.MjData(model) per env                  custom_env.py:54
+ *                           x SubprocVecEnv([make_env(...)] * n_envs)     train_sb3.py:203
+ *   hs_set_config        <- env_config keys duration/frame_skip/reward_config custom_env.py:21-32,
+ *                           train_sb3.py:183-200
+ *   hs_reset             <- HumanoidEnv.reset: mj_resetData + noise + one mj_step  custom_env.py:97-150
+ *   hs_step              <- HumanoidEnv.step: frame_skip x mj_step, _get_state, reward, done
+ *                           custom_env.py:152-230 (+ SB3 auto-reset on done)
+ *   hs_physics_step      <- raw `data.ctrl[:] = a; mujoco.mj_step(model, data)` custom_env.py:159-160
+ *   hs_state_io          <- reads/writes of data.qpos/qvel/qacc_warmstart/time/ctrl (custom_env.py:105-117)
+ *   hs_get_buffers       <- data.* arrays as device buffers (obs, reward, terminated, ...)
+ *   hs_last_error        <- mujoco's error callback / MjModel load error string
+ *
+ * Conventions: status int (0 ok, <0 error, message via hs_last_error(), thread-local); the
+ * model is immutable and shareable; a batch owns (or is bound to) device buffers; every call
+ * takes an optional HIP stream (NULL = default stream) and is asynchronous unless noted; a
+ * batch is not re-entrant.  No torch types cross this boundary.
+ */
+#ifndef HSIM_H
+#define HSIM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct hs_model hs_model;
+typedef struct hs_batch hs_batch;
+
+enum { HS_FP32 = 0, HS_FP64 = 1 };
+enum { HS_REWARD_NONE = -1, HS_REWARD_STAND = 0, HS_REWARD_KNEELING = 1, HS_REWARD_WALK = 2 };
+enum { HS_WARN_BADQPOS = 0, HS_WARN_BADQVEL = 1, HS_WARN_BADQACC = 2, HS_WARN_OVERFLOW = 3, HS_NWARN = 4 };
+#define HS_AUXDIM 40   /* per env aux row: qacc[32], com[3], ncon, nefc, newton iterations, pad */
+
+/* Env semantics (custom_env.py defaults in brackets; train_sb3.py overrides in parentheses). */
+typedef struct {
+  int frame_skip;          /* [5] (3)   custom_env.py:28, train_sb3.py:199 */
+  int max_steps;           /* [750]     custom_env.py:201 forced truncation */
+  int reward_id;           /* HS_REWARD_*; reward_config['type'] custom_env.py:263-271 */
+  int autoreset;           /* 1 = SB3 VecEnv auto-reset (terminal obs kept in terminal_obs) */
+  int max_newton;          /* Newton iteration cap [100 = opt.iterations] */
+  int reserved;
+  double duration;         /* [15] (10.0) custom_env.py:23, train_sb3.py:187 */
+  double init_height;      /* 1.282   custom_env.py:59 */
+  double noise_scale;      /* 0.01    custom_env.py:109-110 */
+  double kneel_params[9];  /* reward_functions.py:71-81: target_height, min_height, max_roll_pitch,
+                              com_radius, energy_weight, posture_weight, com_weight, foot_weight,
+                              alive_weight */
+} hs_env_config;
+
+/* Device buffers of a batch (row-major, env-major).  Element type of the T* entries is float
+ * (HS_FP32) or double (HS_FP64). */
+typedef struct {
+  void* qpos;              /* [N][nq]  */
+  void* qvel;              /* [N][nv]  */
+  void* qacc_warmstart;    /* [N][nv]  */
+  void* ctrl;              /* [N][nu]  */
+  void* time;              /* [N]      */
+  int32_t* step_count;     /* [N]      */
+  uint32_t* episode;       /* [N]      */
+  void* total_reward;      /* [N]      */
+  int32_t* warning;        /* [N][HS_NWARN] */
+  void* obs;               /* [N][obs_dim]  custom_env.py:242-256 layout */
+  void* terminal_obs;      /* [N][obs_dim]  obs before auto-reset (SB3 info["terminal_observation"]) */
+  void* reward;            /* [N]      */
+  uint8_t* terminated;     /* [N]      */
+  uint8_t* truncated;      /* [N]      */
+  void* aux;               /* [N][HS_AUXDIM] */
+} hs_buffers;
+
+typedef struct {
+  int n_envs, precision, nq, nv, nu, nbody, obs_dim, elem_size;
+} hs_batch_info;
+
+hs_model* hs_model_load(const char* xml_path, char* err, int errsz);
+void hs_model_free(hs_model* m);
+int hs_model_field(const hs_model* m, const char* name, double* out, int n);
+
+/* external == NULL: the library allocates (hipMalloc) and owns the buffers.
+ * external != NULL: every pointer must be a device buffer of the documented size on `device`;
+ * the caller keeps ownership (used by the Python layer to hand in torch-allocated tensors). */
+hs_batch* hs_batch_create(const hs_model* m, int n_envs, int device, uint64_t seed, int precision,
+                          const hs_buffers* external);
+void hs_batch_destroy(hs_batch* b);
+int hs_batch_get_info(const hs_batch* b, hs_batch_info* out);
+int hs_get_buffers(const hs_batch* b, hs_buffers* out);
+int hs_set_config(hs_batch* b, const hs_env_config* cfg);
+int hs_get_config(const hs_batch* b, hs_env_config* cfg);
+
+/* mask: [N] uint8 device (NULL = all envs).  qpos_noise/qvel_noise: [N][nq]/[N][nv] device
+ * arrays of the batch precision with the reset noise (NULL = on-device counter RNG). */
+int hs_reset(hs_batch* b, const uint8_t* mask, const void* qpos_noise, const void* qvel_noise, void* stream);
+/* actions: [N][nu] float32 device. Runs frame_skip substeps, writes obs/reward/terminated/truncated. */
+int hs_step(hs_batch* b, const float* actions, void* stream);
+/* ctrl: [N][nu] float32 device (NULL = keep current ctrl).  nsub raw mj_step's, obs refreshed. */
+int hs_physics_step(hs_batch* b, const float* ctrl, int nsub, void* stream);
+
+/* Synchronous host<->device state copy in fp64.  dir 0: device -> host, 1: host -> device.
+ * Any pointer may be NULL.  Arrays are [N][nq], [N][nv], [N][nv], [N], [N][nu]. */
+int hs_state_io(hs_batch* b, int dir, double* qpos, double* qvel, double* qacc_warmstart, double* time,
+                double* ctrl);
+/* Stage dump of env 0 after its last substep (parity debugging); n >= 16384 doubles. */
+int hs_set_debug(hs_batch* b, int enable);
+int hs_get_debug(hs_batch* b, double* out, int n);
+int hs_synchronize(hs_batch* b);
+const char* hs_last_error(void);
+const char* hs_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

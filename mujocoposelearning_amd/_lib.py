@@ -1,0 +1,98 @@
+"""ctypes binding of the hsim C ABI (include/hsim.h).
+
+The native library is REQUIRED: importing this module raises if ``libhsim.so`` is missing
+(there is no CPU fallback in the product path -- the CPU restatement lives in ``oracle/``
+and is test infrastructure only).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libhsim.so")
+
+HS_FP32, HS_FP64 = 0, 1
+HS_REWARD_NONE, HS_REWARD_STAND, HS_REWARD_KNEELING, HS_REWARD_WALK = -1, 0, 1, 2
+HS_NWARN = 4
+HS_AUXDIM = 40
+DBGDIM = 16384
+
+
+class hs_env_config(C.Structure):
+    _fields_ = [("frame_skip", C.c_int), ("max_steps", C.c_int), ("reward_id", C.c_int), ("autoreset", C.c_int),
+                ("max_newton", C.c_int), ("reserved", C.c_int), ("duration", C.c_double),
+                ("init_height", C.c_double), ("noise_scale", C.c_double), ("kneel_params", C.c_double * 9)]
+
+
+class hs_buffers(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("qpos", "qvel", "qacc_warmstart", "ctrl", "time", "step_count", "episode",
+                                          "total_reward", "warning", "obs", "terminal_obs", "reward", "terminated",
+                                          "truncated", "aux")]
+
+
+class hs_batch_info(C.Structure):
+    _fields_ = [(n, C.c_int) for n in ("n_envs", "precision", "nq", "nv", "nu", "nbody", "obs_dim", "elem_size")]
+
+
+_LIB = None
+
+
+def lib():
+    """Load libhsim.so (build it with ``python -c 'import __graft_entry__ as g; g.build()'``)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"hsim native library not found at {LIB_PATH}; build it first "
+                          f"(make -C mujocoposelearning_amd/csrc)")
+    # Bind to the HIP runtime torch already loaded (same SONAME libamdhip64.so.7): one HIP
+    # runtime per process, so torch-allocated buffers and streams are valid in the library.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    L = C.CDLL(LIB_PATH)
+    vp, i, d, u64 = C.c_void_p, C.c_int, C.c_double, C.c_uint64
+    sig = {
+        "hs_model_load": (vp, [C.c_char_p, C.c_char_p, i]),
+        "hs_model_free": (None, [vp]),
+        "hs_model_field": (i, [vp, C.c_char_p, vp, i]),
+        "hs_batch_create": (vp, [vp, i, i, u64, i, vp]),
+        "hs_batch_destroy": (None, [vp]),
+        "hs_batch_get_info": (i, [vp, vp]),
+        "hs_get_buffers": (i, [vp, vp]),
+        "hs_set_config": (i, [vp, vp]),
+        "hs_get_config": (i, [vp, vp]),
+        "hs_reset": (i, [vp, vp, vp, vp, vp]),
+        "hs_step": (i, [vp, vp, vp]),
+        "hs_physics_step": (i, [vp, vp, i, vp]),
+        "hs_state_io": (i, [vp, i, vp, vp, vp, vp, vp]),
+        "hs_set_debug": (i, [vp, i]),
+        "hs_get_debug": (i, [vp, vp, i]),
+        "hs_synchronize": (i, [vp]),
+        "hs_last_error": (C.c_char_p, []),
+        "hs_version": (C.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = L
+    return L
+
+
+EXPORTED = ("hs_model_load", "hs_model_free", "hs_model_field", "hs_batch_create", "hs_batch_destroy",
+            "hs_batch_get_info", "hs_get_buffers", "hs_set_config", "hs_get_config", "hs_reset", "hs_step",
+            "hs_physics_step", "hs_state_io", "hs_set_debug", "hs_get_debug", "hs_synchronize", "hs_last_error",
+            "hs_version")
+
+
+class HsimError(RuntimeError):
+    pass
+
+
+def check(rc):
+    if rc is None or (isinstance(rc, int) and rc < 0):
+        raise HsimError(lib().hs_last_error().decode())
+    return rc

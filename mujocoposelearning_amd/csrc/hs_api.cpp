@@ -1,0 +1,346 @@
+// hsim C ABI implementation (product).  See include/hsim.h for the reference interfaces replaced.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/hsim.h"
+#include "hs_kernels.h"
+#include "mjcf.h"
+
+struct hs_model {
+  hs::HostModel host;
+};
+
+struct hs_batch {
+  const hs_model* model = nullptr;
+  int n = 0, device = 0, precision = HS_FP32, obs_dim = 0;
+  uint64_t seed = 0;
+  void* dmodel = nullptr;
+  hs_buffers buf{};
+  bool owns = false;
+  void* dbg = nullptr;
+  bool debug = false;
+  hs_env_config cfg{};
+};
+
+namespace {
+thread_local std::string g_err;
+
+int fail(const std::string& msg) {
+  g_err = msg;
+  return -1;
+}
+bool hip_ok(hipError_t e, const char* what) {
+  if (e == hipSuccess) return true;
+  g_err = std::string(what) + ": " + hipGetErrorString(e);
+  return false;
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+int obs_dim_of(const hs::HostModel& m) { return (m.nq - 2) + m.nv + 10 * m.nbody + 6 * m.nbody + m.nv; }
+
+template <typename T>
+hs::EnvBuffers<T> env_buffers(const hs_batch* b) {
+  hs::EnvBuffers<T> e;
+  e.qpos = (T*)b->buf.qpos;
+  e.qvel = (T*)b->buf.qvel;
+  e.qacc_ws = (T*)b->buf.qacc_warmstart;
+  e.ctrl = (T*)b->buf.ctrl;
+  e.time = (T*)b->buf.time;
+  e.step_count = b->buf.step_count;
+  e.episode = b->buf.episode;
+  e.total_reward = (T*)b->buf.total_reward;
+  e.warning = b->buf.warning;
+  e.obs = (T*)b->buf.obs;
+  e.terminal_obs = (T*)b->buf.terminal_obs;
+  e.reward = (T*)b->buf.reward;
+  e.terminated = b->buf.terminated;
+  e.truncated = b->buf.truncated;
+  e.aux = (T*)b->buf.aux;
+  e.dbg = b->debug ? (T*)b->dbg : nullptr;
+  return e;
+}
+
+hs::StepParams params_of(const hs_batch* b, int mode, int nsub) {
+  hs::StepParams p{};
+  p.mode = mode;
+  p.nsub = nsub;
+  p.max_steps = b->cfg.max_steps;
+  p.reward_id = b->cfg.reward_id;
+  p.autoreset = b->cfg.autoreset;
+  p.obs_dim = b->obs_dim;
+  p.max_newton = b->cfg.max_newton;
+  p.duration = b->cfg.duration;
+  p.init_height = b->cfg.init_height;
+  p.noise_scale = b->cfg.noise_scale;
+  p.seed = b->seed;
+  for (int k = 0; k < 9; k++) p.kneel[k] = b->cfg.kneel_params[k];
+  return p;
+}
+
+int launch(hs_batch* b, int mode, const float* act, const uint8_t* mask, const void* nq, const void* nvz, int nsub,
+           void* stream) {
+  if (!b) return fail("null batch");
+  DeviceGuard g(b->device);
+  hipError_t e;
+  auto p = params_of(b, mode, nsub);
+  int nv = b->model->host.nv;
+  if (b->precision == HS_FP64)
+    e = hs::launch_step<double>((const hs::DevModel<double>*)b->dmodel, nv, env_buffers<double>(b), act, mask,
+                                (const double*)nq, (const double*)nvz, p, b->n, (hipStream_t)stream);
+  else
+    e = hs::launch_step<float>((const hs::DevModel<float>*)b->dmodel, nv, env_buffers<float>(b), act, mask,
+                               (const float*)nq, (const float*)nvz, p, b->n, (hipStream_t)stream);
+  if (e == hipErrorInvalidValue) return fail("no kernel instance for this model's nv (compiled: nv = 27)");
+  return hip_ok(e, "step kernel launch") ? 0 : -1;
+}
+
+template <typename T>
+bool upload_model(hs_batch* b, std::string& err) {
+  auto* d = new hs::DevModel<T>();
+  if (!hs::build_dev_model<T>(b->model->host, *d, err)) { delete d; return false; }
+  if (!hip_ok(hipMalloc(&b->dmodel, sizeof(hs::DevModel<T>)), "hipMalloc(model)")) { delete d; err = g_err; return false; }
+  bool ok = hip_ok(hipMemcpy(b->dmodel, d, sizeof(hs::DevModel<T>), hipMemcpyHostToDevice), "upload model");
+  delete d;
+  if (!ok) err = g_err;
+  return ok;
+}
+
+template <typename T>
+bool init_state(hs_batch* b) {
+  const auto& m = b->model->host;
+  int N = b->n;
+  std::vector<T> q((size_t)N * m.nq);
+  for (int i = 0; i < N; i++)
+    for (int k = 0; k < m.nq; k++) q[(size_t)i * m.nq + k] = (T)m.qpos0[k];
+  size_t es = sizeof(T);
+  return hip_ok(hipMemcpy(b->buf.qpos, q.data(), q.size() * es, hipMemcpyHostToDevice), "init qpos") &&
+         hip_ok(hipMemset(b->buf.qvel, 0, (size_t)N * m.nv * es), "init") &&
+         hip_ok(hipMemset(b->buf.qacc_warmstart, 0, (size_t)N * m.nv * es), "init") &&
+         hip_ok(hipMemset(b->buf.ctrl, 0, (size_t)N * m.nu * es), "init") &&
+         hip_ok(hipMemset(b->buf.time, 0, (size_t)N * es), "init") &&
+         hip_ok(hipMemset(b->buf.step_count, 0, (size_t)N * 4), "init") &&
+         hip_ok(hipMemset(b->buf.episode, 0, (size_t)N * 4), "init") &&
+         hip_ok(hipMemset(b->buf.total_reward, 0, (size_t)N * es), "init") &&
+         hip_ok(hipMemset(b->buf.warning, 0, (size_t)N * HS_NWARN * 4), "init") &&
+         hip_ok(hipMemset(b->buf.obs, 0, (size_t)N * b->obs_dim * es), "init") &&
+         hip_ok(hipMemset(b->buf.terminal_obs, 0, (size_t)N * b->obs_dim * es), "init") &&
+         hip_ok(hipMemset(b->buf.reward, 0, (size_t)N * es), "init") &&
+         hip_ok(hipMemset(b->buf.terminated, 0, (size_t)N), "init") &&
+         hip_ok(hipMemset(b->buf.truncated, 0, (size_t)N), "init") &&
+         hip_ok(hipMemset(b->buf.aux, 0, (size_t)N * hs::AUXDIM * es), "init");
+}
+
+template <typename T>
+int state_io(hs_batch* b, int dir, double* qpos, double* qvel, double* warm, double* time, double* ctrl) {
+  const auto& m = b->model->host;
+  size_t N = (size_t)b->n;
+  struct Item { void* dev; double* host; size_t n; } items[] = {
+      {b->buf.qpos, qpos, N * m.nq}, {b->buf.qvel, qvel, N * m.nv}, {b->buf.qacc_warmstart, warm, N * m.nv},
+      {b->buf.time, time, N}, {b->buf.ctrl, ctrl, N * m.nu}};
+  for (auto& it : items) {
+    if (!it.host) continue;
+    std::vector<T> tmp(it.n);
+    if (dir == 0) {
+      if (!hip_ok(hipMemcpy(tmp.data(), it.dev, it.n * sizeof(T), hipMemcpyDeviceToHost), "state get")) return -1;
+      for (size_t k = 0; k < it.n; k++) it.host[k] = (double)tmp[k];
+    } else {
+      for (size_t k = 0; k < it.n; k++) tmp[k] = (T)it.host[k];
+      if (!hip_ok(hipMemcpy(it.dev, tmp.data(), it.n * sizeof(T), hipMemcpyHostToDevice), "state set")) return -1;
+    }
+  }
+  return 0;
+}
+}  // namespace
+
+extern "C" {
+
+const char* hs_last_error(void) { return g_err.c_str(); }
+const char* hs_version(void) { return "hsim 0.1.0 (gfx950)"; }
+
+hs_model* hs_model_load(const char* xml_path, char* err, int errsz) {
+  auto* m = new hs_model();
+  std::string e;
+  if (!xml_path || !hs::compile_mjcf_file(xml_path, m->host, e)) {
+    if (!xml_path) e = "null path";
+    g_err = e;
+    if (err && errsz > 0) { std::strncpy(err, e.c_str(), errsz - 1); err[errsz - 1] = 0; }
+    delete m;
+    return nullptr;
+  }
+  return m;
+}
+
+void hs_model_free(hs_model* m) { delete m; }
+
+int hs_model_field(const hs_model* m, const char* name, double* out, int n) {
+  if (!m || !name) return fail("null argument");
+  int r = hs::model_field(m->host, name, out, n);
+  if (r < 0) return fail(std::string("unknown model field '") + name + "'");
+  return r;
+}
+
+hs_batch* hs_batch_create(const hs_model* m, int n_envs, int device, uint64_t seed, int precision,
+                          const hs_buffers* external) {
+  if (!m || n_envs <= 0) { fail("hs_batch_create: null model or n_envs <= 0"); return nullptr; }
+  if (precision != HS_FP32 && precision != HS_FP64) { fail("precision must be HS_FP32 or HS_FP64"); return nullptr; }
+  int ndev = 0;
+  hipError_t de = hipGetDeviceCount(&ndev);
+  if (de != hipSuccess || ndev == 0) {
+    fail(std::string("no HIP device available (hipGetDeviceCount: ") + hipGetErrorString(de) + ", count " +
+         std::to_string(ndev) + ")");
+    return nullptr;
+  }
+  if (device < 0 || device >= ndev) { fail("device index out of range"); return nullptr; }
+  DeviceGuard g(device);
+  auto* b = new hs_batch();
+  b->model = m;
+  b->n = n_envs;
+  b->device = device;
+  b->seed = seed;
+  b->precision = precision;
+  b->obs_dim = obs_dim_of(m->host);
+  b->cfg.frame_skip = 5;
+  b->cfg.max_steps = 750;
+  b->cfg.reward_id = HS_REWARD_STAND;
+  b->cfg.autoreset = 1;
+  b->cfg.max_newton = 100;
+  b->cfg.duration = 15.0;
+  b->cfg.init_height = 1.282;
+  b->cfg.noise_scale = 0.01;
+  const double kneel[9] = {1.282, 0.85, 3.14159265358979323846 / 6, 0.1, 0.3, 0.3, 0.2, 0.1, 0.1};
+  std::memcpy(b->cfg.kneel_params, kneel, sizeof kneel);
+  std::string err;
+  bool ok = precision == HS_FP64 ? upload_model<double>(b, err) : upload_model<float>(b, err);
+  if (!ok) { g_err = err; delete b; return nullptr; }
+  size_t es = precision == HS_FP64 ? 8 : 4, N = (size_t)n_envs;
+  const auto& h = m->host;
+  if (external) {
+    b->buf = *external;
+    b->owns = false;
+  } else {
+    b->owns = true;
+    auto al = [&](void** p, size_t bytes) { return hip_ok(hipMalloc(p, bytes > 0 ? bytes : 4), "hipMalloc"); };
+    ok = al(&b->buf.qpos, N * h.nq * es) && al(&b->buf.qvel, N * h.nv * es) &&
+         al(&b->buf.qacc_warmstart, N * h.nv * es) && al(&b->buf.ctrl, N * h.nu * es) && al(&b->buf.time, N * es) &&
+         al((void**)&b->buf.step_count, N * 4) && al((void**)&b->buf.episode, N * 4) &&
+         al(&b->buf.total_reward, N * es) && al((void**)&b->buf.warning, N * HS_NWARN * 4) &&
+         al(&b->buf.obs, N * b->obs_dim * es) && al(&b->buf.terminal_obs, N * b->obs_dim * es) &&
+         al(&b->buf.reward, N * es) && al((void**)&b->buf.terminated, N) && al((void**)&b->buf.truncated, N) &&
+         al(&b->buf.aux, N * hs::AUXDIM * es);
+    if (!ok) { hs_batch_destroy(b); return nullptr; }
+  }
+  if (!hip_ok(hipMalloc(&b->dbg, hs::DBGDIM * 8), "hipMalloc(dbg)")) { hs_batch_destroy(b); return nullptr; }
+  ok = precision == HS_FP64 ? init_state<double>(b) : init_state<float>(b);
+  if (!ok) { hs_batch_destroy(b); return nullptr; }
+  return b;
+}
+
+void hs_batch_destroy(hs_batch* b) {
+  if (!b) return;
+  DeviceGuard g(b->device);
+  if (b->owns) {
+    void* ptrs[] = {b->buf.qpos, b->buf.qvel, b->buf.qacc_warmstart, b->buf.ctrl, b->buf.time, b->buf.step_count,
+                    b->buf.episode, b->buf.total_reward, b->buf.warning, b->buf.obs, b->buf.terminal_obs,
+                    b->buf.reward, b->buf.terminated, b->buf.truncated, b->buf.aux};
+    for (void* p : ptrs)
+      if (p) (void)hipFree(p);
+  }
+  if (b->dmodel) (void)hipFree(b->dmodel);
+  if (b->dbg) (void)hipFree(b->dbg);
+  delete b;
+}
+
+int hs_batch_get_info(const hs_batch* b, hs_batch_info* out) {
+  if (!b || !out) return fail("null argument");
+  const auto& h = b->model->host;
+  out->n_envs = b->n;
+  out->precision = b->precision;
+  out->nq = h.nq; out->nv = h.nv; out->nu = h.nu; out->nbody = h.nbody;
+  out->obs_dim = b->obs_dim;
+  out->elem_size = b->precision == HS_FP64 ? 8 : 4;
+  return 0;
+}
+
+int hs_get_buffers(const hs_batch* b, hs_buffers* out) {
+  if (!b || !out) return fail("null argument");
+  *out = b->buf;
+  return 0;
+}
+
+int hs_set_config(hs_batch* b, const hs_env_config* cfg) {
+  if (!b || !cfg) return fail("null argument");
+  if (cfg->frame_skip < 1) return fail("frame_skip must be >= 1");
+  if (cfg->max_newton < 1) return fail("max_newton must be >= 1");
+  if (cfg->reward_id < HS_REWARD_NONE || cfg->reward_id > HS_REWARD_WALK) return fail("unknown reward id");
+  b->cfg = *cfg;
+  return 0;
+}
+
+int hs_get_config(const hs_batch* b, hs_env_config* cfg) {
+  if (!b || !cfg) return fail("null argument");
+  *cfg = b->cfg;
+  return 0;
+}
+
+int hs_reset(hs_batch* b, const uint8_t* mask, const void* qpos_noise, const void* qvel_noise, void* stream) {
+  return launch(b, hs::MODE_RESET, nullptr, mask, qpos_noise, qvel_noise, 1, stream);
+}
+
+int hs_step(hs_batch* b, const float* actions, void* stream) {
+  if (!actions) return fail("hs_step: actions must not be NULL");
+  return launch(b, hs::MODE_ENV_STEP, actions, nullptr, nullptr, nullptr, b ? b->cfg.frame_skip : 1, stream);
+}
+
+int hs_physics_step(hs_batch* b, const float* ctrl, int nsub, void* stream) {
+  if (nsub < 1) return fail("nsub must be >= 1");
+  return launch(b, hs::MODE_PHYSICS, ctrl, nullptr, nullptr, nullptr, nsub, stream);
+}
+
+int hs_state_io(hs_batch* b, int dir, double* qpos, double* qvel, double* qacc_warmstart, double* time, double* ctrl) {
+  if (!b) return fail("null batch");
+  if (dir != 0 && dir != 1) return fail("dir must be 0 (get) or 1 (set)");
+  DeviceGuard g(b->device);
+  if (!hip_ok(hipDeviceSynchronize(), "sync")) return -1;
+  return b->precision == HS_FP64 ? state_io<double>(b, dir, qpos, qvel, qacc_warmstart, time, ctrl)
+                                 : state_io<float>(b, dir, qpos, qvel, qacc_warmstart, time, ctrl);
+}
+
+int hs_set_debug(hs_batch* b, int enable) {
+  if (!b) return fail("null batch");
+  b->debug = enable != 0;
+  return 0;
+}
+
+int hs_get_debug(hs_batch* b, double* out, int n) {
+  if (!b || !out) return fail("null argument");
+  if (n < hs::DBGDIM) return fail("debug buffer too small");
+  DeviceGuard g(b->device);
+  if (!hip_ok(hipDeviceSynchronize(), "sync")) return -1;
+  if (b->precision == HS_FP64) return hip_ok(hipMemcpy(out, b->dbg, hs::DBGDIM * 8, hipMemcpyDeviceToHost), "dbg") ? 0 : -1;
+  std::vector<float> t(hs::DBGDIM);
+  if (!hip_ok(hipMemcpy(t.data(), b->dbg, hs::DBGDIM * 4, hipMemcpyDeviceToHost), "dbg")) return -1;
+  for (int k = 0; k < hs::DBGDIM; k++) out[k] = t[k];
+  return 0;
+}
+
+int hs_synchronize(hs_batch* b) {
+  if (!b) return fail("null batch");
+  DeviceGuard g(b->device);
+  return hip_ok(hipDeviceSynchronize(), "hipDeviceSynchronize") ? 0 : -1;
+}
+
+}  // extern "C"

@@ -1,0 +1,62 @@
+// hsim device buffers and launch interface (product).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "hs_model.h"
+
+namespace hs {
+
+constexpr int AUXDIM = MAXDOF + 8;   // per env: qacc[nv], com[3], ncon, nefc, newton iters, solver flag
+constexpr int DBGDIM = 16384;        // stage dump (env 0 only) for parity debugging
+
+enum StepMode { MODE_ENV_STEP = 0, MODE_RESET = 1, MODE_PHYSICS = 2 };
+enum RewardId { REWARD_NONE = -1, REWARD_STAND = 0, REWARD_KNEELING = 1, REWARD_WALK = 2 };
+enum Warn { WARN_BADQPOS = 0, WARN_BADQVEL = 1, WARN_BADQACC = 2, WARN_OVERFLOW = 3, NWARN = 4 };
+
+template <typename T>
+struct EnvBuffers {
+  T* qpos;               // [N][nq]
+  T* qvel;               // [N][nv]
+  T* qacc_ws;            // [N][nv]  (mjData.qacc_warmstart)
+  T* ctrl;               // [N][nu]
+  T* time;               // [N]
+  int* step_count;       // [N]
+  uint32_t* episode;     // [N]      reset counter (device RNG stream)
+  T* total_reward;       // [N]
+  int* warning;          // [N][NWARN]
+  T* obs;                // [N][obs_dim]
+  T* terminal_obs;       // [N][obs_dim]  written for envs that auto-reset this step
+  T* reward;             // [N]
+  uint8_t* terminated;   // [N]
+  uint8_t* truncated;    // [N]
+  T* aux;                // [N][AUXDIM]
+  T* dbg;                // [DBGDIM] or nullptr
+};
+
+struct StepParams {
+  int mode;              // StepMode
+  int nsub;              // substeps per call (frame_skip for env steps, n for physics)
+  int max_steps;         // custom_env.py:201 truncation (750)
+  int reward_id;         // RewardId
+  int autoreset;         // SB3 VecEnv auto-reset semantics
+  int obs_dim;
+  int max_newton;        // Newton iteration cap
+  int reserved;
+  double duration;       // custom_env.py:213 (10.0 in training)
+  double init_height;    // custom_env.py:59 (1.282)
+  double noise_scale;    // custom_env.py:109-110 (0.01)
+  uint64_t seed;
+  double kneel[9];       // target_height, min_height, max_roll_pitch, com_radius, energy_w, posture_w,
+                         // com_w, foot_w, alive_w (reward_functions.py:71-81)
+};
+
+// actions: [N][nu] float32 (may be null in MODE_RESET); reset_mask: [N] (null = all);
+// noise_qpos/noise_qvel: [N][nq]/[N][nv] host-supplied reset noise (null = device RNG).
+template <typename T>
+hipError_t launch_step(const DevModel<T>* dmodel, int nv, const EnvBuffers<T>& b, const float* actions,
+                       const uint8_t* reset_mask, const T* noise_qpos, const T* noise_qvel,
+                       const StepParams& p, int nenv, hipStream_t stream);
+
+}  // namespace hs

@@ -1,0 +1,70 @@
+// hsim -- MI355X-native batched humanoid engine: compiled-model layout shared by the host
+// compiler (mjcf.cpp) and the HIP step kernel (hs_kernels.hip).
+//
+// Replaces the reference's `mujoco.MjModel.from_xml_path` product (custom_env.py:53): a
+// read-only model shared by every env of a batch.  The host compiler keeps an fp64
+// `HostModel`; the device gets a `DevModel<T>` (T = float for throughput, double for the
+// parity mode) plus derived topology tables (levels, chain/subtree bitmasks, static
+// collision pairs with pre-mixed contact parameters) that let one wavefront step one env.
+#pragma once
+#include <cstdint>
+
+namespace hs {
+
+// Engine capacity (compile time).  hs_batch_create rejects models that exceed it.
+constexpr int MAXBODY = 24;   // bodies incl. world
+constexpr int MAXDOF = 32;    // <= 32 so dof sets fit a 32-bit mask and one lane per dof
+constexpr int MAXQ = 40;
+constexpr int MAXJNT = 24;
+constexpr int MAXGEOM = 24;
+constexpr int MAXTEN = 4;
+constexpr int MAXWRAP = 4;    // joints per fixed tendon
+constexpr int MAXU = 24;
+constexpr int MAXPAIR = 192;  // static candidate geom pairs
+constexpr int MAXCON = 48;    // contacts per env (overflow counted in a warning word)
+constexpr int MAXEFC = 128;   // constraint rows per env (2 per lane)
+constexpr int MAXLEVEL = 16;
+
+enum GeomType { GEOM_PLANE = 0, GEOM_SPHERE = 2, GEOM_CAPSULE = 3 };
+enum JointType { JNT_FREE = 0, JNT_HINGE = 3 };
+enum PairFn { PAIR_PLANE_SPHERE = 0, PAIR_PLANE_CAPSULE = 1, PAIR_SPHERE_SPHERE = 2, PAIR_SPHERE_CAPSULE = 3,
+              PAIR_CAPSULE_CAPSULE = 4 };
+
+template <typename T>
+struct DevModel {
+  int nq, nv, nu, nbody, njnt, ngeom, ntendon, npair, nlevel, nhinge_limited;
+  T timestep, gravity[3];
+  T newton_scale;                     // 1 / (meaninertia * nv)  (MuJoCo solver scaling)
+  T total_mass;
+  int level_adr[MAXLEVEL + 1], level_body[MAXBODY];   // bodies grouped by tree depth
+  int body_parentid[MAXBODY], body_jntadr[MAXBODY], body_jntnum[MAXBODY];
+  int body_dofadr[MAXBODY], body_dofnum[MAXBODY];
+  uint32_t body_chainmask[MAXBODY];   // dofs on the path world -> body (incl. own)
+  uint32_t body_descmask[MAXBODY];    // bodies in the subtree rooted at body (incl. self)
+  T body_pos[MAXBODY][3], body_quat[MAXBODY][4], body_ipos[MAXBODY][3];
+  T body_inert[MAXBODY][6];           // inertia about COM in body frame: xx yy zz xy xz yz
+  T body_mass[MAXBODY], body_invweight_tran[MAXBODY];
+  int jnt_type[MAXJNT], jnt_qposadr[MAXJNT], jnt_dofadr[MAXJNT], jnt_bodyid[MAXJNT], jnt_limited[MAXJNT];
+  T jnt_pos[MAXJNT][3], jnt_axis[MAXJNT][3], jnt_range[MAXJNT][2];
+  T jnt_solref[MAXJNT][2], jnt_solimp[MAXJNT][5], jnt_margin[MAXJNT];
+  int dof_bodyid[MAXDOF], dof_jntid[MAXDOF], dof_qposadr[MAXDOF];   // qposadr: hinge dofs, else -1
+  uint32_t dof_ancmask[MAXDOF];       // dof ancestors incl. self (dof_parentid chain)
+  uint32_t dof_dotmask[MAXDOF];       // dofs whose motion precedes this dof in mj_comVel
+  T dof_armature[MAXDOF], dof_damping[MAXDOF], dof_invweight0[MAXDOF];
+  T dof_stiffness[MAXDOF], dof_springref[MAXDOF];
+  int dof_actuator[MAXDOF];           // motor driving this dof (-1 none)
+  int act_dof[MAXU], act_ctrllimited[MAXU];
+  T act_gear[MAXU], act_ctrlrange[MAXU][2];
+  int geom_type[MAXGEOM], geom_bodyid[MAXGEOM];
+  T geom_pos[MAXGEOM][3], geom_zaxis[MAXGEOM][3], geom_size[MAXGEOM][2];
+  // static candidate pairs, canonical (MuJoCo) processing order; g1 has the lower geom type
+  int pair_g1[MAXPAIR], pair_g2[MAXPAIR], pair_b1[MAXPAIR], pair_b2[MAXPAIR];
+  int pair_fn[MAXPAIR], pair_dim[MAXPAIR];
+  T pair_mu[MAXPAIR], pair_margin[MAXPAIR], pair_solref[MAXPAIR][2], pair_solimp[MAXPAIR][5];
+  int ten_nwrap[MAXTEN], ten_wrapdof[MAXTEN][MAXWRAP], ten_wrapqadr[MAXTEN][MAXWRAP], ten_limited[MAXTEN];
+  T ten_wrapcoef[MAXTEN][MAXWRAP], ten_range[MAXTEN][2], ten_solref[MAXTEN][2], ten_solimp[MAXTEN][5];
+  T ten_margin[MAXTEN], ten_invweight0[MAXTEN];
+  T qpos0[MAXQ];
+};
+
+}  // namespace hs

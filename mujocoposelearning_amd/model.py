@@ -1,0 +1,80 @@
+"""Compiled model handle -- the engine's counterpart of ``mujoco.MjModel``.
+
+``load_model(path)`` replaces ``mujoco.MjModel.from_xml_path`` (reference custom_env.py:53)
+and exposes MjModel-style attributes (``nq``, ``nv``, ``nu``, ``body_mass`` ...) read through
+the C ABI's ``hs_model_field``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._lib import HsimError, lib
+
+_INT_FIELDS = {"nq", "nv", "nu", "nbody", "njnt", "ngeom", "ntendon"}
+_SHAPES = {"body_pos": 3, "body_quat": 4, "body_ipos": 3, "body_iquat": 4, "body_inertia": 3,
+           "body_inertia_full": (3, 3), "body_invweight0": 2, "jnt_pos": 3, "jnt_axis": 3, "jnt_range": 2,
+           "jnt_solref": 2, "jnt_solimp": 5, "geom_size": 3, "geom_pos": 3, "geom_quat": 4,
+           "geom_friction": 3, "geom_solref": 2, "geom_solimp": 5, "tendon_range": 2, "actuator_ctrlrange": 2,
+           "collision_pairs": 2}
+
+
+class HsModel:
+    """Immutable compiled model (shareable across batches)."""
+
+    def __init__(self, path):
+        L = lib()
+        err = C.create_string_buffer(512)
+        h = L.hs_model_load(str(path).encode(), err, 512)
+        if not h:
+            raise HsimError(f"hs_model_load({path}): {err.value.decode()}")
+        self._h = h
+        self.path = str(path)
+        for k in _INT_FIELDS:
+            setattr(self, k, int(self.field(k)[0]))
+
+    @property
+    def handle(self):
+        return self._h
+
+    def field(self, name):
+        L = lib()
+        n = L.hs_model_field(self._h, name.encode(), None, 0)
+        if n < 0:
+            raise HsimError(L.hs_last_error().decode())
+        out = np.zeros(max(n, 1), np.float64)
+        L.hs_model_field(self._h, name.encode(), out.ctypes.data, n)
+        out = out[:n]
+        shp = _SHAPES.get(name)
+        if shp is not None:
+            out = out.reshape((-1,) + (shp if isinstance(shp, tuple) else (shp,)))
+        return out
+
+    def keyframe(self, name):
+        return self.field("key_" + name)
+
+    @property
+    def qpos0(self):
+        return self.field("qpos0")
+
+    def __getattr__(self, name):
+        if name.startswith("_"):
+            raise AttributeError(name)
+        try:
+            return self.field(name)
+        except HsimError:
+            raise AttributeError(name) from None
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            try:
+                lib().hs_model_free(h)
+            except Exception:
+                pass
+            self._h = None
+
+
+def load_model(path):
+    return HsModel(path)

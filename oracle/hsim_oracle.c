@@ -1,0 +1,837 @@
+/* ORACLE -- TEST INFRASTRUCTURE ONLY. Never linked into the product (mujocoposelearning_amd).
+ *
+ * Plain-C fp64 restatement of MuJoCo 3.2.5's mj_step for the model class used by the
+ * reference (XML/humanoid.xml: one free joint + hinges, capsule/sphere/plane geoms,
+ * fixed tendons, motors; Euler integrator, Newton solver, pyramidal cones, impratio 1).
+ *
+ * Reference call sites replaced: custom_env.py:121 and custom_env.py:160 (mujoco.mj_step),
+ * custom_env.py:102 (mujoco.mj_resetData).  MuJoCo 3.2.5 (environment.yml:152,204) is a
+ * third-party C library that is NOT present in this container, so every stage below is a
+ * restatement of its published pipeline (engine_forward.c / engine_core_smooth.c /
+ * engine_collision_*.c / engine_core_constraint.c / engine_solver.c semantics), and the
+ * result is "parity unpinned" against real mj_step.
+ *
+ * Solver note: MuJoCo's Newton solver minimises the convex primal
+ *   0.5 (a - a0)' M (a - a0) + sum_active 0.5 D (J a - aref)^2
+ * which has a unique minimiser; this oracle runs Newton with an EXACT piecewise-quadratic
+ * line search until the active set is stable, i.e. it returns that minimiser to fp64
+ * round-off (MuJoCo stops at tolerance 1e-8, a difference far below the parity tolerance).
+ */
+#include "hsim_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define MINVAL 1e-15
+#define MAXVAL 1e10
+#define MINIMP 0.0001
+#define MAXIMP 0.9999
+
+int orc_sizeof_model(void) { return (int)sizeof(OrcModel); }
+int orc_sizeof_data(void) { return (int)sizeof(OrcData); }
+
+/* ------------------------------------------------------------------ small vector algebra */
+static double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static void cross3(double* r, const double* a, const double* b) {
+  double t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2], t2 = a[0] * b[1] - a[1] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+static double normalize3(double* v) {
+  double n = sqrt(dot3(v, v));
+  if (n < MINVAL) { v[0] = 1; v[1] = 0; v[2] = 0; }
+  else { v[0] /= n; v[1] /= n; v[2] /= n; }
+  return n;
+}
+static double normalize4(double* q) {
+  double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  if (n < MINVAL) { q[0] = 1; q[1] = q[2] = q[3] = 0; }
+  else { q[0] /= n; q[1] /= n; q[2] /= n; q[3] /= n; }
+  return n;
+}
+static void mulquat(double* r, const double* a, const double* b) {
+  double t[4] = {a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3],
+                 a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2],
+                 a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1],
+                 a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0]};
+  memcpy(r, t, sizeof t);
+}
+static void quat2mat(double* R, const double* q) {
+  double w = q[0], x = q[1], y = q[2], z = q[3];
+  R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - w * z); R[2] = 2 * (x * z + w * y);
+  R[3] = 2 * (x * y + w * z); R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - w * x);
+  R[6] = 2 * (x * z - w * y); R[7] = 2 * (y * z + w * x); R[8] = 1 - 2 * (x * x + y * y);
+}
+static void matvec3(double* r, const double* R, const double* v) {
+  double t[3] = {R[0] * v[0] + R[1] * v[1] + R[2] * v[2], R[3] * v[0] + R[4] * v[1] + R[5] * v[2],
+                 R[6] * v[0] + R[7] * v[1] + R[8] * v[2]};
+  memcpy(r, t, sizeof t);
+}
+static void rotvecquat(double* r, const double* v, const double* q) {
+  double R[9]; quat2mat(R, q); matvec3(r, R, v);
+}
+static void axisangle2quat(double* q, const double* axis, double ang) {
+  double s = sin(0.5 * ang);
+  q[0] = cos(0.5 * ang); q[1] = axis[0] * s; q[2] = axis[1] * s; q[3] = axis[2] * s;
+}
+static int isbad(double x) { return x != x || x > MAXVAL || x < -MAXVAL; }
+
+/* spatial algebra, motion = (ang, lin), force = (torque, force); MuJoCo engine_util_spatial.c */
+static void mul_inert_vec(double* r, const double* i, const double* v) {
+  r[0] = i[0] * v[0] + i[3] * v[1] + i[4] * v[2] - i[8] * v[4] + i[7] * v[5];
+  r[1] = i[3] * v[0] + i[1] * v[1] + i[5] * v[2] + i[8] * v[3] - i[6] * v[5];
+  r[2] = i[4] * v[0] + i[5] * v[1] + i[2] * v[2] - i[7] * v[3] + i[6] * v[4];
+  r[3] = i[8] * v[1] - i[7] * v[2] + i[9] * v[3];
+  r[4] = i[6] * v[2] - i[8] * v[0] + i[9] * v[4];
+  r[5] = i[7] * v[0] - i[6] * v[1] + i[9] * v[5];
+}
+static void cross_motion(double* r, const double* v, const double* m) {
+  r[0] = -v[2] * m[1] + v[1] * m[2];
+  r[1] = v[2] * m[0] - v[0] * m[2];
+  r[2] = -v[1] * m[0] + v[0] * m[1];
+  r[3] = -v[2] * m[4] + v[1] * m[5] - v[5] * m[1] + v[4] * m[2];
+  r[4] = v[2] * m[3] - v[0] * m[5] + v[5] * m[0] - v[3] * m[2];
+  r[5] = -v[1] * m[3] + v[0] * m[4] - v[4] * m[0] + v[3] * m[1];
+}
+static void cross_force(double* r, const double* v, const double* f) {
+  r[0] = -v[2] * f[1] + v[1] * f[2] - v[5] * f[4] + v[4] * f[5];
+  r[1] = v[2] * f[0] - v[0] * f[2] + v[5] * f[3] - v[3] * f[5];
+  r[2] = -v[1] * f[0] + v[0] * f[1] - v[4] * f[3] + v[3] * f[4];
+  r[3] = -v[2] * f[4] + v[1] * f[5];
+  r[4] = v[2] * f[3] - v[0] * f[5];
+  r[5] = -v[1] * f[3] + v[0] * f[4];
+}
+
+/* dense Cholesky (lower) of n x n block of A (row stride OMAXV); returns 0 ok */
+static int chol(double L[OMAXV][OMAXV], const double A[OMAXV][OMAXV], int n) {
+  for (int j = 0; j < n; j++) {
+    double s = A[j][j];
+    for (int k = 0; k < j; k++) s -= L[j][k] * L[j][k];
+    if (s <= 0) return -1;
+    L[j][j] = sqrt(s);
+    for (int i = j + 1; i < n; i++) {
+      double t = A[i][j];
+      for (int k = 0; k < j; k++) t -= L[i][k] * L[j][k];
+      L[i][j] = t / L[j][j];
+    }
+    for (int i = 0; i < j; i++) L[i][j] = 0;
+  }
+  return 0;
+}
+static void chol_solve(double* x, double L[OMAXV][OMAXV], const double* b, int n) {
+  double y[OMAXV];
+  for (int i = 0; i < n; i++) {
+    double t = b[i];
+    for (int k = 0; k < i; k++) t -= L[i][k] * y[k];
+    y[i] = t / L[i][i];
+  }
+  for (int i = n - 1; i >= 0; i--) {
+    double t = y[i];
+    for (int k = i + 1; k < n; k++) t -= L[k][i] * x[k];
+    x[i] = t / L[i][i];
+  }
+}
+
+/* ------------------------------------------------------------------ mj_resetData */
+void orc_reset_data(const OrcModel* m, OrcData* d) {
+  memset(d, 0, sizeof(OrcData));
+  memcpy(d->qpos, m->qpos0, sizeof(double) * m->nq);
+}
+
+/* ------------------------------------------------------------------ mj_kinematics */
+static void kinematics(const OrcModel* m, OrcData* d) {
+  d->xquat[0][0] = 1; d->xmat[0][0] = d->xmat[0][4] = d->xmat[0][8] = 1;
+  for (int i = 1; i < m->nbody; i++) {
+    double xpos[3], xquat[4];
+    int ja = m->body_jntadr[i], jn = m->body_jntnum[i];
+    if (jn == 1 && m->jnt_type[ja] == 0) {        /* free joint: pose straight from qpos */
+      int qa = m->jnt_qposadr[ja];
+      memcpy(xpos, d->qpos + qa, 3 * sizeof(double));
+      memcpy(xquat, d->qpos + qa + 3, 4 * sizeof(double));
+      normalize4(xquat);
+      memcpy(d->xanchor[ja], xpos, 3 * sizeof(double));
+      memcpy(d->xaxis[ja], m->jnt_axis[ja], 3 * sizeof(double));
+    } else {
+      int p = m->body_parentid[i];
+      if (p) {
+        matvec3(xpos, d->xmat[p], m->body_pos[i]);
+        for (int k = 0; k < 3; k++) xpos[k] += d->xpos[p][k];
+        mulquat(xquat, d->xquat[p], m->body_quat[i]);
+      } else {
+        memcpy(xpos, m->body_pos[i], sizeof xpos);
+        memcpy(xquat, m->body_quat[i], sizeof xquat);
+      }
+      for (int j = ja; j < ja + jn; j++) {           /* hinges, applied in order */
+        double xaxis[3], xanchor[3], ql[4], v[3];
+        rotvecquat(xaxis, m->jnt_axis[j], xquat);
+        rotvecquat(xanchor, m->jnt_pos[j], xquat);
+        for (int k = 0; k < 3; k++) xanchor[k] += xpos[k];
+        int qa = m->jnt_qposadr[j];
+        axisangle2quat(ql, m->jnt_axis[j], d->qpos[qa] - m->qpos0[qa]);
+        mulquat(xquat, xquat, ql);
+        rotvecquat(v, m->jnt_pos[j], xquat);
+        for (int k = 0; k < 3; k++) xpos[k] = xanchor[k] - v[k];
+        memcpy(d->xanchor[j], xanchor, sizeof xanchor);
+        memcpy(d->xaxis[j], xaxis, sizeof xaxis);
+      }
+    }
+    normalize4(xquat);
+    memcpy(d->xquat[i], xquat, sizeof xquat);
+    memcpy(d->xpos[i], xpos, sizeof xpos);
+    quat2mat(d->xmat[i], xquat);
+  }
+  for (int i = 1; i < m->nbody; i++) {           /* inertial frame positions */
+    matvec3(d->xipos[i], d->xmat[i], m->body_ipos[i]);
+    for (int k = 0; k < 3; k++) d->xipos[i][k] += d->xpos[i][k];
+  }
+  for (int g = 0; g < m->ngeom; g++) {           /* geom frames (mj_local2Global) */
+    int b = m->geom_bodyid[g];
+    double q[4];
+    matvec3(d->geom_xpos[g], d->xmat[b], m->geom_pos[g]);
+    for (int k = 0; k < 3; k++) d->geom_xpos[g][k] += d->xpos[b][k];
+    mulquat(q, d->xquat[b], m->geom_quat[g]);
+    quat2mat(d->geom_xmat[g], q);
+  }
+}
+
+/* ------------------------------------------------------------------ mj_comPos */
+static void com_pos(const OrcModel* m, OrcData* d) {
+  int nb = m->nbody;
+  for (int i = 0; i < nb; i++)
+    for (int k = 0; k < 3; k++) d->subtree_com[i][k] = m->body_mass[i] * d->xipos[i][k];
+  for (int i = nb - 1; i > 0; i--)
+    for (int k = 0; k < 3; k++) d->subtree_com[m->body_parentid[i]][k] += d->subtree_com[i][k];
+  for (int i = 0; i < nb; i++) {
+    if (m->body_subtreemass[i] < MINVAL) memcpy(d->subtree_com[i], d->xipos[i], 3 * sizeof(double));
+    else for (int k = 0; k < 3; k++) d->subtree_com[i][k] /= m->body_subtreemass[i];
+  }
+  memset(d->cinert[0], 0, sizeof d->cinert[0]);
+  for (int i = 1; i < nb; i++) {                 /* mju_inertCom with the full body-frame tensor */
+    const double* R = d->xmat[i];
+    const double* I = m->body_inertia_full[i];
+    double T[9], Ic[9], dif[3], mass = m->body_mass[i];
+    for (int r = 0; r < 3; r++)
+      for (int c = 0; c < 3; c++) T[3 * r + c] = R[3 * r] * I[c] + R[3 * r + 1] * I[3 + c] + R[3 * r + 2] * I[6 + c];
+    for (int r = 0; r < 3; r++)
+      for (int c = 0; c < 3; c++) Ic[3 * r + c] = T[3 * r] * R[3 * c] + T[3 * r + 1] * R[3 * c + 1] + T[3 * r + 2] * R[3 * c + 2];
+    for (int k = 0; k < 3; k++) dif[k] = d->xipos[i][k] - d->subtree_com[m->body_rootid[i]][k];
+    double* ci = d->cinert[i];
+    ci[0] = Ic[0] + mass * (dif[1] * dif[1] + dif[2] * dif[2]);
+    ci[1] = Ic[4] + mass * (dif[0] * dif[0] + dif[2] * dif[2]);
+    ci[2] = Ic[8] + mass * (dif[0] * dif[0] + dif[1] * dif[1]);
+    ci[3] = Ic[1] - mass * dif[0] * dif[1];
+    ci[4] = Ic[2] - mass * dif[0] * dif[2];
+    ci[5] = Ic[5] - mass * dif[1] * dif[2];
+    ci[6] = mass * dif[0]; ci[7] = mass * dif[1]; ci[8] = mass * dif[2];
+    ci[9] = mass;
+  }
+  for (int j = 0; j < m->njnt; j++) {             /* com-based dof motion vectors */
+    int b = m->jnt_bodyid[j], da = m->jnt_dofadr[j];
+    double off[3];
+    for (int k = 0; k < 3; k++) off[k] = d->subtree_com[m->body_rootid[b]][k] - d->xanchor[j][k];
+    if (m->jnt_type[j] == 0) {
+      memset(d->cdof[da], 0, 18 * sizeof(double));
+      for (int i = 0; i < 3; i++) d->cdof[da + i][3 + i] = 1;
+      for (int i = 0; i < 3; i++) {
+        double ax[3] = {d->xmat[b][i], d->xmat[b][3 + i], d->xmat[b][6 + i]};
+        memcpy(d->cdof[da + 3 + i], ax, sizeof ax);
+        cross3(d->cdof[da + 3 + i] + 3, ax, off);
+      }
+    } else {
+      memcpy(d->cdof[da], d->xaxis[j], 3 * sizeof(double));
+      cross3(d->cdof[da] + 3, d->xaxis[j], off);
+    }
+  }
+}
+
+/* ------------------------------------------------------------------ mj_tendon (fixed) */
+static void tendon(const OrcModel* m, OrcData* d) {
+  for (int t = 0; t < m->ntendon; t++) {
+    d->ten_length[t] = 0;
+    memset(d->ten_J[t], 0, sizeof d->ten_J[t]);
+    for (int w = m->tendon_adr[t]; w < m->tendon_adr[t] + m->tendon_num[t]; w++) {
+      int j = m->wrap_jnt[w];
+      d->ten_length[t] += m->wrap_coef[w] * d->qpos[m->jnt_qposadr[j]];
+      d->ten_J[t][m->jnt_dofadr[j]] += m->wrap_coef[w];
+    }
+  }
+}
+
+/* ------------------------------------------------------------------ mj_crb (dense qM) */
+static void crb(const OrcModel* m, OrcData* d) {
+  int nv = m->nv;
+  memcpy(d->crb, d->cinert, sizeof(double) * 10 * m->nbody);
+  for (int i = m->nbody - 1; i > 0; i--)
+    if (m->body_parentid[i] > 0)
+      for (int k = 0; k < 10; k++) d->crb[m->body_parentid[i]][k] += d->crb[i][k];
+  memset(d->qM, 0, sizeof d->qM);
+  for (int i = 0; i < nv; i++) {
+    double buf[6];
+    mul_inert_vec(buf, d->crb[m->dof_bodyid[i]], d->cdof[i]);
+    for (int j = i; j >= 0; j = m->dof_parentid[j]) {
+      double v = 0;
+      for (int k = 0; k < 6; k++) v += d->cdof[j][k] * buf[k];
+      d->qM[i][j] += v;
+      if (j != i) d->qM[j][i] = d->qM[i][j];
+    }
+    d->qM[i][i] += m->dof_armature[i];
+  }
+}
+
+/* ------------------------------------------------------------------ collision (narrow phase) */
+static void make_frame(double* f) {              /* mju_makeFrame */
+  double t[3];
+  normalize3(f);
+  if (sqrt(dot3(f + 3, f + 3)) < 0.5) {
+    if (fabs(f[1]) < 0.5) { f[3] = 0; f[4] = 1; f[5] = 0; }
+    else { f[3] = 0; f[4] = 0; f[5] = 1; }
+  }
+  double s = dot3(f, f + 3);
+  for (int k = 0; k < 3; k++) t[k] = f[k] * s;
+  for (int k = 0; k < 3; k++) f[3 + k] -= t[k];
+  normalize3(f + 3);
+  cross3(f + 6, f, f + 3);
+}
+
+static int raw_plane_sphere(OrcContact* c, double margin, const double* pp, const double* pm,
+                            const double* sp, double r) {
+  double n[3] = {pm[2], pm[5], pm[8]}, tmp[3];
+  for (int k = 0; k < 3; k++) tmp[k] = sp[k] - pp[k];
+  double cd = dot3(tmp, n);
+  if (cd > margin + r) return 0;
+  c->dist = cd - r;
+  memcpy(c->frame, n, sizeof n);
+  for (int k = 0; k < 3; k++) c->pos[k] = sp[k] - n[k] * (c->dist / 2 + r);
+  c->frame[3] = c->frame[4] = c->frame[5] = 0;
+  return 1;
+}
+
+static int raw_sphere_sphere(OrcContact* c, double margin, const double* p1, double r1, const double* p2, double r2) {
+  double dif[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+  double dist = sqrt(dot3(dif, dif)) - r1 - r2;
+  if (dist > margin) return 0;
+  c->dist = dist;
+  memcpy(c->frame, dif, sizeof dif);
+  double len = normalize3(c->frame);
+  if (len < MINVAL) { c->frame[0] = 1; c->frame[1] = 0; c->frame[2] = 0; }
+  for (int k = 0; k < 3; k++) c->pos[k] = p1[k] + c->frame[k] * (r1 + dist / 2);
+  c->frame[3] = c->frame[4] = c->frame[5] = 0;
+  return 1;
+}
+
+static int col_plane_sphere(const OrcModel* m, const OrcData* d, OrcContact* c, int g1, int g2, double mg) {
+  return raw_plane_sphere(c, mg, d->geom_xpos[g1], d->geom_xmat[g1], d->geom_xpos[g2], m->geom_size[g2][0]);
+}
+
+static int col_plane_capsule(const OrcModel* m, const OrcData* d, OrcContact* c, int g1, int g2, double mg) {
+  const double* mat2 = d->geom_xmat[g2];
+  double axis[3] = {mat2[2], mat2[5], mat2[8]}, p[3];
+  double hl = m->geom_size[g2][1], r = m->geom_size[g2][0];
+  for (int k = 0; k < 3; k++) p[k] = d->geom_xpos[g2][k] + hl * axis[k];
+  int n1 = raw_plane_sphere(c, mg, d->geom_xpos[g1], d->geom_xmat[g1], p, r);
+  for (int k = 0; k < 3; k++) p[k] = d->geom_xpos[g2][k] - hl * axis[k];
+  int n2 = raw_plane_sphere(c + n1, mg, d->geom_xpos[g1], d->geom_xmat[g1], p, r);
+  if (n1) memcpy(c->frame + 3, axis, sizeof axis);
+  if (n2) memcpy((c + n1)->frame + 3, axis, sizeof axis);
+  return n1 + n2;
+}
+
+static int col_sphere_sphere(const OrcModel* m, const OrcData* d, OrcContact* c, int g1, int g2, double mg) {
+  return raw_sphere_sphere(c, mg, d->geom_xpos[g1], m->geom_size[g1][0], d->geom_xpos[g2], m->geom_size[g2][0]);
+}
+
+static int col_sphere_capsule(const OrcModel* m, const OrcData* d, OrcContact* c, int g1, int g2, double mg) {
+  const double* mat2 = d->geom_xmat[g2];
+  double axis[3] = {mat2[2], mat2[5], mat2[8]}, dif[3], v[3];
+  double hl = m->geom_size[g2][1];
+  for (int k = 0; k < 3; k++) dif[k] = d->geom_xpos[g1][k] - d->geom_xpos[g2][k];
+  double x = dot3(axis, dif);
+  if (x > hl) x = hl; else if (x < -hl) x = -hl;
+  for (int k = 0; k < 3; k++) v[k] = d->geom_xpos[g2][k] + x * axis[k];
+  return raw_sphere_sphere(c, mg, d->geom_xpos[g1], m->geom_size[g1][0], v, m->geom_size[g2][0]);
+}
+
+static int col_capsule_capsule(const OrcModel* m, const OrcData* d, OrcContact* c, int g1, int g2, double mg) {
+  const double *p1 = d->geom_xpos[g1], *p2 = d->geom_xpos[g2], *m1 = d->geom_xmat[g1], *m2 = d->geom_xmat[g2];
+  double s1 = m->geom_size[g1][1], s2 = m->geom_size[g2][1], r1 = m->geom_size[g1][0], r2 = m->geom_size[g2][0];
+  double a1[3] = {m1[2] * s1, m1[5] * s1, m1[8] * s1}, a2[3] = {m2[2] * s2, m2[5] * s2, m2[8] * s2};
+  double dif[3] = {p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2]}, v1[3], v2[3];
+  double ma = dot3(a1, a1), mb = -dot3(a1, a2), mc = dot3(a2, a2), u = -dot3(a1, dif), v = dot3(a2, dif);
+  double det = ma * mc - mb * mb;
+  if (fabs(det) >= MINVAL) {
+    double x1 = (mc * u - mb * v) / det, x2 = (ma * v - mb * u) / det;
+    if (x1 > 1) { x1 = 1; x2 = (v - mb) / mc; }
+    else if (x1 < -1) { x1 = -1; x2 = (v + mb) / mc; }
+    if (x2 > 1) { x2 = 1; x1 = (u - mb) / ma; if (x1 > 1) x1 = 1; else if (x1 < -1) x1 = -1; }
+    else if (x2 < -1) { x2 = -1; x1 = (u + mb) / ma; if (x1 > 1) x1 = 1; else if (x1 < -1) x1 = -1; }
+    for (int k = 0; k < 3; k++) { v1[k] = p1[k] + x1 * a1[k]; v2[k] = p2[k] + x2 * a2[k]; }
+    return raw_sphere_sphere(c, mg, v1, r1, v2, r2);
+  }
+  /* parallel axes: end of capsule 1 at +1 and -1, projected onto capsule 2 */
+  int n = 0;
+  for (int side = 1; side >= -1; side -= 2) {
+    double x2 = (v - side * mb) / mc;
+    if (x2 > 1) x2 = 1; else if (x2 < -1) x2 = -1;
+    for (int k = 0; k < 3; k++) { v1[k] = p1[k] + side * a1[k]; v2[k] = p2[k] + x2 * a2[k]; }
+    n += raw_sphere_sphere(c + n, mg, v1, r1, v2, r2);
+  }
+  return n;
+}
+
+/* mj_contactParam: mix geom parameters (equal priority branch) */
+static void contact_param(const OrcModel* m, OrcContact* c, int g1, int g2) {
+  double fr[3];
+  if (m->geom_priority[g1] != m->geom_priority[g2]) {
+    int g = m->geom_priority[g1] > m->geom_priority[g2] ? g1 : g2;
+    c->dim = m->geom_condim[g];
+    memcpy(fr, m->geom_friction[g], sizeof fr);
+    memcpy(c->solref, m->geom_solref[g], sizeof c->solref);
+    memcpy(c->solimp, m->geom_solimp[g], sizeof c->solimp);
+  } else {
+    c->dim = m->geom_condim[g1] > m->geom_condim[g2] ? m->geom_condim[g1] : m->geom_condim[g2];
+    for (int k = 0; k < 3; k++) fr[k] = fmax(m->geom_friction[g1][k], m->geom_friction[g2][k]);
+    double s1 = m->geom_solmix[g1], s2 = m->geom_solmix[g2], mix;
+    if (s1 >= MINVAL && s2 >= MINVAL) mix = s1 / (s1 + s2);
+    else if (s1 < MINVAL && s2 < MINVAL) mix = 0.5;
+    else mix = s1 < MINVAL ? 0.0 : 1.0;
+    if (m->geom_solref[g1][0] > 0 && m->geom_solref[g2][0] > 0)
+      for (int k = 0; k < 2; k++) c->solref[k] = mix * m->geom_solref[g1][k] + (1 - mix) * m->geom_solref[g2][k];
+    else
+      for (int k = 0; k < 2; k++) c->solref[k] = fmin(m->geom_solref[g1][k], m->geom_solref[g2][k]);
+    for (int k = 0; k < 5; k++) c->solimp[k] = mix * m->geom_solimp[g1][k] + (1 - mix) * m->geom_solimp[g2][k];
+  }
+  c->friction[0] = fr[0]; c->friction[1] = fr[0]; c->friction[2] = fr[1];
+  c->friction[3] = fr[2]; c->friction[4] = fr[2];
+  double margin = fmax(m->geom_margin[g1], m->geom_margin[g2]);
+  double gap = fmax(m->geom_gap[g1], m->geom_gap[g2]);
+  c->includemargin = margin - gap;
+}
+
+static void collision(const OrcModel* m, OrcData* d) {
+  d->ncon = 0;
+  for (int p = 0; p < m->npair; p++) {
+    int g1 = m->pair_geom[p][0], g2 = m->pair_geom[p][1];
+    if (m->geom_type[g1] > m->geom_type[g2]) { int t = g1; g1 = g2; g2 = t; }
+    double margin = fmax(m->geom_margin[g1], m->geom_margin[g2]);
+    int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
+    if (t1 != 0) {                                  /* bounding-sphere early out (not planes) */
+      double dif[3] = {d->geom_xpos[g1][0] - d->geom_xpos[g2][0], d->geom_xpos[g1][1] - d->geom_xpos[g2][1],
+                       d->geom_xpos[g1][2] - d->geom_xpos[g2][2]};
+      if (sqrt(dot3(dif, dif)) > margin + m->geom_rbound[g1] + m->geom_rbound[g2]) continue;
+    }
+    OrcContact tmp[4];
+    memset(tmp, 0, sizeof tmp);
+    int n = 0;
+    if (t1 == 0 && t2 == 2) n = col_plane_sphere(m, d, tmp, g1, g2, margin);
+    else if (t1 == 0 && t2 == 3) n = col_plane_capsule(m, d, tmp, g1, g2, margin);
+    else if (t1 == 2 && t2 == 2) n = col_sphere_sphere(m, d, tmp, g1, g2, margin);
+    else if (t1 == 2 && t2 == 3) n = col_sphere_capsule(m, d, tmp, g1, g2, margin);
+    else if (t1 == 3 && t2 == 3) n = col_capsule_capsule(m, d, tmp, g1, g2, margin);
+    for (int k = 0; k < n; k++) {
+      if (d->ncon >= OMAXCON) { d->warning_overflow++; return; }
+      OrcContact* c = d->contact + d->ncon++;
+      *c = tmp[k];
+      c->geom[0] = g1; c->geom[1] = g2;
+      make_frame(c->frame);
+      contact_param(m, c, g1, g2);
+    }
+  }
+}
+
+/* ------------------------------------------------------------------ constraints */
+/* translational Jacobian of point p attached to body b (mj_jac) */
+static void jac_point(const OrcModel* m, const OrcData* d, double jp[3][OMAXV], int b, const double* p) {
+  for (int k = 0; k < 3; k++) memset(jp[k], 0, sizeof(double) * m->nv);
+  if (b == 0) return;
+  double off[3];
+  for (int k = 0; k < 3; k++) off[k] = p[k] - d->subtree_com[m->body_rootid[b]][k];
+  int dof = -1;                                   /* last dof of nearest body with dofs */
+  for (int bb = b; bb > 0 && dof < 0; bb = m->body_parentid[bb])
+    if (m->body_dofnum[bb]) dof = m->body_dofadr[bb] + m->body_dofnum[bb] - 1;
+  for (; dof >= 0; dof = m->dof_parentid[dof]) {
+    double t[3];
+    cross3(t, d->cdof[dof], off);
+    for (int k = 0; k < 3; k++) jp[k][dof] = d->cdof[dof][3 + k] + t[k];
+  }
+}
+
+static void getimpedance(const double* si, double pos, double margin, double* imp, double* impP) {
+  double s0 = fmin(MAXIMP, fmax(MINIMP, si[0])), s1 = fmin(MAXIMP, fmax(MINIMP, si[1]));
+  if (s0 == s1 || si[2] <= MINVAL) { *imp = 0.5 * (s0 + s1); *impP = 0; return; }
+  double x = (pos - margin) / si[2], sgn = 1;
+  if (x < 0) { x = -x; sgn = -1; }
+  if (x >= 1 || x <= 0) { *imp = (x >= 1 ? s1 : s0); *impP = 0; return; }
+  double y, yP;
+  if (si[4] == 1) { y = x; yP = 1; }
+  else if (x <= si[3]) {
+    double a = 1 / pow(si[3], si[4] - 1);
+    y = a * pow(x, si[4]); yP = si[4] * a * pow(x, si[4] - 1);
+  } else {
+    double b = 1 / pow(1 - si[3], si[4] - 1);
+    y = 1 - b * pow(1 - x, si[4]); yP = si[4] * b * pow(1 - x, si[4] - 1);
+  }
+  *imp = s0 + y * (s1 - s0);
+  *impP = yP * sgn * (s1 - s0) / si[2];
+}
+
+static int add_row(const OrcModel* m, OrcData* d, const double* J, double pos, double margin, int type, int id) {
+  if (d->nefc >= OMAXEFC) { d->warning_overflow++; return -1; }
+  int r = d->nefc++;
+  memcpy(d->efc_J[r], J, sizeof(double) * m->nv);
+  d->efc_pos[r] = pos; d->efc_margin[r] = margin; d->efc_type[r] = type; d->efc_id[r] = id;
+  return r;
+}
+
+/* mj_makeConstraint + mj_diagApprox + mj_makeImpedance (position-dependent part) */
+static void make_constraint(const OrcModel* m, OrcData* d) {
+  int nv = m->nv;
+  double J[OMAXV];
+  d->nefc = 0;
+  for (int j = 0; j < m->njnt; j++) {            /* joint limits */
+    if (!m->jnt_limited[j] || m->jnt_type[j] != 3) continue;
+    double q = d->qpos[m->jnt_qposadr[j]];
+    for (int side = -1; side <= 1; side += 2) {
+      double dist = side * (m->jnt_range[j][(side + 1) / 2] - q);
+      if (dist < m->jnt_margin[j]) {
+        memset(J, 0, sizeof(double) * nv);
+        J[m->jnt_dofadr[j]] = -side;
+        int r = add_row(m, d, J, dist, m->jnt_margin[j], ORC_LIMIT_JOINT, j);
+        if (r >= 0) d->efc_diagApprox[r] = m->dof_invweight0[m->jnt_dofadr[j]];
+      }
+    }
+  }
+  for (int t = 0; t < m->ntendon; t++) {         /* tendon limits */
+    if (!m->tendon_limited[t]) continue;
+    double L = d->ten_length[t];
+    for (int side = -1; side <= 1; side += 2) {
+      double dist = side * (m->tendon_range[t][(side + 1) / 2] - L);
+      if (dist < m->tendon_margin[t]) {
+        for (int k = 0; k < nv; k++) J[k] = -side * d->ten_J[t][k];
+        int r = add_row(m, d, J, dist, m->tendon_margin[t], ORC_LIMIT_TENDON, t);
+        if (r >= 0) d->efc_diagApprox[r] = m->tendon_invweight0[t];
+      }
+    }
+  }
+  for (int ci = 0; ci < d->ncon; ci++) {          /* contacts */
+    OrcContact* c = d->contact + ci;
+    int b1 = m->geom_bodyid[c->geom[0]], b2 = m->geom_bodyid[c->geom[1]];
+    double j1[3][OMAXV], j2[3][OMAXV], jc[3][OMAXV];
+    jac_point(m, d, j1, b1, c->pos);
+    jac_point(m, d, j2, b2, c->pos);
+    for (int r = 0; r < 3; r++)
+      for (int k = 0; k < nv; k++)
+        jc[r][k] = c->frame[3 * r] * (j2[0][k] - j1[0][k]) + c->frame[3 * r + 1] * (j2[1][k] - j1[1][k]) +
+                   c->frame[3 * r + 2] * (j2[2][k] - j1[2][k]);
+    double tran = m->body_invweight0[b1][0] + m->body_invweight0[b2][0];
+    c->efc_address = d->nefc;
+    if (c->dim == 1) {
+      int r = add_row(m, d, jc[0], c->dist, c->includemargin, ORC_CONTACT_FRICTIONLESS, ci);
+      if (r >= 0) d->efc_diagApprox[r] = tran;
+    } else {
+      for (int k = 1; k < c->dim && k < 3; k++) {
+        double mu = c->friction[k - 1];
+        for (int sgn = 1; sgn >= -1; sgn -= 2) {
+          for (int q = 0; q < nv; q++) J[q] = jc[0][q] + sgn * mu * jc[k][q];
+          int r = add_row(m, d, J, c->dist, c->includemargin, ORC_CONTACT_PYRAMIDAL, ci);
+          if (r >= 0) d->efc_diagApprox[r] = tran + mu * mu * tran;
+        }
+      }
+    }
+  }
+  /* impedance, R, D, K/B (mj_makeImpedance) */
+  for (int r = 0; r < d->nefc; r++) {
+    const double *sr, *si;
+    int id = d->efc_id[r];
+    if (d->efc_type[r] == ORC_LIMIT_JOINT) { sr = m->jnt_solref[id]; si = m->jnt_solimp[id]; }
+    else if (d->efc_type[r] == ORC_LIMIT_TENDON) { sr = m->tendon_solref[id]; si = m->tendon_solimp[id]; }
+    else { sr = d->contact[id].solref; si = d->contact[id].solimp; }
+    double imp, impP;
+    getimpedance(si, d->efc_pos[r], d->efc_margin[r], &imp, &impP);
+    double dmax = fmin(MAXIMP, fmax(MINIMP, si[1]));
+    double K, B;
+    if (sr[0] > 0) {
+      double tc = fmax(sr[0], 2 * m->timestep), dr = sr[1];
+      K = 1 / (dmax * dmax * tc * tc * dr * dr);
+      B = 2 / (dmax * tc);
+    } else {
+      K = -sr[0] / (dmax * dmax);
+      B = -sr[1] / dmax;
+    }
+    d->efc_KBIP[r][0] = K; d->efc_KBIP[r][1] = B; d->efc_KBIP[r][2] = imp; d->efc_KBIP[r][3] = impP;
+    d->efc_R[r] = fmax(MINVAL, (1 - imp) * d->efc_diagApprox[r] / imp);
+    d->efc_D[r] = 1 / d->efc_R[r];
+  }
+}
+
+/* ------------------------------------------------------------------ velocity stage */
+static void com_vel(const OrcModel* m, OrcData* d) {
+  memset(d->cvel[0], 0, sizeof d->cvel[0]);
+  for (int i = 1; i < m->nbody; i++) {
+    double cvel[6], tmp[6];
+    memcpy(cvel, d->cvel[m->body_parentid[i]], sizeof cvel);
+    int da = m->body_dofadr[i];
+    for (int j = 0; j < m->body_dofnum[i]; j++) {
+      int dof = da + j;
+      if (m->jnt_type[m->dof_jntid[dof]] == 0) {
+        for (int k = 0; k < 3; k++) memset(d->cdof_dot[dof + k], 0, sizeof d->cdof_dot[0]);
+        for (int k = 0; k < 3; k++)
+          for (int q = 0; q < 6; q++) cvel[q] += d->cdof[dof + k][q] * d->qvel[dof + k];
+        for (int k = 0; k < 3; k++) cross_motion(d->cdof_dot[dof + 3 + k], cvel, d->cdof[dof + 3 + k]);
+        for (int k = 0; k < 3; k++)
+          for (int q = 0; q < 6; q++) cvel[q] += d->cdof[dof + 3 + k][q] * d->qvel[dof + 3 + k];
+        j += 5;
+      } else {
+        cross_motion(d->cdof_dot[dof], cvel, d->cdof[dof]);
+        for (int q = 0; q < 6; q++) tmp[q] = d->cdof[dof][q] * d->qvel[dof];
+        for (int q = 0; q < 6; q++) cvel[q] += tmp[q];
+      }
+    }
+    memcpy(d->cvel[i], cvel, sizeof cvel);
+  }
+}
+
+static void passive(const OrcModel* m, OrcData* d) {
+  memset(d->qfrc_passive, 0, sizeof(double) * m->nv);
+  for (int j = 0; j < m->njnt; j++) {
+    if (m->jnt_type[j] != 3) continue;           /* free joint has stiffness 0 */
+    int qa = m->jnt_qposadr[j], da = m->jnt_dofadr[j];
+    d->qfrc_passive[da] -= m->jnt_stiffness[j] * (d->qpos[qa] - m->qpos_spring[qa]);
+  }
+  for (int i = 0; i < m->nv; i++) d->qfrc_passive[i] -= m->dof_damping[i] * d->qvel[i];
+}
+
+static void reference_constraint(const OrcModel* m, OrcData* d) {
+  for (int r = 0; r < d->nefc; r++) {
+    double v = 0;
+    for (int k = 0; k < m->nv; k++) v += d->efc_J[r][k] * d->qvel[k];
+    d->efc_vel[r] = v;
+    d->efc_aref[r] = -d->efc_KBIP[r][1] * v - d->efc_KBIP[r][0] * d->efc_KBIP[r][2] * (d->efc_pos[r] - d->efc_margin[r]);
+  }
+}
+
+static void rne(const OrcModel* m, OrcData* d) {
+  double cacc[OMAXB][6], cfrc[OMAXB][6], tmp[6], tmp1[6];
+  memset(cacc[0], 0, sizeof cacc[0]);
+  for (int k = 0; k < 3; k++) cacc[0][3 + k] = -m->gravity[k];
+  for (int i = 1; i < m->nbody; i++) {
+    int da = m->body_dofadr[i];
+    memcpy(cacc[i], cacc[m->body_parentid[i]], sizeof cacc[i]);
+    for (int j = 0; j < m->body_dofnum[i]; j++)
+      for (int q = 0; q < 6; q++) cacc[i][q] += d->cdof_dot[da + j][q] * d->qvel[da + j];
+    mul_inert_vec(cfrc[i], d->cinert[i], cacc[i]);
+    mul_inert_vec(tmp, d->cinert[i], d->cvel[i]);
+    cross_force(tmp1, d->cvel[i], tmp);
+    for (int q = 0; q < 6; q++) cfrc[i][q] += tmp1[q];
+  }
+  memset(cfrc[0], 0, sizeof cfrc[0]);
+  for (int i = m->nbody - 1; i > 0; i--)
+    if (m->body_parentid[i])
+      for (int q = 0; q < 6; q++) cfrc[m->body_parentid[i]][q] += cfrc[i][q];
+  for (int i = 0; i < m->nv; i++) {
+    double v = 0;
+    for (int q = 0; q < 6; q++) v += d->cdof[i][q] * cfrc[m->dof_bodyid[i]][q];
+    d->qfrc_bias[i] = v;
+  }
+}
+
+static void actuation(const OrcModel* m, OrcData* d) {
+  memset(d->qfrc_actuator, 0, sizeof(double) * m->nv);
+  for (int u = 0; u < m->nu; u++) {
+    double c = d->ctrl[u];
+    if (m->actuator_ctrllimited[u]) c = fmin(m->actuator_ctrlrange[u][1], fmax(m->actuator_ctrlrange[u][0], c));
+    d->actuator_force[u] = c;                       /* motor: gain 1, bias 0 */
+    d->qfrc_actuator[m->jnt_dofadr[m->actuator_trnid[u]]] += m->actuator_gear[u] * c;
+  }
+}
+
+/* ------------------------------------------------------------------ Newton solver */
+static double eval_cost(const OrcModel* m, const OrcData* d, const double* x, double* jar) {
+  int nv = m->nv;
+  double dx[OMAXV], c = 0;
+  for (int i = 0; i < nv; i++) dx[i] = x[i] - d->qacc_smooth[i];
+  for (int i = 0; i < nv; i++) {
+    double t = 0;
+    for (int k = 0; k < nv; k++) t += d->qM[i][k] * dx[k];
+    c += 0.5 * dx[i] * t;
+  }
+  for (int r = 0; r < d->nefc; r++) {
+    double v = -d->efc_aref[r];
+    for (int k = 0; k < nv; k++) v += d->efc_J[r][k] * x[k];
+    jar[r] = v;
+    if (v < 0) c += 0.5 * d->efc_D[r] * v * v;
+  }
+  return c;
+}
+
+static int cmp_double(const void* a, const void* b) {
+  double x = *(const double*)a, y = *(const double*)b;
+  return x < y ? -1 : (x > y ? 1 : 0);
+}
+
+/* exact minimiser along s of the convex piecewise quadratic (breakpoint walk) */
+static double line_search(const OrcModel* m, const OrcData* d, const double* x, const double* s,
+                          const double* jar, double* Js) {
+  int nv = m->nv, ne = d->nefc;
+  double Ms[OMAXV], A0 = 0, B0 = 0, bp[OMAXEFC];
+  for (int i = 0; i < nv; i++) {
+    double t = 0;
+    for (int k = 0; k < nv; k++) t += d->qM[i][k] * s[k];
+    Ms[i] = t;
+  }
+  for (int i = 0; i < nv; i++) { A0 += s[i] * Ms[i]; B0 += (x[i] - d->qacc_smooth[i]) * Ms[i]; }
+  int nb = 0;
+  for (int r = 0; r < ne; r++) {
+    double v = 0;
+    for (int k = 0; k < nv; k++) v += d->efc_J[r][k] * s[k];
+    Js[r] = v;
+    if (v != 0) { double t = -jar[r] / v; if (t > 0) bp[nb++] = t; }
+  }
+  qsort(bp, nb, sizeof(double), cmp_double);
+  double lo = 0;
+  for (int k = 0; k <= nb; k++) {
+    double hi = k < nb ? bp[k] : INFINITY;
+    double mid = k < nb ? 0.5 * (lo + hi) : lo + 1.0;
+    double A = A0, B = B0;
+    for (int r = 0; r < ne; r++)
+      if (jar[r] + mid * Js[r] < 0) { A += d->efc_D[r] * Js[r] * Js[r]; B += d->efc_D[r] * jar[r] * Js[r]; }
+    if (A <= 0) return 0;
+    double root = -B / A;
+    if (root <= hi) return root > lo ? root : lo;
+    lo = hi;
+  }
+  return lo;
+}
+
+static void solve_newton(const OrcModel* m, OrcData* d) {
+  int nv = m->nv, ne = d->nefc;
+  double x[OMAXV], jar[OMAXEFC], Js[OMAXEFC], g[OMAXV], s[OMAXV];
+  static double H[OMAXV][OMAXV], L[OMAXV][OMAXV];
+  double cw = eval_cost(m, d, d->qacc_warmstart, jar);
+  double cs = eval_cost(m, d, d->qacc_smooth, jar);
+  memcpy(x, cs < cw ? d->qacc_smooth : d->qacc_warmstart, sizeof(double) * nv);
+  double cost = eval_cost(m, d, x, jar);
+  double scale = 1.0 / (m->meaninertia * (nv > 1 ? nv : 1));
+  int it;
+  for (it = 0; it < m->iterations; it++) {
+    unsigned char act[OMAXEFC];
+    for (int r = 0; r < ne; r++) act[r] = jar[r] < 0;
+    /* gradient and Hessian */
+    for (int i = 0; i < nv; i++) {
+      double t = 0;
+      for (int k = 0; k < nv; k++) t += d->qM[i][k] * (x[k] - d->qacc_smooth[k]);
+      g[i] = t;
+    }
+    memcpy(H, d->qM, sizeof H);
+    for (int r = 0; r < ne; r++) {
+      if (!act[r]) continue;
+      double Dr = d->efc_D[r], *Jr = d->efc_J[r];
+      for (int i = 0; i < nv; i++) {
+        g[i] += Dr * jar[r] * Jr[i];
+        if (Jr[i] == 0) continue;
+        for (int k = 0; k <= i; k++) H[i][k] += Dr * Jr[i] * Jr[k];
+      }
+    }
+    for (int i = 0; i < nv; i++) for (int k = i + 1; k < nv; k++) H[i][k] = H[k][i];
+    double gn = 0;
+    for (int i = 0; i < nv; i++) gn += g[i] * g[i];
+    if (scale * sqrt(gn) < 1e-14) break;
+    if (chol(L, H, nv)) break;
+    chol_solve(s, L, g, nv);
+    for (int i = 0; i < nv; i++) s[i] = -s[i];
+    double alpha = line_search(m, d, x, s, jar, Js);
+    for (int i = 0; i < nv; i++) x[i] += alpha * s[i];
+    double newcost = eval_cost(m, d, x, jar);
+    int same = 1;
+    for (int r = 0; r < ne; r++) if ((jar[r] < 0) != act[r]) { same = 0; break; }
+    double improvement = cost - newcost;
+    cost = newcost;
+    if (same || scale * improvement < 1e-16) { it++; break; }
+  }
+  d->solver_niter = it;
+  memcpy(d->qacc, x, sizeof(double) * nv);
+  memset(d->qfrc_constraint, 0, sizeof(double) * nv);
+  for (int r = 0; r < ne; r++) {
+    d->efc_force[r] = jar[r] < 0 ? -d->efc_D[r] * jar[r] : 0;
+    for (int k = 0; k < nv; k++) d->qfrc_constraint[k] += d->efc_J[r][k] * d->efc_force[r];
+  }
+}
+
+/* ------------------------------------------------------------------ mj_forward */
+void orc_forward(const OrcModel* m, OrcData* d) {
+  int nv = m->nv;
+  static double L[OMAXV][OMAXV];
+  kinematics(m, d);
+  com_pos(m, d);
+  tendon(m, d);
+  crb(m, d);
+  collision(m, d);
+  make_constraint(m, d);
+  com_vel(m, d);
+  passive(m, d);
+  reference_constraint(m, d);
+  rne(m, d);
+  actuation(m, d);
+  for (int i = 0; i < nv; i++) d->qfrc_smooth[i] = d->qfrc_passive[i] - d->qfrc_bias[i] + d->qfrc_actuator[i];
+  chol(L, d->qM, nv);
+  chol_solve(d->qacc_smooth, L, d->qfrc_smooth, nv);
+  if (d->nefc == 0) {
+    memcpy(d->qacc, d->qacc_smooth, sizeof(double) * nv);
+    memset(d->qfrc_constraint, 0, sizeof(double) * nv);
+    d->solver_niter = 0;
+  } else {
+    solve_newton(m, d);
+  }
+}
+
+/* ------------------------------------------------------------------ mj_Euler / mj_advance */
+static void euler(const OrcModel* m, OrcData* d) {
+  int nv = m->nv;
+  double h = m->timestep, f[OMAXV], a[OMAXV];
+  static double H[OMAXV][OMAXV], L[OMAXV][OMAXV];
+  memcpy(H, d->qM, sizeof H);
+  for (int i = 0; i < nv; i++) H[i][i] += h * m->dof_damping[i];
+  for (int i = 0; i < nv; i++) f[i] = d->qfrc_smooth[i] + d->qfrc_constraint[i];
+  chol(L, H, nv);
+  chol_solve(a, L, f, nv);
+  for (int i = 0; i < nv; i++) d->qvel[i] += h * a[i];
+  for (int j = 0; j < m->njnt; j++) {             /* mj_integratePos */
+    int qa = m->jnt_qposadr[j], da = m->jnt_dofadr[j];
+    if (m->jnt_type[j] == 0) {
+      for (int k = 0; k < 3; k++) d->qpos[qa + k] += h * d->qvel[da + k];
+      double axis[3] = {d->qvel[da + 3], d->qvel[da + 4], d->qvel[da + 5]}, qrot[4];
+      double ang = h * normalize3(axis);
+      axisangle2quat(qrot, axis, ang);
+      normalize4(d->qpos + qa + 3);
+      mulquat(d->qpos + qa + 3, d->qpos + qa + 3, qrot);
+    } else {
+      d->qpos[qa] += h * d->qvel[da];
+    }
+  }
+  d->time += h;
+  memcpy(d->qacc_warmstart, d->qacc, sizeof(double) * nv);
+}
+
+/* ------------------------------------------------------------------ mj_step */
+static void reset_keep_warnings(const OrcModel* m, OrcData* d) {
+  int w0 = d->warning_badqpos, w1 = d->warning_badqvel, w2 = d->warning_badqacc, w3 = d->warning_overflow;
+  orc_reset_data(m, d);
+  d->warning_badqpos = w0; d->warning_badqvel = w1; d->warning_badqacc = w2; d->warning_overflow = w3;
+}
+
+void orc_step(const OrcModel* m, OrcData* d) {
+  for (int i = 0; i < m->nq; i++)                 /* mj_checkPos */
+    if (isbad(d->qpos[i])) { d->warning_badqpos++; reset_keep_warnings(m, d); break; }
+  for (int i = 0; i < m->nv; i++)                 /* mj_checkVel */
+    if (isbad(d->qvel[i])) { d->warning_badqvel++; reset_keep_warnings(m, d); break; }
+  orc_forward(m, d);
+  for (int i = 0; i < m->nv; i++)                 /* mj_checkAcc */
+    if (isbad(d->qacc[i])) { d->warning_badqacc++; reset_keep_warnings(m, d); orc_forward(m, d); break; }
+  euler(m, d);
+}
+
+void orc_step_n(const OrcModel* m, OrcData* d, const double* ctrl, int nsub) {
+  for (int s = 0; s < nsub; s++) {
+    memcpy(d->ctrl, ctrl, sizeof(double) * m->nu);
+    orc_step(m, d);
+  }
+}
