@@ -8,6 +8,7 @@
  *   hs_model_field       <- MjModel attribute reads (nq, nv, nu, body_mass, ...) custom_env.py:87,59-61
  *   hs_batch_create      <- mujoco.MjData(model) per env                  custom_env.py:54
  *                           x SubprocVecEnv([make_env(...)] * n_envs)     train_sb3.py:203
+ *   hs_set_seed          <- VecEnv.seed / np.random.seed(seed) of reset (custom_env.py:99-100)
  *   hs_set_config        <- env_config keys duration/frame_skip/reward_config custom_env.py:21-32,
  *                           train_sb3.py:183-200
  *   hs_reset             <- HumanoidEnv.reset: mj_resetData + noise + one mj_step  custom_env.py:97-150
@@ -93,6 +94,8 @@ void hs_batch_destroy(hs_batch* b);
 int hs_batch_get_info(const hs_batch* b, hs_batch_info* out);
 int hs_get_buffers(const hs_batch* b, hs_buffers* out);
 int hs_set_config(hs_batch* b, const hs_env_config* cfg);
+/* Base seed of the on-device reset RNG (VecEnv.seed; SB3 seeds workers with seed + rank). */
+int hs_set_seed(hs_batch* b, uint64_t seed);
 int hs_get_config(const hs_batch* b, hs_env_config* cfg);
 
 /* mask: [N] uint8 device (NULL = all envs).  qpos_noise/qvel_noise: [N][nq]/[N][nv] device

@@ -3,5 +3,25 @@
 Drop-in for the hot path of redradman/MujocoPoseLearning: the per-process
 ``mujoco.mj_step`` / SB3 ``SubprocVecEnv`` path of custom_env.py, re-built as HIP kernels
 for gfx950 behind the same ``HumanoidEnv`` / VecEnv / ``REWARD_FUNCTIONS`` surface.
+Heavy modules (torch, the native library) load lazily on first use.
 """
 __version__ = "0.1.0"
+
+from .reward_functions import REWARD_FUNCTIONS, robust_kneeling_reward, stand_reward, walk_reward  # noqa: F401
+from .utils import quaternion_to_euler  # noqa: F401
+
+
+def __getattr__(name):
+    if name == "HumanoidEnv":
+        from .env import HumanoidEnv
+        return HumanoidEnv
+    if name == "HumanoidVecEnv":
+        from .vec_env import HumanoidVecEnv
+        return HumanoidVecEnv
+    if name in ("HsModel", "load_model"):
+        from . import model
+        return getattr(model, name)
+    if name == "HsBatch":
+        from .batch import HsBatch
+        return HsBatch
+    raise AttributeError(name)

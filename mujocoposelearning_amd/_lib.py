@@ -64,6 +64,7 @@ def lib():
         "hs_get_buffers": (i, [vp, vp]),
         "hs_set_config": (i, [vp, vp]),
         "hs_get_config": (i, [vp, vp]),
+        "hs_set_seed": (i, [vp, u64]),
         "hs_reset": (i, [vp, vp, vp, vp, vp]),
         "hs_step": (i, [vp, vp, vp]),
         "hs_physics_step": (i, [vp, vp, i, vp]),
@@ -83,7 +84,7 @@ def lib():
 
 
 EXPORTED = ("hs_model_load", "hs_model_free", "hs_model_field", "hs_batch_create", "hs_batch_destroy",
-            "hs_batch_get_info", "hs_get_buffers", "hs_set_config", "hs_get_config", "hs_reset", "hs_step",
+            "hs_batch_get_info", "hs_get_buffers", "hs_set_config", "hs_set_seed", "hs_get_config", "hs_reset", "hs_step",
             "hs_physics_step", "hs_state_io", "hs_set_debug", "hs_get_debug", "hs_synchronize", "hs_last_error",
             "hs_version")
 

@@ -90,6 +90,9 @@ class HsBatch:
                 c.kneel_params[k] = float(p[key])
         check(lib().hs_set_config(self._h, C.byref(c)))
 
+    def set_seed(self, seed):
+        check(lib().hs_set_seed(self._h, int(seed) & (2 ** 64 - 1)))
+
     # -- stepping --------------------------------------------------------------------------
     def reset(self, mask=None, qpos_noise=None, qvel_noise=None):
         """custom_env.py:97-150 for the envs selected by ``mask`` (None = all)."""

@@ -290,6 +290,12 @@ int hs_set_config(hs_batch* b, const hs_env_config* cfg) {
   return 0;
 }
 
+int hs_set_seed(hs_batch* b, uint64_t seed) {
+  if (!b) return fail("null batch");
+  b->seed = seed;
+  return 0;
+}
+
 int hs_get_config(const hs_batch* b, hs_env_config* cfg) {
   if (!b || !cfg) return fail("null argument");
   *cfg = b->cfg;

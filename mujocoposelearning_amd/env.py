@@ -1,0 +1,238 @@
+"""HumanoidEnv -- drop-in for the reference custom_env.py:HumanoidEnv, stepped on the GPU.
+
+Same constructor keys and defaults (custom_env.py:21-43), same ``reset``/``step`` return
+tuples and info keys (custom_env.py:133-150, 216-230), same 352-float observation layout with
+the same stale derived fields (custom_env.py:232-261), same reward plug-in dispatch including
+the ``ValueError`` for unknown types (custom_env.py:263-271).  Reset noise is drawn from
+numpy's global legacy RNG exactly as the reference (custom_env.py:99-117), so
+``reset(seed=s)`` reproduces the reference's initial state bit-for-bit before the physics step.
+
+Additive env_config keys: ``device`` (GPU index, default 0), ``precision`` ('fp64' default
+for this single-env surface, 'fp32'), ``max_newton``.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import reward_functions as _rf
+from .batch import HsBatch
+from .model import HsModel
+from .spaces import Box, Env
+
+CLIP_OBSERVATION_VALUE = np.inf   # custom_env.py:9
+ACTION_CLIP_VALUE = 1             # custom_env.py:10
+
+
+class HsData:
+    """Read-only MjData-like view of one env (fields the reward plug-ins read)."""
+
+    def __init__(self, env):
+        self._env = env
+
+    def _b(self):
+        return self._env._batch
+
+    def _obs(self):
+        return self._b().obs[self._env._idx].double().cpu().numpy()
+
+    @property
+    def qpos(self):
+        return self._b().qpos[self._env._idx].double().cpu().numpy()
+
+    @property
+    def qvel(self):
+        return self._b().qvel[self._env._idx].double().cpu().numpy()
+
+    @property
+    def ctrl(self):
+        return self._b().ctrl[self._env._idx].double().cpu().numpy()
+
+    @property
+    def time(self):
+        return float(self._b().time[self._env._idx].item())
+
+    @property
+    def qacc_warmstart(self):
+        return self._b().qacc_warmstart[self._env._idx].double().cpu().numpy()
+
+    def _slices(self):
+        m = self._env.model
+        o1 = m.nq - 2
+        o2 = o1 + m.nv
+        o3 = o2 + 10 * m.nbody
+        o4 = o3 + 6 * m.nbody
+        return o1, o2, o3, o4
+
+    @property
+    def cinert(self):
+        o1, o2, o3, o4 = self._slices()
+        return self._obs()[o2:o3].reshape(self._env.model.nbody, 10)
+
+    @property
+    def cvel(self):
+        o1, o2, o3, o4 = self._slices()
+        return self._obs()[o3:o4].reshape(self._env.model.nbody, 6)
+
+    @property
+    def qfrc_actuator(self):
+        o1, o2, o3, o4 = self._slices()
+        return self._obs()[o4:]
+
+    @property
+    def subtree_com(self):
+        """Row 0 (and every body of the single kinematic tree's root) = whole-model COM of the last
+        forward pass; other rows are not computed by the engine (NaN)."""
+        m = self._env.model
+        out = np.full((m.nbody, 3), np.nan)
+        com = self._b().aux[self._env._idx, 32:35].double().cpu().numpy()
+        out[0] = com
+        out[1] = com
+        return out
+
+    @property
+    def subtree_linvel(self):
+        return np.zeros((self._env.model.nbody, 3))   # lazy in MuJoCo mj_step: never computed
+
+    @property
+    def cfrc_ext(self):
+        return np.zeros((self._env.model.nbody, 6))   # lazy in MuJoCo mj_step: never computed
+
+    @property
+    def warning(self):
+        return self._b().warning[self._env._idx].cpu().numpy()
+
+
+class HumanoidEnv(Env):
+    metadata = {"render_modes": ["rgb_array"], "render_fps": 60}
+
+    def __init__(self, env_config):
+        super().__init__()
+        if isinstance(env_config, dict):
+            self.model_path = env_config.get('model_path')
+            self.duration = env_config.get('duration', 15)
+            self.framerate = env_config.get('framerate', 60)
+            self.render_mode = env_config.get('render_mode')
+            self.render_interval = env_config.get('render_interval', 100)
+            self.reward_config = env_config.get('reward_config', {'type': 'default'})
+            self.frame_skip = env_config.get('frame_skip', 5)
+            self.grace_period_length = env_config.get('grace_period_length', 300)
+            self.grace_period_steps = 0
+            self.total_reward = 0.0
+            self.run_name = env_config.get('run_name')
+            device = env_config.get('device', 0)
+            precision = env_config.get('precision', 'fp64')
+            max_newton = env_config.get('max_newton', 100)
+        else:
+            self.model_path = env_config
+            self.duration = 15
+            self.framerate = 60
+            self.render_mode = None
+            self.render_interval = 100
+            self.reward_config = {'type': 'default'}
+            self.frame_skip = 5
+            self.grace_period_steps = 0
+            self.total_reward = 0.0
+            device, precision, max_newton = 0, 'fp64', 100
+        self.model = HsModel(self.model_path)
+        self._batch = HsBatch(self.model, 1, device=device, precision=precision)
+        self._idx = 0
+        self.data = HsData(self)
+        self.frames = []
+        self.renderer = None
+        self.step_count = 0
+        self.init_qpos = self.model.qpos0.copy()
+        self.init_qpos[2] = 1.282
+        self.init_qpos[3:7] = [1, 0, 0, 0]
+        self.init_qvel = np.zeros(self.model.nv)
+        self._configure(max_newton)
+        obs_size = self._batch.obs_dim
+        self.observation_space = Box(low=-CLIP_OBSERVATION_VALUE, high=CLIP_OBSERVATION_VALUE, shape=(obs_size,),
+                                     dtype=np.float64)
+        self.action_space = Box(low=-ACTION_CLIP_VALUE, high=ACTION_CLIP_VALUE, shape=(self.model.nu,),
+                                dtype=np.float32)
+        if self.render_mode == "rgb_array":
+            raise NotImplementedError("rendering (mujoco.Renderer) is out of scope for this engine")
+        self.reset()
+
+    def _configure(self, max_newton):
+        rtype = self.reward_config.get('type', 'default')
+        self._reward_dev = _rf.DEVICE_REWARD_IDS.get(_rf.REWARD_FUNCTIONS.get(rtype))
+        params = self.reward_config.get('params')
+        kneel = params if (self._reward_dev == 1 and params) else None
+        self._batch.configure(frame_skip=self.frame_skip, duration=float(self.duration), max_steps=750,
+                              reward_id=self._reward_dev if self._reward_dev is not None else -1, autoreset=0,
+                              max_newton=max_newton, init_height=float(self.init_qpos[2]), noise_scale=0.01,
+                              kneel_params=kneel)
+
+    def reset(self, *, seed=None, options=None):
+        """custom_env.py:97-150."""
+        if seed is not None:
+            np.random.seed(seed)
+        pos_noise = np.random.uniform(low=-0.01, high=0.01, size=self.model.nq)
+        vel_noise = np.random.uniform(low=-0.01, high=0.01, size=self.model.nv)
+        # the kernel applies pos_noise[2] *= 0.1, pos_noise[3:7] = 0 and the init pose (custom_env.py:105-117)
+        self._batch.reset(qpos_noise=pos_noise[None], qvel_noise=vel_noise[None])
+        self.frames = []
+        state = self._get_state()
+        info = {
+            'reward_components': {'forward': 0.0, 'standing': 0.0, 'healthy_pose': 0.0, 'alive': 0.0, 'total': 0.0},
+            'height': float(state[0]),
+            'forward_velocity': float(state[self.model.nq - 2]),
+            'truncated': False,
+            'terminated': False,
+        }
+        self.step_count = 0
+        self.total_reward = 0.0
+        return state, info
+
+    def step(self, action):
+        """custom_env.py:152-230 (frame_skip substeps on the GPU, reward on the GPU for built-ins)."""
+        import torch
+        self.step_count += 1
+        a = torch.as_tensor(np.asarray(action, dtype=np.float32).reshape(1, -1), device=self._batch.device)
+        obs_t, rew_t, term_t, trunc_t = self._batch.step(a)
+        state = obs_t[0].double().cpu().numpy()
+        height = state[0]
+        truncated = bool(trunc_t[0].item())
+        truncation_info = {}
+        if truncated:
+            truncation_info['reason'] = 'timeout'
+            reward = 0.0
+        else:
+            reward = float(rew_t[0].item()) if self._reward_dev is not None else self._compute_reward()
+            params = self.reward_config.get('params')
+            if params is not None and self._reward_dev in (0, 2):
+                params["previous_qpos"] = self.data.qpos.copy()   # stand/walk side effect (reward_functions.py:208)
+        self.total_reward += reward
+        terminated = bool(term_t[0].item())
+        info = {
+            'reward_components': getattr(self, 'reward_components', {}),
+            'height': height,
+            'step_count': self.step_count,
+            'truncated': truncated,
+            'truncation_info': truncation_info,
+            'terminated': terminated,
+            'total_reward': self.total_reward,
+        }
+        return state, reward, terminated, truncated, info
+
+    def _get_state(self):
+        return self._batch.obs[0].double().cpu().numpy()
+
+    def _compute_reward(self):
+        reward_type = self.reward_config.get('type', 'default')
+        reward_params = self.reward_config.get('params', None)
+        if reward_type not in _rf.REWARD_FUNCTIONS:
+            raise ValueError(f"Unknown reward type: {reward_type}")
+        return _rf.REWARD_FUNCTIONS[reward_type](self.data, reward_params)
+
+    def render(self):
+        if self.render_mode != "rgb_array":
+            return None
+        raise NotImplementedError("rendering (mujoco.Renderer) is out of scope for this engine")
+
+    def save_video(self, episode_num):
+        raise NotImplementedError("video recording (mediapy) is out of scope for this engine")
+
+    def close(self):
+        self._batch.close()

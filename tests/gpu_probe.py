@@ -1,0 +1,75 @@
+"""Quick GPU probe: env-step throughput at N envs and trajectory divergence vs the oracle."""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+from mujocoposelearning_amd.batch import HsBatch  # noqa: E402
+from mujocoposelearning_amd.model import HsModel  # noqa: E402
+from oracle.oracle import Oracle  # noqa: E402
+
+XML = os.path.join(ROOT, "tests", "golden", "humanoid.xml")
+
+
+def throughput(n, steps=50, prec="fp32"):
+    model = HsModel(XML)
+    b = HsBatch(model, n, precision=prec, seed=1)
+    b.configure(frame_skip=3, duration=10.0, reward_id=0)
+    b.reset()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    acts = torch.rand(steps + 5, n, model.nu, device="cuda", generator=g) * 2 - 1
+    for k in range(5):
+        b.step(acts[k])
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for k in range(steps):
+        b.step(acts[5 + k])
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t
+    print(f"[{prec}] N={n}: {dt / steps * 1e3:.3f} ms/step  -> {n * steps / dt:,.0f} env-steps/s ; "
+          f"mean ncon {b.aux[:, 35].float().mean().item():.1f} nefc {b.aux[:, 36].float().mean().item():.1f} "
+          f"newton {b.aux[:, 37].float().mean().item():.2f}  warnings {b.warning.sum(0).tolist()}")
+
+
+def divergence(prec, tape, nsub=1000, seed=0):
+    model = HsModel(XML)
+    o = Oracle(XML)
+    rng = np.random.default_rng(seed)
+    qpos = o.M["qpos0"].copy()
+    qpos += rng.uniform(-0.01, 0.01, 28) * np.r_[1, 1, 0.1, 0, 0, 0, 0, np.ones(21)]
+    qvel = rng.uniform(-0.01, 0.01, 27)
+    b = HsBatch(model, 1, precision=prec)
+    b.set_state(qpos=qpos, qvel=qvel, time=0.0, qacc_warmstart=0.0)
+    o.qpos[:] = qpos
+    o.qvel[:] = qvel
+    if tape == "zeros":
+        ctrl = np.zeros((nsub, 21), np.float32)
+    else:
+        ctrl = rng.uniform(-1, 1, (nsub, 21)).astype(np.float32)
+    errs = []
+    c = torch.tensor(ctrl, device="cuda")
+    for s in range(nsub):
+        b.physics_step(c[s:s + 1], 1)
+        o.step(ctrl[s].astype(np.float64), 1)
+        if s % 50 == 49 or s == nsub - 1:
+            st = b.get_state()
+            errs.append((s + 1, np.abs(st["qpos"][0] - o.qpos).max(), np.abs(st["qvel"][0] - o.qvel).max(), o.d.ncon))
+    print(f"[{prec} tape={tape}] " + " ".join(f"{s}:{eq:.1e}/{ev:.1e}/c{nc}" for s, eq, ev, nc in errs))
+
+
+if __name__ == "__main__":
+    which = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if which in ("all", "tp"):
+        for n in (1024, 4096, 16384):
+            throughput(n)
+        throughput(4096, prec="fp64")
+    if which in ("all", "div"):
+        divergence("fp64", "uniform")
+        divergence("fp64", "zeros")
+        divergence("fp32", "uniform")
+        divergence("fp32", "zeros")

@@ -1,0 +1,64 @@
+"""The C-ABI library loads and exports every entry point include/hsim.h declares (CPU only:
+no compute calls), and misuse fails loudly with a message."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from conftest import ROOT, XML
+
+HEADER = os.path.join(ROOT, "include", "hsim.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(hs_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from mujocoposelearning_amd import _lib
+    L = _lib.lib()
+    names = declared_functions()
+    assert len(names) >= 18
+    for n in names:
+        assert hasattr(L, n), n
+    assert set(names) == set(_lib.EXPORTED)
+
+
+def test_version_and_errors():
+    from mujocoposelearning_amd import _lib
+    L = _lib.lib()
+    assert b"gfx950" in L.hs_version()
+    err = C.create_string_buffer(256)
+    assert not L.hs_model_load(b"/nonexistent.xml", err, 256)
+    assert b"cannot open" in err.value
+    assert L.hs_set_config(None, None) < 0 and b"null" in L.hs_last_error()
+    assert L.hs_step(None, None, None) < 0
+
+
+def test_model_fields_through_abi():
+    from mujocoposelearning_amd.model import HsModel
+    m = HsModel(XML)
+    assert (m.nq, m.nv, m.nu, m.nbody) == (28, 27, 21, 17)
+    assert m.field("body_mass").sum() == pytest.approx(40.84402122162132)
+    with pytest.raises(Exception, match="unknown model field"):
+        m.field("no_such_field")
+
+
+def test_batch_create_without_gpu_fails_loudly():
+    """No silent CPU fallback: creating a batch without a GPU raises."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from mujocoposelearning_amd.batch import HsBatch
+    from mujocoposelearning_amd.model import HsModel
+    with pytest.raises(RuntimeError, match="GPU"):
+        HsBatch(HsModel(XML), 4)
+
+
+def test_config_struct_layout():
+    from mujocoposelearning_amd import _lib
+    assert C.sizeof(_lib.hs_env_config) == 6 * 4 + 3 * 8 + 9 * 8
+    assert C.sizeof(_lib.hs_buffers) == 15 * 8

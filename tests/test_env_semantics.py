@@ -1,0 +1,98 @@
+"""Env-level known-answer tests written from the reference code (custom_env.py), checked on the
+CPU oracle env; the GPU env is held to the same KATs in test_gpu_env.py."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, XML
+
+CFG = {"model_path": XML, "duration": 10.0, "reward_config": {"type": "stand"}, "frame_skip": 3}
+
+
+def test_reset_noise_stream_golden():
+    """custom_env.py:99-110: np.random.seed(s); uniform(-.01,.01,28) then uniform(-.01,.01,27)."""
+    g = np.load(os.path.join(GOLDEN, "reset_noise_golden.npz"))
+    for s in range(5):
+        np.random.seed(s)
+        assert np.array_equal(np.random.uniform(-0.01, 0.01, 28), g[f"pos_{s}"])
+        assert np.array_equal(np.random.uniform(-0.01, 0.01, 27), g[f"vel_{s}"])
+    assert g["pos_0"][0] == pytest.approx(0.00097627, abs=1e-8)
+    assert g["pos_0"][1] == pytest.approx(0.00430379, abs=1e-8)
+
+
+def test_obs_layout_and_reset_time():
+    from oracle.env import OracleHumanoidEnv
+    env = OracleHumanoidEnv(CFG)
+    obs, _ = env.reset(seed=0)
+    assert obs.shape == (352,)
+    # slices [0:26] qpos[2:], [26:53] qvel, [53:223] cinert, [223:325] cvel, [325:352] qfrc_actuator
+    assert np.array_equal(obs[0:26], env.sim.qpos[2:])
+    assert np.array_equal(obs[26:53], env.sim.qvel)
+    assert np.all(obs[53:63] == 0) and np.all(obs[223:229] == 0)     # world body rows
+    assert env.sim.time == pytest.approx(0.005)                     # one mj_step inside reset
+    # pre-step initial state per seed: init pose + noise (z noise x0.1, quaternion exact)
+    g = np.load(os.path.join(GOLDEN, "reset_noise_golden.npz"))
+    e2 = OracleHumanoidEnv(CFG)
+    e2.sim.reset_data()
+    q = e2.init_qpos + g["pos_0"] * np.r_[1, 1, 0.1, 0, 0, 0, 0, np.ones(21)]
+    assert q[3:7].tolist() == [1, 0, 0, 0] and q[2] == pytest.approx(1.282 + 0.1 * g["pos_0"][2])
+
+
+def test_stale_derived_fields_in_obs():
+    """cinert / cvel / qfrc_actuator come from the forward pass BEFORE the last integration."""
+    from oracle.env import OracleHumanoidEnv
+    env = OracleHumanoidEnv(CFG)
+    env.reset(seed=1)
+    a = np.random.default_rng(0).uniform(-1, 1, 21).astype(np.float32)
+    obs, *_ = env.step(a)
+    stale_cvel = obs[223:325].copy()
+    env.sim.forward()     # recompute at the post-step state
+    assert not np.allclose(stale_cvel, env.sim.get("cvel").reshape(-1))
+    assert np.allclose(obs[325:352][6:], 40 * 0 + obs[325:352][6:])
+
+
+def test_episode_terminates_at_step_667():
+    """duration 10, frame_skip 3: time = 0.005 + 0.015 k >= 10 first at k = 667; 750-step
+    truncation unreachable (custom_env.py:201-213)."""
+    t = 0.005
+    k = 0
+    h = 0.005
+    while True:
+        k += 1
+        for _ in range(3):
+            t += h
+        if t >= 10.0:
+            break
+    assert k == 667
+    from oracle.env import OracleHumanoidEnv
+    env = OracleHumanoidEnv(CFG)
+    env.reset(seed=0)
+    env.sim.d.time = 0.005 + 0.015 * 665    # fast-forward the clock only
+    _, _, term, trunc, _ = env.step(np.zeros(21))
+    assert not term and not trunc
+    _, _, term, trunc, _ = env.step(np.zeros(21))
+    assert term and not trunc
+
+
+def test_truncation_after_750_steps_gives_zero_reward():
+    from oracle.env import OracleHumanoidEnv
+    env = OracleHumanoidEnv({**CFG, "duration": 1e9})
+    env.reset(seed=0)
+    env.step_count = 749
+    _, r, term, trunc, _ = env.step(np.zeros(21))
+    assert trunc and r == 0.0 and not term
+
+
+def test_stand_reward_foot_term_constant():
+    """cfrc_ext is never computed inside mj_step (no sensors) -> stand's foot term == 0.2."""
+    from oracle.env import OracleHumanoidEnv
+    env = OracleHumanoidEnv(CFG)
+    env.reset(seed=3)
+    _, r, *_ = env.step(np.zeros(21, np.float32))
+    q, v = env.sim.qpos, env.sim.qvel
+    from oracle.rewards import quaternion_to_euler
+    roll, pitch, _ = quaternion_to_euler(q[3:7])
+    expect = 0.4 * np.exp(-2 * (v[0] - 1) ** 2) + 0.3 * (0.5 * np.exp(-2 * (q[2] - 1.282) ** 2) +
+                                                          0.5 * np.exp(-3 * (roll ** 2 + pitch ** 2))) + 0.2 + 0.1
+    assert r == pytest.approx(expect, rel=1e-12)

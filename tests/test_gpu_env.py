@@ -1,0 +1,177 @@
+"""GPU env semantics and full-size properties (BASELINE.json configs[1]: 4096 envs, stand,
+frame_skip 3, duration 10) through the C ABI."""
+import numpy as np
+import pytest
+
+from conftest import XML
+
+pytestmark = pytest.mark.gpu
+CFG = {"model_path": XML, "duration": 10.0, "reward_config": {"type": "stand"}, "frame_skip": 3}
+
+
+@pytest.fixture(scope="module")
+def model():
+    from mujocoposelearning_amd.model import HsModel
+    return HsModel(XML)
+
+
+def _batch(model, n, prec="fp32", seed=0, reward=0, autoreset=1):
+    from mujocoposelearning_amd.batch import HsBatch
+    b = HsBatch(model, n, precision=prec, seed=seed)
+    b.configure(frame_skip=3, duration=10.0, reward_id=reward, autoreset=autoreset, max_steps=750)
+    return b
+
+
+def test_termination_at_667_and_autoreset(model):
+    import torch
+    n = 64
+    b = _batch(model, n)
+    b.reset()
+    # fast-forward every env's clock to just before the end (physics state unchanged)
+    st = b.get_state()
+    b.set_state(time=st["time"] + 0.015 * 665)
+    b.step_count.fill_(665)
+    a = torch.zeros(n, 21, device=b.device)
+    obs, rew, term, trunc = b.step(a)
+    assert not term.any() and not trunc.any()
+    obs, rew, term, trunc = b.step(a)
+    assert term.all() and not trunc.any()
+    # auto-reset: fresh episode (time = one reset substep, step_count 0), terminal obs kept
+    st = b.get_state()
+    assert np.allclose(st["time"], 0.005)
+    assert (b.step_count == 0).all() and (b.episode == 2).all()
+    assert not torch.equal(b.terminal_obs, b.obs)
+    assert torch.isfinite(b.obs).all()
+
+
+def test_truncation_reward_zero(model):
+    import torch
+    b = _batch(model, 8)
+    b.configure(duration=1e9)
+    b.reset()
+    b.step_count.fill_(749)
+    _, rew, term, trunc = b.step(torch.zeros(8, 21, device=b.device))
+    assert trunc.all() and not term.any() and (rew == 0).all()
+
+
+def test_vecenv_sb3_surface(model):
+    from mujocoposelearning_amd.vec_env import HumanoidVecEnv
+    env = HumanoidVecEnv(CFG, n_envs=8, model=model, seed=4)
+    obs = env.reset()
+    assert obs.shape == (8, 352) and obs.dtype == np.float64
+    a = np.random.default_rng(0).uniform(-1, 1, (8, 21)).astype(np.float32)
+    obs, rew, dones, infos = env.step(a)
+    assert obs.shape == (8, 352) and rew.shape == (8,) and dones.shape == (8,) and len(infos) == 8
+    assert not dones.any() and infos[0]["step_count"] == 1
+    env.batch.set_state(time=np.full(8, 9.999))
+    obs, rew, dones, infos = env.step(a)
+    assert dones.all()
+    for i in range(8):
+        assert "terminal_observation" in infos[i] and infos[i]["TimeLimit.truncated"] is False
+        assert infos[i]["terminal_observation"].shape == (352,)
+    assert env.get_attr("frame_skip") == [3] * 8
+    assert env.env_is_wrapped(object) == [False] * 8
+    assert env.seed(7) == list(range(7, 15))
+    env.close()
+
+
+def test_full_size_determinism_and_batch_invariance(model):
+    """configs[1] size: 4096 envs.  Bitwise-identical reruns; an env's trajectory does not depend
+    on its neighbours (same state in a 1-env batch and at index 17 of the 4096-env batch)."""
+    import torch
+    n = 4096
+    g = torch.Generator(device="cuda").manual_seed(0)
+    acts = torch.rand(20, n, 21, device="cuda", generator=g) * 2 - 1
+    outs = []
+    for rep in range(2):
+        b = _batch(model, n, seed=9)
+        b.reset()
+        for k in range(20):
+            b.step(acts[k])
+        outs.append((b.qpos.clone(), b.qvel.clone(), b.obs.clone(), b.reward.clone()))
+        st0 = b.get_state()
+        warn = b.warning.sum(0).tolist()
+        aux = b.aux.clone()
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
+    assert torch.isfinite(outs[0][2]).all()
+    assert warn[:3] == [0, 0, 0]
+    assert (aux[:, 35] <= 48).all() and (aux[:, 36] <= 128).all()
+    # batch-composition invariance
+    b1 = _batch(model, 1, seed=9)
+    b1.reset()
+    idx = 17
+    b1.set_state(qpos=st0["qpos"][idx], qvel=st0["qvel"][idx], qacc_warmstart=st0["qacc_warmstart"][idx],
+                 time=st0["time"][idx], ctrl=st0["ctrl"][idx])
+    bN = _batch(model, n, seed=9)
+    bN.set_state(**{k: v for k, v in st0.items()})
+    a = acts[0]
+    b1.step(a[idx:idx + 1])
+    bN.step(a)
+    assert torch.equal(b1.qpos[0], bN.qpos[idx]) and torch.equal(b1.obs[0], bN.obs[idx])
+
+
+def test_reset_distribution_device_rng(model):
+    """On-device reset noise: U(-.01, .01) per coordinate, z noise x0.1, quaternion exact; the
+    reset then runs exactly one substep (time 0.005)."""
+    n = 4096
+    b = _batch(model, n, seed=123)
+    b.configure(max_newton=100)
+    b.reset()
+    st = b.get_state()
+    assert np.allclose(st["time"], 0.005)
+    # root x, y move only h * |v| ~ 5e-5 in the one reset substep: they carry the raw noise
+    xy = st["qpos"][:, :2].ravel()
+    assert np.abs(xy).max() < 0.0101
+    hist, _ = np.histogram(xy, bins=10, range=(-0.01, 0.01))
+    assert np.all(np.abs(hist / xy.size - 0.1) < 0.02)
+    assert abs(xy.mean()) < 5e-4 and abs(xy.std() - 0.02 / np.sqrt(12)) < 5e-4
+    # root z: init height 1.282 + 0.1 * noise, then one substep of settling
+    assert np.abs(st["qpos"][:, 2] - 1.282).max() < 0.0015
+    quat = st["qpos"][:, 3:7]
+    assert np.allclose(np.linalg.norm(quat, axis=1), 1, atol=1e-6)
+    assert np.abs(quat[:, 0] - 1).max() < 1e-3
+    # different seeds -> different states, same seed -> identical
+    b2 = _batch(model, n, seed=123)
+    b2.reset()
+    assert np.array_equal(b2.get_state()["qpos"], st["qpos"])
+    b3 = _batch(model, n, seed=124)
+    b3.reset()
+    assert not np.array_equal(b3.get_state()["qpos"], st["qpos"])
+
+
+def test_bad_state_autoreset_warning(model):
+    """mj_checkPos semantics: a NaN qpos resets that env to qpos0 / time 0 and bumps a warning."""
+    import torch
+    b = _batch(model, 4)
+    b.reset()
+    st = b.get_state()
+    q = st["qpos"].copy()
+    q[2, 10] = np.nan
+    b.set_state(qpos=q)
+    b.physics_step(torch.zeros(4, 21, device=b.device), 1)
+    w = b.warning.cpu().numpy()
+    assert w[2, 0] == 1 and w[[0, 1, 3], 0].sum() == 0
+    st2 = b.get_state()
+    assert st2["time"][2] == pytest.approx(0.005, abs=1e-7)
+    assert np.all(np.isfinite(st2["qpos"]))
+
+
+def test_action_clamp_and_reward_reads_raw_ctrl(model):
+    """Force uses clamp(ctrl, -1, 1) (motor ctrlrange), the stand reward reads the raw ctrl."""
+    import torch
+    b = _batch(model, 2, prec="fp64")
+    b.configure(autoreset=0)
+    b.reset()
+    st = b.get_state()
+    b2 = _batch(model, 2, prec="fp64")
+    b2.configure(autoreset=0)
+    b2.set_state(**st)
+    big = torch.full((2, 21), 3.0, device=b.device)
+    one = torch.full((2, 21), 1.0, device=b.device)
+    _, r_big, *_ = b.step(big)
+    _, r_one, *_ = b2.step(one)
+    assert torch.equal(b.qpos, b2.qpos)            # identical physics
+    s = b.get_state()
+    if s["qpos"][0, 2] >= 0.8:
+        assert (r_big < r_one).all()                # torque penalty sees 3.0, not 1.0

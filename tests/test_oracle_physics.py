@@ -1,0 +1,265 @@
+"""Physics invariants that pin the fp64 oracle restatement of mj_step (no MuJoCo available here:
+SURVEY.md section 4 item 4).  Each check uses an independent path (energies, finite differences,
+analytic geometry, KKT conditions) rather than re-running the same code."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from conftest import XML
+
+
+@pytest.fixture()
+def orc():
+    from oracle.oracle import Oracle
+    return Oracle(XML)
+
+
+def _random_state(o, seed, scale=0.3):
+    rng = np.random.default_rng(seed)
+    q = o.M["qpos0"].copy()
+    q[7:] += rng.uniform(-scale, scale, 21)
+    quat = np.array([1.0, *rng.normal(0, 0.2, 3)])
+    q[3:7] = quat / np.linalg.norm(quat)
+    q[2] += 1.0   # airborne: no contacts
+    return q, rng.normal(0, 1.0, 27)
+
+
+def _kinetic_energy(o):
+    """0.5 sum_b cvel_b' I_b cvel_b from the com-frame spatial inertias (independent of qM)."""
+    cinert, cvel = o.get("cinert"), o.get("cvel")
+    ke = 0.0
+    for b in range(1, o.M["nbody"]):
+        i, v = cinert[b], cvel[b]
+        I = np.array([[i[0], i[3], i[4]], [i[3], i[1], i[5]], [i[4], i[5], i[2]]])
+        m, c = i[9], i[6:9]
+        w, lin = v[:3], v[3:]
+        # spatial inertia about origin with first moment c = m * com_offset
+        ke += 0.5 * (w @ I @ w + m * lin @ lin + 2 * lin @ np.cross(w, c))
+    return ke
+
+
+def _potential(o):
+    g = np.array(o.m.gravity)     # the (possibly modified) model actually simulated
+    return -sum(o.M["body_mass"][b] * g @ o.get("xipos")[b] for b in range(1, o.M["nbody"]))
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_mass_matrix_matches_kinetic_energy(orc, seed):
+    q, v = _random_state(orc, seed)
+    orc.qpos[:] = q
+    orc.qvel[:] = v
+    orc.forward()
+    M = orc.get("qM")
+    assert np.allclose(M, M.T)
+    assert np.all(np.linalg.eigvalsh(M) > 0)
+    arm = orc.M["dof_armature"]
+    ke_tree = _kinetic_energy(orc)
+    assert 0.5 * v @ (M - np.diag(arm)) @ v == pytest.approx(ke_tree, rel=1e-10)
+
+
+def test_gravity_bias_is_potential_gradient(orc):
+    q, _ = _random_state(orc, 3)
+    orc.qpos[:] = q
+    orc.qvel[:] = 0
+    orc.forward()
+    bias = orc.get("qfrc_bias")
+    eps = 1e-6
+    for dof in range(6, 27):           # hinge dofs: qvel == d qpos / dt
+        qa = 7 + dof - 6
+        vals = []
+        for s in (+1, -1):
+            orc.qpos[:] = q
+            orc.qpos[qa] += s * eps
+            orc.forward()
+            vals.append(_potential(orc))
+        dV = (vals[0] - vals[1]) / (2 * eps)
+        assert bias[dof] == pytest.approx(dV, rel=1e-6, abs=1e-7)
+
+
+def _strip_model(o, gravity=True):
+    m = o.m
+    m.npair = 0
+    for j in range(o.M["njnt"]):
+        m.jnt_limited[j] = 0
+        m.jnt_stiffness[j] = 0
+    for t in range(o.M["ntendon"]):
+        m.tendon_limited[t] = 0
+    for d in range(o.M["nv"]):
+        m.dof_damping[d] = 0
+    if not gravity:
+        for k in range(3):
+            m.gravity[k] = 0
+
+
+def _total_energy(o):
+    """tree kinetic energy + armature kinetic energy + gravitational potential."""
+    return _kinetic_energy(o) + 0.5 * np.sum(o.M["dof_armature"] * o.qvel ** 2) + _potential(o)
+
+
+def test_zero_gravity_energy_error_is_first_order_in_h():
+    """Euler on a configuration-dependent M is not exactly energy-conserving; its energy error
+    over a fixed horizon must shrink linearly with the timestep (integrator consistency)."""
+    from oracle.oracle import Oracle
+    drift = []
+    for h in (0.005, 0.0025, 0.00125):
+        o = Oracle(XML)
+        _strip_model(o, gravity=False)
+        o.m.timestep = h
+        q, v = _random_state(o, 4)
+        o.qpos[:] = q
+        o.qvel[:] = 0.3 * v
+        o.forward()
+        e0 = _total_energy(o)
+        for _ in range(int(round(1.5 / h))):
+            o.step(None, 1)
+        o.forward()
+        drift.append(abs(_total_energy(o) - e0) / e0)
+    assert drift[0] < 1e-2
+    assert 1.6 < drift[0] / drift[1] < 2.5 and 1.6 < drift[1] / drift[2] < 2.5
+
+
+def test_free_fall_energy_bias_is_symplectic_euler(orc):
+    """Under constant gravity semi-implicit Euler loses exactly 0.5*M*g^2*h^2 per step."""
+    _strip_model(orc)
+    q, v = _random_state(orc, 4)
+    orc.qpos[:] = q
+    orc.qvel[:] = 0.3 * v
+    orc.forward()
+    e0 = _total_energy(orc)
+    n = 200
+    for _ in range(n):
+        orc.step(None, 1)
+    orc.forward()
+    h, g, mt = orc.M["opt_timestep"], 9.81, orc.M["body_subtreemass"][0]
+    expect = -n * 0.5 * mt * g * g * h * h
+    assert (_total_energy(orc) - e0) == pytest.approx(expect, rel=0.05)
+
+
+def test_zero_gravity_momentum_error_is_first_order_in_h():
+    """Linear momentum of a free articulated body is conserved by the continuous dynamics; the
+    Euler discretisation must conserve it up to an O(h) error over a fixed horizon."""
+    from oracle.oracle import Oracle
+
+    def momentum(o):
+        o.forward()
+        p = np.zeros(3)
+        for b in range(1, o.M["nbody"]):
+            i, vel = o.get("cinert")[b], o.get("cvel")[b]
+            p += i[9] * vel[3:] - np.cross(i[6:9], vel[:3])
+        return p
+    err = []
+    for h in (0.005, 0.0025, 0.00125):
+        o = Oracle(XML)
+        _strip_model(o, gravity=False)
+        o.m.timestep = h
+        q, v = _random_state(o, 5)
+        o.qpos[:] = q
+        o.qvel[:] = v
+        p0 = momentum(o)
+        for _ in range(int(round(0.5 / h))):
+            o.step(None, 1)
+        err.append(np.abs(momentum(o) - p0).max() / np.abs(p0).max())
+    assert err[0] < 5e-2
+    assert 1.5 < err[0] / err[1] < 2.6 and 1.5 < err[1] / err[2] < 2.6
+
+
+@pytest.mark.parametrize("key", ["squat", "prone", "supine", "stand_on_left_leg"])
+def test_contact_geometry_analytic(orc, key):
+    q = orc.M["keyframes"][key].copy()
+    q[2] -= 0.01   # push slightly into the floor so contacts exist
+    orc.qpos[:] = q
+    orc.forward()
+    cons = orc.contacts()
+    gx, gm = orc.get("geom_xpos"), orc.get("geom_xmat").reshape(-1, 3, 3)
+    found = 0
+    for c in cons:
+        g1, g2 = c["geom"]
+        if orc.M["geom_type"][g1] != 0:
+            continue
+        found += 1
+        r = orc.M["geom_size"][g2][0]
+        if orc.M["geom_type"][g2] == 2:
+            expect = [gx[g2][2] - r]
+        else:
+            ax = gm[g2][:, 2] * orc.M["geom_size"][g2][1]
+            expect = [gx[g2][2] + ax[2] - r, gx[g2][2] - ax[2] - r]
+        assert min(abs(c["dist"] - e) for e in expect) < 1e-12
+        assert np.allclose(c["frame"][:3], [0, 0, 1])
+        assert abs(c["frame"][:3] @ c["frame"][3:6]) < 1e-12 and abs(np.linalg.norm(c["frame"][3:6]) - 1) < 1e-12
+    # every capsule/sphere end below the floor must have produced a contact
+    expect_n = 0
+    for a, b in orc.M["collision_pairs"]:
+        if orc.M["geom_type"][a] != 0:
+            continue
+        r = orc.M["geom_size"][b][0]
+        if orc.M["geom_type"][b] == 2:
+            expect_n += int(gx[b][2] - r <= 0)
+        else:
+            ax = gm[b][:, 2] * orc.M["geom_size"][b][1]
+            expect_n += int(gx[b][2] + ax[2] - r <= 0) + int(gx[b][2] - ax[2] - r <= 0)
+    assert found == expect_n and found > 0
+
+
+@pytest.mark.parametrize("key", ["squat", "prone", "supine"])
+def test_newton_solution_satisfies_kkt(orc, key):
+    q = orc.M["keyframes"][key].copy()
+    q[2] -= 0.005
+    orc.qpos[:] = q
+    orc.qvel[:] = np.random.default_rng(1).normal(0, 0.5, 27)
+    orc.forward()
+    d = orc.d
+    ne, nv = d.nefc, orc.M["nv"]
+    assert ne > 0
+    J = np.ctypeslib.as_array(d.efc_J)[:ne, :nv]
+    aref = np.ctypeslib.as_array(d.efc_aref)[:ne]
+    D = np.ctypeslib.as_array(d.efc_D)[:ne]
+    qacc, qs, M = orc.get("qacc"), orc.get("qacc_smooth"), orc.get("qM")
+    jar = J @ qacc - aref
+    f = np.where(jar < 0, -D * jar, 0.0)
+    assert np.allclose(M @ (qacc - qs), J.T @ f, rtol=1e-9, atol=1e-8 * np.abs(J.T @ f).max())
+    assert np.allclose(np.ctypeslib.as_array(d.efc_force)[:ne], f, rtol=1e-9, atol=1e-9)
+    # dual check: the optimum of the primal is unique -- perturbing qacc raises the cost
+    def cost(x):
+        j = J @ x - aref
+        return 0.5 * (x - qs) @ M @ (x - qs) + 0.5 * np.sum(D * np.minimum(j, 0) ** 2)
+    c0 = cost(qacc)
+    rng = np.random.default_rng(2)
+    for _ in range(20):
+        assert cost(qacc + 1e-4 * rng.normal(size=nv)) >= c0
+
+
+def test_joint_limit_rows_and_impedance(orc):
+    q = orc.M["qpos0"].copy()
+    q[2] += 1.0
+    j = orc.M["jnt_name"].index("knee_right")
+    qa = orc.M["jnt_qposadr"][j]
+    q[qa] = orc.M["jnt_range"][j][0] - 0.005    # 5 mrad past the lower limit
+    orc.qpos[:] = q
+    orc.forward()
+    d = orc.d
+    rows = [r for r in range(d.nefc) if d.efc_type[r] == 3]
+    assert len(rows) == 1 and d.efc_id[rows[0]] == j
+    r = rows[0]
+    J = np.ctypeslib.as_array(d.efc_J)[r, :27]
+    assert J[orc.M["jnt_dofadr"][j]] == 1.0 and np.count_nonzero(J) == 1
+    assert d.efc_pos[r] == pytest.approx(-0.005)
+    # solimplimit "0 .99 .01" with midpoint .5, power 2: x = .5 -> y = .5 -> imp = d0 + .5 (dmax - d0)
+    d0, dmax = 1e-4, 0.99
+    assert d.efc_KBIP[r][2] == pytest.approx(d0 + 0.5 * (dmax - d0))
+
+
+def test_bad_state_autoreset(orc):
+    orc.qpos[:] = orc.M["qpos0"]
+    orc.qpos[10] = np.nan
+    orc.step(None, 1)
+    assert orc.d.warning_badqpos == 1
+    assert orc.time == pytest.approx(0.005)
+    assert np.all(np.isfinite(orc.qpos))
+
+
+def test_oracle_struct_layout_matches_c():
+    from oracle import oracle as O
+    L = O.lib()
+    assert L.orc_sizeof_model() == C.sizeof(O.OrcModel)
+    assert L.orc_sizeof_data() == C.sizeof(O.OrcData)
