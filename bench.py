@@ -1,0 +1,230 @@
+#!/usr/bin/env python
+"""Headline benchmark: humanoid env steps/sec (whole node), 'stand' task -- BASELINE.json metric.
+
+One "step" = one batched env step of every env on the rank: frame_skip=3 physics substeps
+(full mj_step pipeline incl. contacts + Newton solve), the 352-float observation, the device
+stand reward, termination/truncation and auto-reset -- one launch of the fused step kernel.
+Workload (BASELINE.json configs[1]): 4096 humanoid.xml envs per GPU, stand reward,
+frame_skip 3, duration 10; actions come from a pre-generated U(-1,1) action tape already
+resident in HBM (sim-only mode).  N GPUs run N independent env shards (weak scaling, no
+data-path collective).  rank 0 prints one JSON line.
+
+Also reported (extra keys): the rollout mode (MLP[256,256] policy forward + Gaussian sampling
++ env step, all on device), the step-kernel roofline (HBM bytes vs 8 TB/s, measured live with
+HIP events on the launch stream) and the CPU baseline (the reference's n_envs=8
+SubprocVecEnv-style path, run on the oracle's fp64 C restatement of mj_step because MuJoCo is
+not installable: kind "port").
+"""
+import argparse
+import json
+import multiprocessing as mp
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+XML = os.path.join(ROOT, "tests", "golden", "humanoid.xml")
+
+N_ENVS_PER_GPU = 4096
+FRAME_SKIP = 3
+DURATION = 10.0
+# algorithmic HBM bytes per env step of the fused kernel: read qpos 28 + qvel 27
+# + qacc_warmstart 27 + time 1 + action 21 floats; write qpos/qvel/warmstart/time 83 + obs 352
+# + reward 1 floats; + 2 B done flags
+ALGO_BYTES_PER_ENV_STEP = (104 + 436) * 4 + 2
+HBM_PEAK_GBS = 8000.0
+PROFILE_TRAFFIC = os.path.join(ROOT, "profiles", "traffic_step_kernel.json")
+
+
+# ----------------------------------------------------------------------------- CPU baseline
+def _cpu_worker(conn, seed):
+    """SubprocVecEnv._worker equivalent around the fp64 oracle env (train_sb3.py:203)."""
+    from oracle.env import OracleHumanoidEnv
+    env = OracleHumanoidEnv({"model_path": XML, "duration": DURATION, "reward_config": {"type": "stand"},
+                             "frame_skip": FRAME_SKIP})
+    env.reset(seed=seed)
+    while True:
+        cmd, data = conn.recv()
+        if cmd == "step":
+            obs, r, term, trunc, info = env.step(data)
+            if term or trunc:
+                info["terminal_observation"] = obs
+                obs, _ = env.reset()
+            conn.send((obs, r, term or trunc, info))
+        elif cmd == "close":
+            conn.close()
+            return
+
+
+def cpu_baseline(n_envs=8, vec_steps=1500):
+    ctx = mp.get_context("fork")
+    pipes, procs = [], []
+    for i in range(n_envs):
+        a, b = ctx.Pipe()
+        p = ctx.Process(target=_cpu_worker, args=(b, i), daemon=True)
+        p.start()
+        pipes.append(a)
+        procs.append(p)
+    rng = np.random.default_rng(0)
+    acts = rng.uniform(-1, 1, (vec_steps + 20, n_envs, 21)).astype(np.float32)
+
+    def vec_step(k):
+        for i, c in enumerate(pipes):
+            c.send(("step", acts[k, i]))
+        return [c.recv() for c in pipes]
+    for k in range(20):
+        vec_step(k)
+    t = time.perf_counter()
+    for k in range(vec_steps):
+        vec_step(20 + k)
+    dt = time.perf_counter() - t
+    for c in pipes:
+        c.send(("close", None))
+    for p in procs:
+        p.join(timeout=10)
+    return dict(value=n_envs * vec_steps / dt, unit="env_steps/s", cores=n_envs, kind="port",
+                sample=f"{n_envs} worker processes x {vec_steps} env steps (stand, frame_skip 3, U(-1,1) actions, "
+                       f"pipe IPC per step as SB3 SubprocVecEnv) on the fp64 oracle restatement of mj_step; "
+                       f"{dt:.1f} s wall; host nproc={os.cpu_count()}")
+
+
+# ----------------------------------------------------------------------------- GPU
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--envs", type=int, default=N_ENVS_PER_GPU, help="envs per GPU")
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp64"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-rollout", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=25000)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    cpu_res = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu_res = cpu_baseline(vec_steps=args.cpu_steps)   # before any GPU/torch init (fork-safe)
+
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        dist.init_process_group("nccl", device_id=dev)
+
+    from mujocoposelearning_amd.model import HsModel
+    from mujocoposelearning_amd.vec_env import HumanoidVecEnv
+    cfg = {"model_path": XML, "duration": DURATION, "reward_config": {"type": "stand"}, "frame_skip": FRAME_SKIP}
+    model = HsModel(XML)
+    n = args.envs
+    env = HumanoidVecEnv(cfg, n_envs=n, device=local_rank, precision=args.precision, seed=1000 + rank,
+                         model=model)
+    env.reset_tensors()
+    g = torch.Generator(device=dev).manual_seed(rank)
+    tape_len = min(args.steps + args.warmup, 256)
+    tape = (torch.rand(tape_len, n, model.nu, device=dev, generator=g) * 2 - 1).contiguous()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    for k in range(args.warmup):
+        env.step_tensors(tape[k % tape_len])
+    barrier()
+    stream = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for k in range(args.steps):
+        env.step_tensors(tape[(args.warmup + k) % tape_len])
+    ev1.record(stream)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps          # only the step kernel runs in this region
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    total_env_steps = n * args.steps * world
+    value = total_env_steps / elapsed
+    warn = env.batch.warning.sum(0).tolist()
+    aux = env.batch.aux
+    stats = dict(mean_contacts=float(aux[:, 35].float().mean()), mean_rows=float(aux[:, 36].float().mean()),
+                 mean_newton_iters=float(aux[:, 37].float().mean()), warnings=warn)
+
+    # rollout mode: policy MLP[256,256] forward + sampling + env step (on device)
+    rollout = None
+    if not args.no_rollout:
+        from mujocoposelearning_amd.ppo import ActorCritic
+        pol = ActorCritic(env.batch.obs_dim, model.nu, (256, 256)).to(dev)
+        obs = env.batch.obs
+        with torch.no_grad():
+            for k in range(5):
+                a, _, _ = pol.act(obs.float())
+                obs, *_ = env.step_tensors(a.clamp_(-1, 1))
+            barrier()
+            tr0 = time.perf_counter()
+            rs = max(10, args.steps // 2)
+            for k in range(rs):
+                a, _, _ = pol.act(obs.float())
+                obs, *_ = env.step_tensors(a.clamp_(-1, 1))
+            barrier()
+            rel = time.perf_counter() - tr0
+        t = torch.tensor([rel], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        rollout = dict(value=n * rs * world / float(t.item()), unit="env_steps/s",
+                       note="policy MLP[256,256] (pi+vf) forward + diag-Gaussian sample + clip + env step")
+
+    if rank == 0:
+        achieved = ALGO_BYTES_PER_ENV_STEP * n / (kernel_ms * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(PROFILE_TRAFFIC):
+            try:
+                tr = json.load(open(PROFILE_TRAFFIC))
+                if tr.get("n_envs") == n and tr.get("precision") == args.precision:
+                    traffic = tr.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        out = {
+            "metric": "env steps/sec (whole node), humanoid 'stand' task",
+            "value": value,
+            "unit": "env_steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32" if args.precision == "fp32" else "f64",
+            "data": "synthetic (reset distribution of custom_env.py:97-121; U(-1,1) action tape in HBM)",
+            "config": {"workload": "configs[1]: humanoid.xml x 4096 envs per GPU, 'stand' reward, frame_skip 3, "
+                                   "duration 10 (sim-only env steps)",
+                       "n_envs_per_gpu": n, "n_envs_total": n * world, "frame_skip": FRAME_SKIP,
+                       "reward": "stand", "parallelism": f"dp{world} (env shards, no collective)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "step_kernel<float,27>" if args.precision == "fp32" else "step_kernel<double,27>",
+                         "kernel_ms_per_launch": kernel_ms,
+                         "algo_bytes_per_env_step": ALGO_BYTES_PER_ENV_STEP,
+                         "note": "latency/VALU-bound kernel; HBM fraction reported per BASELINE.json"},
+            "cpu_baseline": cpu_res,
+            "rollout": rollout,
+            "sim_stats": stats,
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,225 @@
+"""On-device PPO (PyTorch-ROCm) restating SB3 2.3.2's PPO/MlpPolicy semantics (the reference's
+trainer, train_sb3.py:208-231) so rollouts never leave HBM.
+
+* ActorCritic: separate pi / vf MLPs (net_arch dict, ReLU -- main.py:16,100), diagonal Gaussian
+  with state-independent log_std (init 0), orthogonal init (gain sqrt(2) hidden, 0.01 action
+  head, 1 value head) -- SB3 ActorCriticPolicy defaults.
+* Rollout: n_steps x n_envs on device; actions clipped to the action space before stepping
+  (SB3 collect_rollouts); time-limit truncation bootstraps r += gamma V(terminal_obs).
+* GAE(gamma, lambda) reverse scan; per-minibatch advantage normalisation; clipped surrogate,
+  value MSE (vf_coef 0.5), entropy bonus, clip_grad_norm(max_grad_norm 0.5), Adam(eps 1e-5).
+* Multi-GPU: envs are sharded per rank; each optimizer step all-reduces the flattened gradient
+  bucket ONCE (RCCL over xGMI, ~1.27 MB at [256,256]) and averages it -- no other collective on
+  the data path.
+"""
+from __future__ import annotations
+
+import math
+import time
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+
+def _mlp(inp, sizes, act=nn.ReLU):
+    layers, d = [], inp
+    for s in sizes:
+        layers += [nn.Linear(d, s), act()]
+        d = s
+    return nn.Sequential(*layers), d
+
+
+class ActorCritic(nn.Module):
+    def __init__(self, obs_dim, act_dim, pi=(64, 64), vf=None, activation=nn.ReLU, log_std_init=0.0):
+        super().__init__()
+        vf = pi if vf is None else vf
+        self.pi_net, dp = _mlp(obs_dim, pi, activation)
+        self.vf_net, dv = _mlp(obs_dim, vf, activation)
+        self.action_net = nn.Linear(dp, act_dim)
+        self.value_net = nn.Linear(dv, 1)
+        self.log_std = nn.Parameter(torch.full((act_dim,), float(log_std_init)))
+        for mod, gain in ((self.pi_net, math.sqrt(2)), (self.vf_net, math.sqrt(2)), (self.action_net, 0.01),
+                          (self.value_net, 1.0)):
+            for m in mod.modules() if isinstance(mod, nn.Sequential) else [mod]:
+                if isinstance(m, nn.Linear):
+                    nn.init.orthogonal_(m.weight, gain=gain)
+                    nn.init.zeros_(m.bias)
+
+    def forward(self, obs):
+        return self.action_net(self.pi_net(obs)), self.value_net(self.vf_net(obs)).squeeze(-1)
+
+    def _logp(self, mean, actions):
+        std = self.log_std.exp()
+        z = (actions - mean) / std
+        return (-0.5 * z * z - self.log_std - 0.5 * math.log(2 * math.pi)).sum(-1)
+
+    @torch.no_grad()
+    def act(self, obs, deterministic=False):
+        mean, value = self(obs)
+        a = mean if deterministic else mean + self.log_std.exp() * torch.randn_like(mean)
+        return a, self._logp(mean, a), value
+
+    def evaluate(self, obs, actions):
+        mean, value = self(obs)
+        ent = (0.5 + 0.5 * math.log(2 * math.pi) + self.log_std).sum().expand(obs.shape[0])
+        return self._logp(mean, actions), ent, value
+
+    @torch.no_grad()
+    def value(self, obs):
+        return self.value_net(self.vf_net(obs)).squeeze(-1)
+
+
+def gae(rewards, values, dones, last_values, last_dones, gamma, lam):
+    """SB3 RolloutBuffer.compute_returns_and_advantage: reverse scan over time, vectorised over envs.
+    rewards/values/dones: [T, N] (dones[t] = episode_start flag of step t, as SB3 stores it)."""
+    T = rewards.shape[0]
+    adv = torch.zeros_like(rewards)
+    last = torch.zeros_like(last_values)
+    for t in range(T - 1, -1, -1):
+        if t == T - 1:
+            nonterm = 1.0 - last_dones
+            nv = last_values
+        else:
+            nonterm = 1.0 - dones[t + 1]
+            nv = values[t + 1]
+        delta = rewards[t] + gamma * nv * nonterm - values[t]
+        last = delta + gamma * lam * nonterm * last
+        adv[t] = last
+    return adv, adv + values
+
+
+class PPO:
+    """PPO over a HumanoidVecEnv's device fast path."""
+
+    def __init__(self, env, learning_rate=3e-4, n_steps=2048, batch_size=64, n_epochs=10, gamma=0.99,
+                 gae_lambda=0.95, clip_range=0.2, ent_coef=0.0, vf_coef=0.5, max_grad_norm=0.5,
+                 policy_kwargs=None, seed=0, world_size=1, rank=0):
+        pk = dict(policy_kwargs or {})
+        net = pk.get("net_arch", {"pi": [64, 64], "vf": [64, 64]})
+        if isinstance(net, (list, tuple)):
+            net = {"pi": list(net), "vf": list(net)}
+        act = pk.get("activation_fn", nn.Tanh)
+        if isinstance(act, str):
+            act = getattr(nn, act)
+        self.env = env
+        self.device = env.batch.device
+        torch.manual_seed(seed + rank)
+        self.policy = ActorCritic(env.batch.obs_dim, env.model.nu, net["pi"], net["vf"], act,
+                                  pk.get("log_std_init", 0.0)).to(self.device)
+        self.opt = torch.optim.Adam(self.policy.parameters(), lr=learning_rate, eps=1e-5)
+        self.n_steps, self.batch_size, self.n_epochs = n_steps, batch_size, n_epochs
+        self.gamma, self.gae_lambda, self.clip_range = gamma, gae_lambda, clip_range
+        self.ent_coef, self.vf_coef, self.max_grad_norm = ent_coef, vf_coef, max_grad_norm
+        self.world_size, self.rank = world_size, rank
+        N, T, D, A = env.num_envs, n_steps, env.batch.obs_dim, env.model.nu
+        f, dev = torch.float32, self.device
+        self.buf = dict(obs=torch.zeros(T, N, D, dtype=f, device=dev), act=torch.zeros(T, N, A, dtype=f, device=dev),
+                        rew=torch.zeros(T, N, dtype=f, device=dev), start=torch.zeros(T, N, dtype=f, device=dev),
+                        val=torch.zeros(T, N, dtype=f, device=dev), logp=torch.zeros(T, N, dtype=f, device=dev))
+        self.obs = env.reset_tensors().float().clone()
+        self.episode_start = torch.ones(N, dtype=f, device=dev)
+        self.num_timesteps = 0
+        self.ep_returns = []
+        self.ep_acc = torch.zeros(N, dtype=torch.float64, device=dev)
+        self.flat = [p for p in self.policy.parameters()]
+        self.logger = {}
+
+    def collect_rollouts(self):
+        b, env, pol = self.buf, self.env, self.policy
+        for t in range(self.n_steps):
+            a, logp, v = pol.act(self.obs)
+            b["obs"][t] = self.obs
+            b["act"][t] = a
+            b["val"][t] = v
+            b["logp"][t] = logp
+            b["start"][t] = self.episode_start
+            obs, rew, term, trunc = env.step_tensors(a.clamp(-1.0, 1.0))
+            r = rew.float()
+            done = (term | trunc).float()
+            if bool(trunc.any()):   # SB3 timeout bootstrap: r += gamma * V(terminal_obs)
+                tv = pol.value(env.batch.terminal_obs.float())
+                r = r + self.gamma * tv * (trunc.float() * (1 - term.float()))
+            b["rew"][t] = r
+            self.ep_acc += rew.double()
+            if bool(done.any()):
+                idx = done.bool()
+                self.ep_returns += self.ep_acc[idx].tolist()
+                self.ep_acc[idx] = 0
+            self.obs = obs.float().clone()
+            self.episode_start = done
+        self.num_timesteps += self.n_steps * env.num_envs * self.world_size
+        last_v = pol.value(self.obs)
+        return gae(b["rew"], b["val"], b["start"], last_v, self.episode_start, self.gamma, self.gae_lambda)
+
+    def _allreduce_grads(self):
+        if self.world_size == 1:
+            return
+        import torch.distributed as dist
+        grads = [p.grad for p in self.flat]
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        dist.all_reduce(flat)            # ONE RCCL all-reduce per optimizer step
+        flat /= self.world_size
+        o = 0
+        for g in grads:
+            n = g.numel()
+            g.copy_(flat[o:o + n].view_as(g))
+            o += n
+
+    def train(self, adv, ret):
+        b = self.buf
+        T, N = self.n_steps, self.env.num_envs
+        obs = b["obs"].reshape(T * N, -1)
+        act = b["act"].reshape(T * N, -1)
+        old_logp, old_v = b["logp"].reshape(-1), b["val"].reshape(-1)
+        adv, ret = adv.reshape(-1), ret.reshape(-1)
+        M = T * N
+        stats = []
+        for epoch in range(self.n_epochs):
+            perm = torch.randperm(M, device=self.device)
+            for s in range(0, M, self.batch_size):
+                idx = perm[s:s + self.batch_size]
+                logp, ent, v = self.policy.evaluate(obs[idx], act[idx])
+                a = adv[idx]
+                if a.numel() > 1:
+                    a = (a - a.mean()) / (a.std() + 1e-8)
+                ratio = torch.exp(logp - old_logp[idx])
+                pg = -torch.min(a * ratio, a * ratio.clamp(1 - self.clip_range, 1 + self.clip_range)).mean()
+                vf = torch.nn.functional.mse_loss(ret[idx], v)
+                loss = pg + self.ent_coef * (-ent.mean()) + self.vf_coef * vf
+                self.opt.zero_grad(set_to_none=False)
+                loss.backward()
+                self._allreduce_grads()
+                torch.nn.utils.clip_grad_norm_(self.policy.parameters(), self.max_grad_norm)
+                self.opt.step()
+                stats.append((pg.detach(), vf.detach()))
+        pg = torch.stack([s[0] for s in stats]).mean().item()
+        vf = torch.stack([s[1] for s in stats]).mean().item()
+        return dict(policy_loss=pg, value_loss=vf)
+
+    def learn(self, total_timesteps, callback=None, log_interval=1):
+        it = 0
+        while self.num_timesteps < total_timesteps:
+            t0 = time.perf_counter()
+            adv, ret = self.collect_rollouts()
+            t1 = time.perf_counter()
+            st = self.train(adv, ret)
+            t2 = time.perf_counter()
+            it += 1
+            mean_ret = float(np.mean(self.ep_returns[-100:])) if self.ep_returns else float("nan")
+            self.logger = dict(iteration=it, timesteps=self.num_timesteps, rollout_s=t1 - t0, train_s=t2 - t1,
+                               ep_rew_mean=mean_ret, **st)
+            if callback is not None and callback(self) is False:
+                break
+        return self
+
+    def save(self, path):
+        torch.save({"policy": self.policy.state_dict(), "optimizer": self.opt.state_dict(),
+                    "num_timesteps": self.num_timesteps}, path)
+
+    def load(self, path):
+        ck = torch.load(path, map_location=self.device, weights_only=True)
+        self.policy.load_state_dict(ck["policy"])
+        self.opt.load_state_dict(ck["optimizer"])
+        self.num_timesteps = ck.get("num_timesteps", 0)
+        return self
