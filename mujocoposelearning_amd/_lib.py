@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libhsim.so")
+LIB_PATH = os.environ.get("HSIM_LIB", os.path.join(HERE, "libhsim.so"))   # HSIM_LIB: diagnostic builds
 
 HS_FP32, HS_FP64 = 0, 1
 HS_REWARD_NONE, HS_REWARD_STAND, HS_REWARD_KNEELING, HS_REWARD_WALK = -1, 0, 1, 2

@@ -6,16 +6,19 @@
 //   custom_env.py:232-261  _get_state         (352-dim obs, stale derived fields)
 //   reward_functions.py:66-261 stand / kneeling / walk rewards (device plug-ins)
 //   SB3 SubprocVecEnv auto-reset semantics (train_sb3.py:203)
-// and MuJoCo 3.2.5's mj_step pipeline (custom_env.py:121,160): kinematics, com, CRB, collision,
-// constraint assembly, RNE, actuation, primal Newton solver (pyramidal cones), Euler with
+// and MuJoCo 3.2.5's mj_step pipeline (custom_env.py:121,160): kinematics, com, collision, CRB,
+// RNE, actuation, constraint assembly, primal Newton solver (pyramidal cones), Euler with
 // implicit joint damping.
 //
-// Execution model: ONE WAVEFRONT (64 lanes) PER ENV.  All per-env state lives in LDS; lanes map
-// to bodies / dofs / geom pairs / contacts / constraint rows stage by stage; dense nv x nv
-// matrices (M, Newton Hessian, M + h*B) live row-per-lane in VGPRs and are factored with
-// v_readlane broadcasts (no LDS traffic, no barriers).  The contact part of the Newton
-// Hessian is assembled with the tree-structured "composite" form  H_ij += jp_j' U jp_i, which
-// costs O(nv * ncon) instead of O(nv^2 * nefc).  HBM traffic is only the per-env state in/out.
+// Execution model: TWO ENVS PER WAVEFRONT.  Lanes 0-31 step env 2w, lanes 32-63 env 2w+1; a
+// half-wave maps its 32 lanes to bodies / dofs / geoms / joints / contacts / constraint rows
+// stage by stage (humanoid: 17 bodies, 27 dofs, <= 32 contacts), so a wave64 instruction does
+// useful work for both envs.  Per-env state lives in LDS (phase-local arrays aliased in a union
+// so one wave = 2 envs fits 20 KB: all 4096 envs of configs[1] are resident at once).  Dense
+// nv x nv matrices (M, the Newton Hessian, M + h*B) live row-per-lane in VGPRs and are factored
+// with per-half v_readlane broadcasts.  The contact part of the Newton Hessian uses the
+// tree-structured form H_ij += jp_j' U jp_i (O(nv * ncon), no nefc x nv Jacobian in memory).
+// HBM traffic is only the per-env state in/out; the model is read through L1/L2.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -28,6 +31,16 @@ namespace hs {
 namespace {
 
 constexpr int WAVE = 64;
+constexpr int HL = 32;            // lanes per env
+constexpr int RPL = MAXEFC / HL;  // constraint rows per lane
+
+// scheduling fence: keeps the machine scheduler from hoisting loads across iterations of fully
+// unrolled loops (which otherwise inflates VGPR pressure far past the occupancy target)
+#define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+
+// single-wave workgroup: LDS ops of a wave execute in order; this fence only stops the compiler
+// from reordering LDS accesses across phase boundaries (no s_barrier needed for one wave).
+#define WSYNC() __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup")
 
 // ------------------------------------------------------------------ cross-lane helpers
 __device__ __forceinline__ float rl(float v, int l) {
@@ -38,6 +51,12 @@ __device__ __forceinline__ double rl(double v, int l) {
   int lo = __builtin_amdgcn_readlane((int)(x & 0xffffffffll), l);
   int hi = __builtin_amdgcn_readlane((int)(x >> 32), l);
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// value of sub-lane k (compile-time / uniform) of the caller's half-wave
+template <typename T>
+__device__ __forceinline__ T bc(T v, int k, bool upper) {
+  T a = rl(v, k), b = rl(v, k + HL);
+  return upper ? b : a;
 }
 template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
@@ -52,7 +71,7 @@ __device__ __forceinline__ double dpp(double v) {
 }
 // sum over each 32-lane half (result in every lane of the half)
 template <typename T>
-__device__ __forceinline__ T hsum32(T v) {
+__device__ __forceinline__ T hsum(T v) {
   v += dpp<0xB1>(v);    // quad_perm [1,0,3,2]
   v += dpp<0x4E>(v);    // quad_perm [2,3,0,1]
   v += dpp<0x141>(v);   // row_half_mirror
@@ -60,15 +79,12 @@ __device__ __forceinline__ T hsum32(T v) {
   v += __shfl_xor(v, 16);
   return v;
 }
-template <typename T>
-__device__ __forceinline__ T wsum(T v) {
-  v = hsum32(v);
-  return rl(v, 0) + rl(v, 32);
+__device__ __forceinline__ uint32_t hballot(bool p, bool upper) {
+  uint64_t m = __ballot(p);
+  return upper ? (uint32_t)(m >> 32) : (uint32_t)m;
 }
+__device__ __forceinline__ int below(uint32_t m, int sl) { return __popc(m & ((1u << sl) - 1u)); }
 __device__ __forceinline__ bool bit(uint32_t mask, int i) { return i < 32 && ((mask >> i) & 1u); }
-__device__ __forceinline__ int lanes_below(uint64_t mask, int lane) {
-  return __popcll(mask & ((1ull << lane) - 1ull));
-}
 template <typename T>
 __device__ __forceinline__ bool isbad(T x) {
   return !(x <= T(1e10) && x >= T(-1e10));   // NaN or |x| > mjMAXVAL
@@ -121,7 +137,7 @@ __device__ __forceinline__ void normalize4(T* q) {
   if (n < T(1e-15)) { q[0] = 1; q[1] = q[2] = q[3] = 0; }
   else { T i = T(1) / n; q[0] *= i; q[1] *= i; q[2] *= i; q[3] *= i; }
 }
-// spatial inertia (10-param cinert layout) times motion vector
+// spatial inertia (10-param cinert layout) times motion vector (mju_mulInertVec)
 template <typename T>
 __device__ __forceinline__ void mul_inert(const T* i, const T* v, T* r) {
   r[0] = i[0] * v[0] + i[3] * v[1] + i[4] * v[2] - i[8] * v[4] + i[7] * v[5];
@@ -151,50 +167,51 @@ __device__ __forceinline__ void cross_force(const T* v, const T* f, T* r) {
 }
 
 // ------------------------------------------------------------------ row-per-lane dense algebra
-// Cholesky A = L L' of an NV x NV SPD matrix held row-per-lane (lane i: A[i][0..NV)); lower part
-// is replaced by L.  Upper part of each row becomes scratch.
+// Cholesky A = L L' of an NV x NV SPD matrix held row-per-lane in each half (sub-lane i: row i);
+// the lower part becomes L, the upper part scratch.
 template <int NV, typename T>
-__device__ __forceinline__ void chol_rows(T (&A)[NV], int lane) {
+__device__ __forceinline__ void chol_rows(T (&A)[NV], int sl, bool up) {
 #pragma unroll
   for (int k = 0; k < NV; k++) {
-    T akk = rl(A[k], k);
+    T akk = bc(A[k], k, up);
     T lkk = sqrt(akk > T(1e-30) ? akk : T(1e-30));
-    T inv = T(1) / lkk;
-    T lik = (lane == k) ? lkk : A[k] * inv;
+    T lik = (sl == k) ? lkk : A[k] * (T(1) / lkk);
     A[k] = lik;
 #pragma unroll
-    for (int j = k + 1; j < NV; j++) A[j] -= lik * rl(lik, j);
+    for (int j = k + 1; j < NV; j++) A[j] -= lik * bc(lik, j, up);
+    SCHED_FENCE();
   }
 }
-// solve (L L') x = b; lane i holds b_i; returns x_i
+// solve (L L') x = b; sub-lane i holds b_i; returns x_i
 template <int NV, typename T>
-__device__ __forceinline__ T chol_solve(const T (&L)[NV], T b, int lane) {
+__device__ __forceinline__ T chol_solve(const T (&L)[NV], T b, int sl, bool up) {
 #pragma unroll
   for (int k = 0; k < NV; k++) {
-    T yk = rl(b, k) / rl(L[k], k);
-    b = (lane == k) ? yk : ((lane > k) ? b - L[k] * yk : b);
+    T yk = bc(b, k, up) / bc(L[k], k, up);
+    b = (sl == k) ? yk : ((sl > k) ? b - L[k] * yk : b);
   }
   T x = 0;
 #pragma unroll
   for (int k = NV - 1; k >= 0; k--) {
-    T part = (lane > k && lane < NV) ? L[k] * x : T(0);
-    T ssum = rl(hsum32(part), 0);
-    T xk = (rl(b, k) - ssum) / rl(L[k], k);
-    x = (lane == k) ? xk : x;
+    T part = (sl > k && sl < NV) ? L[k] * x : T(0);
+    T ssum = hsum(part);
+    T xk = (bc(b, k, up) - ssum) / bc(L[k], k, up);
+    x = (sl == k) ? xk : x;
   }
   return x;
 }
-// y = A x for A row-per-lane (full rows)
 template <int NV, typename T>
-__device__ __forceinline__ T matvec_rows(const T (&A)[NV], T x) {
+__device__ __forceinline__ T matvec_rows(const T (&A)[NV], T x, bool up) {
   T acc = 0;
 #pragma unroll
-  for (int j = 0; j < NV; j++) acc += A[j] * rl(x, j);
+  for (int j = 0; j < NV; j++) acc += A[j] * bc(x, j, up);
   return acc;
 }
 
 // ------------------------------------------------------------------ per-env LDS scratch
 enum RowKind { RK_JLO = 0, RK_JHI = 1, RK_TLO = 2, RK_THI = 3, RK_CN = 4, RK_P0 = 5 };   // P0..P0+3: pyramid
+__device__ __forceinline__ int rk_kind(int kid) { return kid >> 16; }
+__device__ __forceinline__ int rk_id(int kid) { return kid & 0xffff; }
 
 template <typename T>
 struct Scratch {
@@ -202,93 +219,33 @@ struct Scratch {
   T qvel[MAXDOF];
   T ctrl[MAXU];
   T vx[MAXDOF];
-  T qfrc_act[MAXDOF];
   T xpos[MAXBODY][3];
-  T xquat[MAXBODY][4];
   T xmat[MAXBODY][9];
-  T xipos[MAXBODY][3];
-  T xanchor[MAXJNT][3];
-  T xaxis[MAXJNT][3];
-  T gpos[MAXGEOM][3];
-  T gax[MAXGEOM][3];
+  T com[4];
   T cinert[MAXBODY][10];
-  T crb[MAXBODY][10];
   T cdof[MAXDOF][6];
-  T cdofdot[MAXDOF][6];
-  T buf[MAXDOF][6];
   T cvel[MAXBODY][6];
-  T bvel[MAXBODY][6];
-  T cfrc[MAXBODY][6];
   T con_pos[MAXCON][3];
   T con_n[MAXCON][3];
   T con_t1[MAXCON][3];
-  T con_t2[MAXCON][3];
   T con_dist[MAXCON];
   T con_v[MAXCON][3];
   T con_U[MAXCON][6];
   T con_F[MAXCON][3];
   int con_pair[MAXCON];
   int con_adr[MAXCON];
-  int row_kind[MAXEFC];
-  int row_id[MAXEFC];
+  int row_kid[MAXEFC];
   T row_D[MAXEFC];
-  T row_aref[MAXEFC];
   T row_f[MAXEFC];
-  T com[4];
-  int ncon, nefc, nlim, niter;
+  int ncon, nefc, nlim, pad;
+  union {   // phase-local arrays (aliased)
+    struct { T xquat[MAXBODY][4]; T xanchor[MAXJNT][3]; T xaxis[MAXJNT][3];
+             T gpos[MAXGEOM][3]; T gax[MAXGEOM][3]; } k;          // kinematics + collision
+    struct { T crb[MAXBODY][10]; T buf[MAXDOF][6]; } c;          // composite rigid body
+    struct { T cdofdot[MAXDOF][6]; T cfrc[MAXBODY][6]; T csub[MAXBODY][6]; } r;   // RNE
+    struct { T bvel[MAXBODY][6]; } n;                             // J x mapping (rows, Newton)
+  } u;
 };
-
-template <typename T>
-struct Env {
-  const DevModel<T>* __restrict__ m;
-  Scratch<T>& s;
-  int lane;
-  int nv, nb;
-};
-
-// ------------------------------------------------------------------ kinematics (mj_kinematics)
-template <typename T>
-__device__ void body_pose(const DevModel<T>* __restrict__ m, Scratch<T>& s, int b) {
-  T pos[3], q[4];
-  int ja = m->body_jntadr[b], jn = m->body_jntnum[b];
-  if (jn == 1 && m->jnt_type[ja] == JNT_FREE) {
-    int qa = m->jnt_qposadr[ja];
-    for (int k = 0; k < 3; k++) pos[k] = s.qpos[qa + k];
-    for (int k = 0; k < 4; k++) q[k] = s.qpos[qa + 3 + k];
-    normalize4(q);
-    for (int k = 0; k < 3; k++) { s.xanchor[ja][k] = pos[k]; s.xaxis[ja][k] = m->jnt_axis[ja][k]; }
-  } else {
-    int p = m->body_parentid[b];
-    T bp[3] = {m->body_pos[b][0], m->body_pos[b][1], m->body_pos[b][2]};
-    T bq[4] = {m->body_quat[b][0], m->body_quat[b][1], m->body_quat[b][2], m->body_quat[b][3]};
-    mv3(s.xmat[p], bp, pos);
-    for (int k = 0; k < 3; k++) pos[k] += s.xpos[p][k];
-    T pq[4] = {s.xquat[p][0], s.xquat[p][1], s.xquat[p][2], s.xquat[p][3]};
-    mulq(pq, bq, q);
-    for (int j = ja; j < ja + jn; j++) {
-      T R[9], ax[3], an[3], jp[3] = {m->jnt_pos[j][0], m->jnt_pos[j][1], m->jnt_pos[j][2]};
-      T la[3] = {m->jnt_axis[j][0], m->jnt_axis[j][1], m->jnt_axis[j][2]};
-      quat2mat(q, R);
-      mv3(R, la, ax);
-      mv3(R, jp, an);
-      for (int k = 0; k < 3; k++) an[k] += pos[k];
-      int qa = m->jnt_qposadr[j];
-      T ang = s.qpos[qa] - m->qpos0[qa];
-      T sn = sin(T(0.5) * ang), cs = cos(T(0.5) * ang);
-      T ql[4] = {cs, la[0] * sn, la[1] * sn, la[2] * sn};
-      mulq(q, ql, q);
-      quat2mat(q, R);
-      T v[3];
-      mv3(R, jp, v);
-      for (int k = 0; k < 3; k++) pos[k] = an[k] - v[k];
-      for (int k = 0; k < 3; k++) { s.xanchor[j][k] = an[k]; s.xaxis[j][k] = ax[k]; }
-    }
-  }
-  normalize4(q);
-  for (int k = 0; k < 4; k++) s.xquat[b][k] = q[k];
-  for (int k = 0; k < 3; k++) s.xpos[b][k] = pos[k];
-  quat2mat(q, s.xmat[b]);
-}
 
 // ------------------------------------------------------------------ narrow phase
 template <typename T>
@@ -330,14 +287,14 @@ __device__ __forceinline__ void make_frame(Con<T>& c) {
   normalize3(c.t1);
 }
 
-// returns number of contacts (0..2) for static pair p
+// number of contacts (0..2) for static pair p (mjc_* primitives)
 template <typename T>
-__device__ int collide_pair(const DevModel<T>* __restrict__ m, const Scratch<T>& s, int p, Con<T>& c0, Con<T>& c1) {
+__device__ __forceinline__ int collide_pair(const DevModel<T>* __restrict__ m, const Scratch<T>& s, int p, Con<T>& c0, Con<T>& c1) {
   int g1 = m->pair_g1[p], g2 = m->pair_g2[p], fn = m->pair_fn[p];
-  const T* p1 = s.gpos[g1];
-  const T* p2 = s.gpos[g2];
-  const T* a1 = s.gax[g1];
-  const T* a2 = s.gax[g2];
+  const T* p1 = s.u.k.gpos[g1];
+  const T* p2 = s.u.k.gpos[g2];
+  const T* a1 = s.u.k.gax[g1];
+  const T* a2 = s.u.k.gax[g2];
   T r1 = m->geom_size[g1][0], r2 = m->geom_size[g2][0], h1 = m->geom_size[g1][1], h2 = m->geom_size[g2][1];
   int n = 0;
   if (fn == PAIR_PLANE_SPHERE) {
@@ -394,9 +351,6 @@ template <typename T>
 __device__ __forceinline__ void store_contact(Scratch<T>& s, int slot, const Con<T>& c, int p) {
   if (slot >= MAXCON) return;
   for (int k = 0; k < 3; k++) { s.con_pos[slot][k] = c.pos[k]; s.con_n[slot][k] = c.n[k]; s.con_t1[slot][k] = c.t1[k]; }
-  T t2[3];
-  cross3(c.n, c.t1, t2);
-  for (int k = 0; k < 3; k++) s.con_t2[slot][k] = t2[k];
   s.con_dist[slot] = c.dist;
   s.con_pair[slot] = p;
 }
@@ -417,43 +371,46 @@ __device__ __forceinline__ T impedance(const T* si, T pos, T margin) {
 }
 
 // ------------------------------------------------------------------ J x for all rows
-// maps s.vx (generalized vector) -> body spatial velocities -> contact frame velocities
+// s.vx (generalized vector) -> body spatial velocities -> contact frame velocities
 template <typename T>
-__device__ void map_vx(const DevModel<T>* __restrict__ m, Scratch<T>& s, int lane, int nv, int nb) {
-  if (lane > 0 && lane < nb) {
-    uint32_t ch = m->body_chainmask[lane];
+__device__ __forceinline__ void map_vx(const DevModel<T>* __restrict__ m, Scratch<T>& s, int sl, int nv, int nb) {
+  if (sl < nb) {
     T v[6] = {0, 0, 0, 0, 0, 0};
-    for (int j = 0; j < nv; j++) {
-      if ((ch >> j) & 1u) {
-        T xj = s.vx[j];
-        for (int k = 0; k < 6; k++) v[k] += s.cdof[j][k] * xj;
+    if (sl > 0) {
+      uint32_t ch = m->body_chainmask[sl];
+      for (int j = 0; j < nv; j++) {
+        if ((ch >> j) & 1u) {
+          T xj = s.vx[j];
+          for (int k = 0; k < 6; k++) v[k] += s.cdof[j][k] * xj;
+        }
       }
     }
-    for (int k = 0; k < 6; k++) s.bvel[lane][k] = v[k];
+    for (int k = 0; k < 6; k++) s.u.n.bvel[sl][k] = v[k];
   }
-  if (lane == 0)
-    for (int k = 0; k < 6; k++) s.bvel[0][k] = 0;
-  __syncthreads();
-  if (lane < s.ncon) {
-    int p = s.con_pair[lane];
+  WSYNC();
+  if (sl < s.ncon) {
+    int p = s.con_pair[sl];
     int b1 = m->pair_b1[p], b2 = m->pair_b2[p];
-    T r[3] = {s.con_pos[lane][0] - s.com[0], s.con_pos[lane][1] - s.com[1], s.con_pos[lane][2] - s.com[2]};
+    T r[3] = {s.con_pos[sl][0] - s.com[0], s.con_pos[sl][1] - s.com[1], s.con_pos[sl][2] - s.com[2]};
     T w[3], v1[3], v2[3];
-    cross3(s.bvel[b2], r, w);
-    for (int k = 0; k < 3; k++) v2[k] = s.bvel[b2][3 + k] + w[k];
-    cross3(s.bvel[b1], r, w);
-    for (int k = 0; k < 3; k++) v1[k] = s.bvel[b1][3 + k] + w[k];
+    cross3(s.u.n.bvel[b2], r, w);
+    for (int k = 0; k < 3; k++) v2[k] = s.u.n.bvel[b2][3 + k] + w[k];
+    cross3(s.u.n.bvel[b1], r, w);
+    for (int k = 0; k < 3; k++) v1[k] = s.u.n.bvel[b1][3 + k] + w[k];
     T dv[3] = {v2[0] - v1[0], v2[1] - v1[1], v2[2] - v1[2]};
-    s.con_v[lane][0] = dot3(s.con_n[lane], dv);
-    s.con_v[lane][1] = dot3(s.con_t1[lane], dv);
-    s.con_v[lane][2] = dot3(s.con_t2[lane], dv);
+    T t2[3];
+    cross3(s.con_n[sl], s.con_t1[sl], t2);
+    s.con_v[sl][0] = dot3(s.con_n[sl], dv);
+    s.con_v[sl][1] = dot3(s.con_t1[sl], dv);
+    s.con_v[sl][2] = dot3(t2, dv);
   }
-  __syncthreads();
+  WSYNC();
 }
 
 template <typename T>
 __device__ __forceinline__ T row_Jx(const DevModel<T>* __restrict__ m, const Scratch<T>& s, int r) {
-  int kind = s.row_kind[r], id = s.row_id[r];
+  int kid = s.row_kid[r];
+  int kind = rk_kind(kid), id = rk_id(kid);
   if (kind <= RK_JHI) {
     T v = s.vx[m->jnt_dofadr[id]];
     return kind == RK_JLO ? v : -v;
@@ -477,43 +434,45 @@ __device__ __forceinline__ void row_u(const DevModel<T>* __restrict__ m, const S
   int sub = kind - RK_P0;
   T mu = m->pair_mu[s.con_pair[c]];
   T sg = (sub & 1) ? -mu : mu;
-  const T* t = (sub >> 1) ? s.con_t2[c] : s.con_t1[c];
+  T t[3];
+  if (sub >> 1) cross3(s.con_n[c], s.con_t1[c], t);
+  else { t[0] = s.con_t1[c][0]; t[1] = s.con_t1[c][1]; t[2] = s.con_t1[c][2]; }
   for (int k = 0; k < 3; k++) u[k] = s.con_n[c][k] + sg * t[k];
 }
 
-// per-contact aggregates from current row forces / activity: U = sum D u u' (active), F = sum f u
+// per-contact aggregates from current row forces: U = sum D u u' (active rows), F = sum f u
 template <typename T>
-__device__ void contact_aggregates(const DevModel<T>* __restrict__ m, Scratch<T>& s, int lane) {
-  if (lane < s.ncon) {
-    int adr = s.con_adr[lane];
-    int nr = m->pair_dim[s.con_pair[lane]] == 1 ? 1 : 4;
+__device__ __forceinline__ void contact_aggregates(const DevModel<T>* __restrict__ m, Scratch<T>& s, int sl) {
+  if (sl < s.ncon) {
+    int adr = s.con_adr[sl];
+    int nr = m->pair_dim[s.con_pair[sl]] == 1 ? 1 : 4;
     T U[6] = {0, 0, 0, 0, 0, 0}, F[3] = {0, 0, 0};
     for (int q = 0; q < nr; q++) {
       int r = adr + q;
       T f = s.row_f[r];
       if (f != T(0)) {
         T u[3];
-        row_u(m, s, s.row_kind[r], lane, u);
+        row_u(m, s, rk_kind(s.row_kid[r]), sl, u);
         T D = s.row_D[r];
         U[0] += D * u[0] * u[0]; U[1] += D * u[1] * u[1]; U[2] += D * u[2] * u[2];
         U[3] += D * u[0] * u[1]; U[4] += D * u[0] * u[2]; U[5] += D * u[1] * u[2];
         for (int k = 0; k < 3; k++) F[k] += f * u[k];
       }
     }
-    for (int k = 0; k < 6; k++) s.con_U[lane][k] = U[k];
-    for (int k = 0; k < 3; k++) s.con_F[lane][k] = F[k];
+    for (int k = 0; k < 6; k++) s.con_U[sl][k] = U[k];
+    for (int k = 0; k < 3; k++) s.con_F[sl][k] = F[k];
   }
-  __syncthreads();
+  WSYNC();
 }
 
-// (J' f)_i for dof lane i (contacts via point Jacobians, limits via sparse rows)
+// (J' f)_i for dof sub-lane i (contacts via point Jacobians, limits via sparse rows)
 template <typename T>
-__device__ T jtf_lane(const DevModel<T>* __restrict__ m, const Scratch<T>& s, int lane, const T* cd) {
+__device__ __forceinline__ T jtf_lane(const DevModel<T>* __restrict__ m, const Scratch<T>& s, int sl, const T* cd) {
   T acc = 0;
   for (int c = 0; c < s.ncon; c++) {
     int p = s.con_pair[c];
     int b1 = m->pair_b1[p], b2 = m->pair_b2[p];
-    int in2 = bit(m->body_chainmask[b2], lane), in1 = b1 ? bit(m->body_chainmask[b1], lane) : 0;
+    int in2 = bit(m->body_chainmask[b2], sl), in1 = b1 ? bit(m->body_chainmask[b1], sl) : 0;
     if (in1 != in2) {
       T r[3] = {s.con_pos[c][0] - s.com[0], s.con_pos[c][1] - s.com[1], s.con_pos[c][2] - s.com[2]};
       T w[3];
@@ -524,70 +483,139 @@ __device__ T jtf_lane(const DevModel<T>* __restrict__ m, const Scratch<T>& s, in
     }
   }
   for (int r = 0; r < s.nlim; r++) {
-    int kind = s.row_kind[r], id = s.row_id[r];
+    int kid = s.row_kid[r];
+    int kind = rk_kind(kid), id = rk_id(kid);
     T f = s.row_f[r];
     if (kind <= RK_JHI) {
-      if (m->jnt_dofadr[id] == lane) acc += kind == RK_JLO ? f : -f;
+      if (m->jnt_dofadr[id] == sl) acc += kind == RK_JLO ? f : -f;
     } else {
       for (int w = 0; w < m->ten_nwrap[id]; w++)
-        if (m->ten_wrapdof[id][w] == lane) acc += (kind == RK_TLO ? f : -f) * m->ten_wrapcoef[id][w];
+        if (m->ten_wrapdof[id][w] == sl) acc += (kind == RK_TLO ? f : -f) * m->ten_wrapcoef[id][w];
     }
   }
   return acc;
 }
 
-// ------------------------------------------------------------------ one mj_step
+// ------------------------------------------------------------------ diagnostic phase timing
+// Built only with -DHS_TIMING (libhsim_timing.so): s_memtime stamps accumulated per phase,
+// summed over waves into dbg[8000 + slot].  The product build compiles them out.
+#ifdef HS_TIMING
+struct PhaseClock {
+  uint64_t acc[16] = {0};
+  uint64_t prev = 0;
+  __device__ __forceinline__ void start() { prev = __builtin_amdgcn_s_memtime(); }
+  __device__ __forceinline__ void stamp(int slot) {
+    uint64_t now = __builtin_amdgcn_s_memtime();
+    acc[slot] += now - prev;
+    prev = now;
+  }
+};
+#define HS_STAMP(clk, slot) (clk).stamp(slot)
+#else
+struct PhaseClock {
+  __device__ __forceinline__ void start() {}
+  __device__ __forceinline__ void stamp(int) {}
+};
+#define HS_STAMP(clk, slot) ((void)0)
+#endif
+
+// ------------------------------------------------------------------ one mj_step (per half-wave)
 template <typename T, int NV>
 struct Stepper {
+  PhaseClock clk;
   const DevModel<T>* __restrict__ m;
   Scratch<T>& s;
-  int lane, nb;
-  T cd[6];        // cdof of this lane's dof (registers)
-  T Mr[NV];       // mass-matrix row of this lane's dof
+  int sl, nb;
+  bool up;        // upper half-wave (second env of the wave)
+  T cd[6];        // cdof of this sub-lane's dof (registers)
+  T Mr[NV];       // mass-matrix row of this sub-lane's dof
   T fsmooth;      // qfrc_smooth_i
   T fcon;         // qfrc_constraint_i
   T qacc;         // solver output qacc_i
+  T qfa;          // qfrc_actuator_i (obs / kneeling reward)
   int niter;
 
-  __device__ Stepper(const DevModel<T>* mm, Scratch<T>& ss, int l) : m(mm), s(ss), lane(l), nb(mm->nbody) {}
+  __device__ Stepper(const DevModel<T>* mm, Scratch<T>& ss, int lane)
+      : m(mm), s(ss), sl(lane & (HL - 1)), nb(mm->nbody), up(lane >= HL) {}
 
-  __device__ void kinematics() {
-    if (lane == 0) {
+  // mj_kinematics + mj_comPos
+  __device__ __forceinline__ void kinematics() {
+    if (sl == 0) {
       for (int k = 0; k < 3; k++) s.xpos[0][k] = 0;
-      s.xquat[0][0] = 1; s.xquat[0][1] = s.xquat[0][2] = s.xquat[0][3] = 0;
+      s.u.k.xquat[0][0] = 1; s.u.k.xquat[0][1] = s.u.k.xquat[0][2] = s.u.k.xquat[0][3] = 0;
       for (int k = 0; k < 9; k++) s.xmat[0][k] = (k % 4 == 0) ? T(1) : T(0);
     }
-    __syncthreads();
-    for (int L = 0; L < m->nlevel; L++) {
-      int a0 = m->level_adr[L], n = m->level_adr[L + 1] - a0;
-      if (lane < n) body_pose(m, s, m->level_body[a0 + lane]);
-      __syncthreads();
+    const int b = sl;
+    const int depth = (b > 0 && b < nb) ? m->body_depth[b] : -1;
+    WSYNC();
+    for (int L = 1; L <= m->nlevel; L++) {
+      if (depth == L) {
+        T pos[3], q[4];
+        int ja = m->body_jntadr[b], jn = m->body_jntnum[b];
+        if (jn == 1 && m->jnt_type[ja] == JNT_FREE) {
+          int qa = m->jnt_qposadr[ja];
+          for (int k = 0; k < 3; k++) pos[k] = s.qpos[qa + k];
+          for (int k = 0; k < 4; k++) q[k] = s.qpos[qa + 3 + k];
+          normalize4(q);
+          for (int k = 0; k < 3; k++) { s.u.k.xanchor[ja][k] = pos[k]; s.u.k.xaxis[ja][k] = m->jnt_axis[ja][k]; }
+        } else {
+          int p = m->body_parentid[b];
+          T bp[3] = {m->body_pos[b][0], m->body_pos[b][1], m->body_pos[b][2]};
+          T bq[4] = {m->body_quat[b][0], m->body_quat[b][1], m->body_quat[b][2], m->body_quat[b][3]};
+          mv3(s.xmat[p], bp, pos);
+          for (int k = 0; k < 3; k++) pos[k] += s.xpos[p][k];
+          T pq[4] = {s.u.k.xquat[p][0], s.u.k.xquat[p][1], s.u.k.xquat[p][2], s.u.k.xquat[p][3]};
+          mulq(pq, bq, q);
+          for (int j = ja; j < ja + jn; j++) {
+            T R[9], ax[3], an[3], jp[3] = {m->jnt_pos[j][0], m->jnt_pos[j][1], m->jnt_pos[j][2]};
+            T la[3] = {m->jnt_axis[j][0], m->jnt_axis[j][1], m->jnt_axis[j][2]};
+            int qa = m->jnt_qposadr[j];
+            T ang = s.qpos[qa] - m->qpos0[qa];
+            quat2mat(q, R);
+            mv3(R, la, ax);
+            mv3(R, jp, an);
+            for (int k = 0; k < 3; k++) an[k] += pos[k];
+            T sn = sin(T(0.5) * ang), cs = cos(T(0.5) * ang);
+            T ql[4] = {cs, la[0] * sn, la[1] * sn, la[2] * sn};
+            mulq(q, ql, q);
+            quat2mat(q, R);
+            T v[3];
+            mv3(R, jp, v);
+            for (int k = 0; k < 3; k++) pos[k] = an[k] - v[k];
+            for (int k = 0; k < 3; k++) { s.u.k.xanchor[j][k] = an[k]; s.u.k.xaxis[j][k] = ax[k]; }
+          }
+        }
+        normalize4(q);
+        for (int k = 0; k < 4; k++) s.u.k.xquat[b][k] = q[k];
+        for (int k = 0; k < 3; k++) s.xpos[b][k] = pos[k];
+        quat2mat(q, s.xmat[b]);
+      }
+      WSYNC();
     }
-    if (lane < m->ngeom) {
-      int b = m->geom_bodyid[lane];
-      T gp[3] = {m->geom_pos[lane][0], m->geom_pos[lane][1], m->geom_pos[lane][2]};
-      T gz[3] = {m->geom_zaxis[lane][0], m->geom_zaxis[lane][1], m->geom_zaxis[lane][2]};
+    if (sl < m->ngeom) {
+      int g = sl, gb = m->geom_bodyid[g];
+      T gp[3] = {m->geom_pos[g][0], m->geom_pos[g][1], m->geom_pos[g][2]};
+      T gz[3] = {m->geom_zaxis[g][0], m->geom_zaxis[g][1], m->geom_zaxis[g][2]};
       T w[3];
-      mv3(s.xmat[b], gp, w);
-      for (int k = 0; k < 3; k++) s.gpos[lane][k] = s.xpos[b][k] + w[k];
-      mv3(s.xmat[b], gz, s.gax[lane]);
+      mv3(s.xmat[gb], gp, w);
+      for (int k = 0; k < 3; k++) s.u.k.gpos[g][k] = s.xpos[gb][k] + w[k];
+      mv3(s.xmat[gb], gz, s.u.k.gax[g]);
     }
-    T mx = 0, my = 0, mz = 0;
-    if (lane > 0 && lane < nb) {
-      T ip[3] = {m->body_ipos[lane][0], m->body_ipos[lane][1], m->body_ipos[lane][2]}, w[3];
-      mv3(s.xmat[lane], ip, w);
-      for (int k = 0; k < 3; k++) s.xipos[lane][k] = s.xpos[lane][k] + w[k];
-      T mb = m->body_mass[lane];
-      mx = mb * s.xipos[lane][0]; my = mb * s.xipos[lane][1]; mz = mb * s.xipos[lane][2];
+    T mx = 0, my = 0, mz = 0, xi[3] = {0, 0, 0};
+    if (b > 0 && b < nb) {
+      T ip[3] = {m->body_ipos[b][0], m->body_ipos[b][1], m->body_ipos[b][2]}, w[3];
+      mv3(s.xmat[b], ip, w);
+      for (int k = 0; k < 3; k++) xi[k] = s.xpos[b][k] + w[k];
+      T mb = m->body_mass[b];
+      mx = mb * xi[0]; my = mb * xi[1]; mz = mb * xi[2];
     }
     // mj_comPos: single kinematic tree -> subtree_com[root] == subtree_com[0] == whole-model COM
     T inv = T(1) / m->total_mass;
-    T c0 = wsum(mx) * inv, c1 = wsum(my) * inv, c2 = wsum(mz) * inv;
-    if (lane == 0) { s.com[0] = c0; s.com[1] = c1; s.com[2] = c2; }
-    __syncthreads();
-    if (lane > 0 && lane < nb) {   // cinert (mju_inertCom)
-      const T* R = s.xmat[lane];
-      const T* I6 = m->body_inert[lane];
+    T c0 = hsum(mx) * inv, c1 = hsum(my) * inv, c2 = hsum(mz) * inv;
+    if (sl == 0) { s.com[0] = c0; s.com[1] = c1; s.com[2] = c2; }
+    if (b > 0 && b < nb) {   // cinert (mju_inertCom)
+      const T* R = s.xmat[b];
+      const T* I6 = m->body_inert[b];
       T I[9] = {I6[0], I6[3], I6[4], I6[3], I6[1], I6[5], I6[4], I6[5], I6[2]};
       T A[9];
       for (int r = 0; r < 3; r++)
@@ -599,9 +627,9 @@ struct Stepper {
       Ic[3] = A[0] * R[3] + A[1] * R[4] + A[2] * R[5];
       Ic[4] = A[0] * R[6] + A[1] * R[7] + A[2] * R[8];
       Ic[5] = A[3] * R[6] + A[4] * R[7] + A[5] * R[8];
-      T d[3] = {s.xipos[lane][0] - c0, s.xipos[lane][1] - c1, s.xipos[lane][2] - c2};
-      T mass = m->body_mass[lane];
-      T* ci = s.cinert[lane];
+      T d[3] = {xi[0] - c0, xi[1] - c1, xi[2] - c2};
+      T mass = m->body_mass[b];
+      T* ci = s.cinert[b];
       ci[0] = Ic[0] + mass * (d[1] * d[1] + d[2] * d[2]);
       ci[1] = Ic[1] + mass * (d[0] * d[0] + d[2] * d[2]);
       ci[2] = Ic[2] + mass * (d[0] * d[0] + d[1] * d[1]);
@@ -610,298 +638,320 @@ struct Stepper {
       ci[5] = Ic[5] - mass * d[1] * d[2];
       ci[6] = mass * d[0]; ci[7] = mass * d[1]; ci[8] = mass * d[2]; ci[9] = mass;
     }
-    if (lane == 0)
+    if (sl == 0)
       for (int k = 0; k < 10; k++) s.cinert[0][k] = 0;
     for (int k = 0; k < 6; k++) cd[k] = 0;
-    if (lane < NV) {   // cdof (mju_dofCom)
-      int j = m->dof_jntid[lane], b = m->dof_bodyid[lane];
-      T off[3] = {c0 - s.xanchor[j][0], c1 - s.xanchor[j][1], c2 - s.xanchor[j][2]};
+    if (sl < NV) {   // cdof (mju_dofCom)
+      int j = m->dof_jntid[sl], db = m->dof_bodyid[sl];
+      T off[3] = {c0 - s.u.k.xanchor[j][0], c1 - s.u.k.xanchor[j][1], c2 - s.u.k.xanchor[j][2]};
       T ax[3];
       bool lin = false;
       if (m->jnt_type[j] == JNT_FREE) {
-        int k = lane - m->jnt_dofadr[j];
-        if (k < 3) { lin = true; cd[3 + k] = 1; }
-        else { int c = k - 3; ax[0] = s.xmat[b][c]; ax[1] = s.xmat[b][3 + c]; ax[2] = s.xmat[b][6 + c]; }
+        int k = sl - m->jnt_dofadr[j];
+        if (k < 3) {   // no dynamic indexing of register arrays (it would demote the Stepper to scratch)
+          lin = true;
+          cd[3] = k == 0 ? T(1) : T(0); cd[4] = k == 1 ? T(1) : T(0); cd[5] = k == 2 ? T(1) : T(0);
+        } else {
+          int c = k - 3;
+          ax[0] = s.xmat[db][c]; ax[1] = s.xmat[db][3 + c]; ax[2] = s.xmat[db][6 + c];
+        }
       } else {
-        ax[0] = s.xaxis[j][0]; ax[1] = s.xaxis[j][1]; ax[2] = s.xaxis[j][2];
+        ax[0] = s.u.k.xaxis[j][0]; ax[1] = s.u.k.xaxis[j][1]; ax[2] = s.u.k.xaxis[j][2];
       }
       if (!lin) {
         cd[0] = ax[0]; cd[1] = ax[1]; cd[2] = ax[2];
         cross3(ax, off, cd + 3);
       }
-      for (int k = 0; k < 6; k++) s.cdof[lane][k] = cd[k];
+      for (int k = 0; k < 6; k++) s.cdof[sl][k] = cd[k];
     }
-    __syncthreads();
+    WSYNC();
   }
 
-  // mj_crb -> Mr rows (registers), buf = crb * cdof
-  __device__ void mass_matrix() {
-    if (lane > 0 && lane < nb) {
-      uint32_t dm = m->body_descmask[lane];
+  // mj_collision: one static pair per sub-lane per pass, ordered compaction into contacts
+  __device__ __forceinline__ int collision() {
+    int ncon = 0;
+    for (int base = 0; base < m->npair; base += HL) {
+      int p = base + sl;
+      Con<T> c0, c1;
+      int n = 0;
+      if (p < m->npair) n = collide_pair(m, s, p, c0, c1);
+      uint32_t m1 = hballot(n >= 1, up), m2 = hballot(n >= 2, up);
+      int pre = below(m1, sl) + below(m2, sl);
+      if (n >= 1) store_contact(s, ncon + pre, c0, p);
+      if (n >= 2) store_contact(s, ncon + pre + 1, c1, p);
+      ncon += __popc(m1) + __popc(m2);
+    }
+    int overflow = ncon > MAXCON;
+    if (overflow) ncon = MAXCON;
+    if (sl == 0) s.ncon = ncon;
+    WSYNC();
+    return overflow;
+  }
+
+  // mj_crb -> Mr rows (registers)
+  __device__ __forceinline__ void mass_matrix() {
+    if (sl > 0 && sl < nb) {
+      uint32_t dm = m->body_descmask[sl];
       T a[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
       for (int c = 1; c < nb; c++)
         if ((dm >> c) & 1u)
           for (int k = 0; k < 10; k++) a[k] += s.cinert[c][k];
-      for (int k = 0; k < 10; k++) s.crb[lane][k] = a[k];
+      for (int k = 0; k < 10; k++) s.u.c.crb[sl][k] = a[k];
     }
-    __syncthreads();
+    WSYNC();
     T bf[6] = {0, 0, 0, 0, 0, 0};
     uint32_t anci = 0;
     T arm = 0;
-    if (lane < NV) {
-      mul_inert(s.crb[m->dof_bodyid[lane]], cd, bf);
-      for (int k = 0; k < 6; k++) s.buf[lane][k] = bf[k];
-      anci = m->dof_ancmask[lane];
-      arm = m->dof_armature[lane];
+    if (sl < NV) {
+      mul_inert(s.u.c.crb[m->dof_bodyid[sl]], cd, bf);
+      for (int k = 0; k < 6; k++) s.u.c.buf[sl][k] = bf[k];
+      anci = m->dof_ancmask[sl];
+      arm = m->dof_armature[sl];
     }
-    __syncthreads();
+    WSYNC();
 #pragma unroll
     for (int j = 0; j < NV; j++) {
       uint32_t ancj = m->dof_ancmask[j];
-      bool rel = (lane < NV) && (bit(anci, j) || bit(ancj, lane));
+      bool rel = (sl < NV) && (bit(anci, j) || bit(ancj, sl));
       T cj[6], bj[6];
-      for (int k = 0; k < 6; k++) { cj[k] = s.cdof[j][k]; bj[k] = s.buf[j][k]; }
-      T v = (j <= lane) ? dot6(cj, bf) : dot6(cd, bj);
-      Mr[j] = rel ? v + ((j == lane) ? arm : T(0)) : T(0);
+      for (int k = 0; k < 6; k++) { cj[k] = s.cdof[j][k]; bj[k] = s.u.c.buf[j][k]; }
+      T v = (j <= sl) ? dot6(cj, bf) : dot6(cd, bj);
+      Mr[j] = rel ? v + ((j == sl) ? arm : T(0)) : T(0);
+      SCHED_FENCE();
     }
+    WSYNC();
   }
 
   // mj_comVel (cvel, cdof_dot), mj_passive, mj_fwdActuation, mj_rne -> fsmooth
-  __device__ void velocity_forces() {
+  __device__ __forceinline__ void velocity_forces() {
     int nv = m->nv;
-    if (lane > 0 && lane < nb) {
-      uint32_t ch = m->body_chainmask[lane];
+    if (sl < nb) {
       T v[6] = {0, 0, 0, 0, 0, 0};
-      for (int j = 0; j < nv; j++)
-        if ((ch >> j) & 1u) {
-          T q = s.qvel[j];
-          for (int k = 0; k < 6; k++) v[k] += s.cdof[j][k] * q;
-        }
-      for (int k = 0; k < 6; k++) s.cvel[lane][k] = v[k];
+      if (sl > 0) {
+        uint32_t ch = m->body_chainmask[sl];
+        for (int j = 0; j < nv; j++)
+          if ((ch >> j) & 1u) {
+            T q = s.qvel[j];
+            for (int k = 0; k < 6; k++) v[k] += s.cdof[j][k] * q;
+          }
+      }
+      for (int k = 0; k < 6; k++) s.cvel[sl][k] = v[k];
     }
-    if (lane == 0)
-      for (int k = 0; k < 6; k++) s.cvel[0][k] = 0;
-    T cdd[6] = {0, 0, 0, 0, 0, 0};
-    if (lane < NV) {
-      uint32_t dm = m->dof_dotmask[lane];
-      T v[6] = {0, 0, 0, 0, 0, 0};
+    if (sl < NV) {
+      uint32_t dm = m->dof_dotmask[sl];
+      T v[6] = {0, 0, 0, 0, 0, 0}, cdd[6];
       for (int j = 0; j < nv; j++)
         if ((dm >> j) & 1u) {
           T q = s.qvel[j];
           for (int k = 0; k < 6; k++) v[k] += s.cdof[j][k] * q;
         }
       cross_motion(v, cd, cdd);
-      for (int k = 0; k < 6; k++) s.cdofdot[lane][k] = cdd[k];
+      for (int k = 0; k < 6; k++) s.u.r.cdofdot[sl][k] = cdd[k];
     }
-    __syncthreads();
-    // RNE: cacc, cfrc_body
-    if (lane > 0 && lane < nb) {
-      uint32_t ch = m->body_chainmask[lane];
+    WSYNC();
+    if (sl > 0 && sl < nb) {   // RNE: cacc, cfrc_body
+      uint32_t ch = m->body_chainmask[sl];
       T a[6] = {0, 0, 0, -m->gravity[0], -m->gravity[1], -m->gravity[2]};
       for (int j = 0; j < nv; j++)
         if ((ch >> j) & 1u) {
           T q = s.qvel[j];
-          for (int k = 0; k < 6; k++) a[k] += s.cdofdot[j][k] * q;
+          for (int k = 0; k < 6; k++) a[k] += s.u.r.cdofdot[j][k] * q;
         }
       T f[6], t[6], t2[6];
-      mul_inert(s.cinert[lane], a, f);
-      mul_inert(s.cinert[lane], s.cvel[lane], t);
-      cross_force(s.cvel[lane], t, t2);
-      for (int k = 0; k < 6; k++) s.cfrc[lane][k] = f[k] + t2[k];
+      mul_inert(s.cinert[sl], a, f);
+      mul_inert(s.cinert[sl], s.cvel[sl], t);
+      cross_force(s.cvel[sl], t, t2);
+      for (int k = 0; k < 6; k++) s.u.r.cfrc[sl][k] = f[k] + t2[k];
     }
-    __syncthreads();
-    if (lane > 0 && lane < nb) {   // subtree sums of cfrc_body
-      uint32_t dm = m->body_descmask[lane];
+    WSYNC();
+    if (sl > 0 && sl < nb) {   // subtree sums of cfrc_body
+      uint32_t dm = m->body_descmask[sl];
       T a[6] = {0, 0, 0, 0, 0, 0};
       for (int c = 1; c < nb; c++)
         if ((dm >> c) & 1u)
-          for (int k = 0; k < 6; k++) a[k] += s.cfrc[c][k];
-      for (int k = 0; k < 6; k++) s.bvel[lane][k] = a[k];
+          for (int k = 0; k < 6; k++) a[k] += s.u.r.cfrc[c][k];
+      for (int k = 0; k < 6; k++) s.u.r.csub[sl][k] = a[k];
     }
-    __syncthreads();
+    WSYNC();
     fsmooth = 0;
-    if (lane < NV) {
-      T bias = dot6(cd, s.bvel[m->dof_bodyid[lane]]);
-      int qa = m->dof_qposadr[lane];
-      T pas = -m->dof_damping[lane] * s.qvel[lane];
-      if (qa >= 0) pas -= m->dof_stiffness[lane] * (s.qpos[qa] - m->dof_springref[lane]);
-      T act = 0;
-      int u = m->dof_actuator[lane];
+    qfa = 0;
+    if (sl < NV) {
+      T bias = dot6(cd, s.u.r.csub[m->dof_bodyid[sl]]);
+      int qa = m->dof_qposadr[sl];
+      T pas = -m->dof_damping[sl] * s.qvel[sl];
+      if (qa >= 0) pas -= m->dof_stiffness[sl] * (s.qpos[qa] - m->dof_springref[sl]);
+      int u = m->dof_actuator[sl];
       if (u >= 0) {
         T c = s.ctrl[u];
         if (m->act_ctrllimited[u]) c = fmin(m->act_ctrlrange[u][1], fmax(m->act_ctrlrange[u][0], c));
-        act = m->act_gear[u] * c;
+        qfa = m->act_gear[u] * c;
       }
-      s.qfrc_act[lane] = act;
-      fsmooth = pas - bias + act;
+      fsmooth = pas - bias + qfa;
     }
-    __syncthreads();
+    WSYNC();
   }
 
-  // mj_collision + mj_makeConstraint + mj_makeImpedance + reference (aref)
-  __device__ int collide_and_rows() {
+  // mj_makeConstraint + mj_makeImpedance + reference (aref); row q of this lane: r = sl + 32 q
+  __device__ __forceinline__ int rows(T (&D)[RPL], T (&ar)[RPL]) {
     int overflow = 0;
-    int ncon = 0;
-    for (int base = 0; base < m->npair; base += WAVE) {
-      int p = base + lane;
-      Con<T> c0, c1;
-      int n = 0;
-      if (p < m->npair) n = collide_pair(m, s, p, c0, c1);
-      uint64_t m1 = __ballot(n >= 1), m2 = __ballot(n >= 2);
-      int pre = lanes_below(m1, lane) + lanes_below(m2, lane);
-      int tot = __popcll(m1) + __popcll(m2);
-      if (n >= 1) store_contact(s, ncon + pre, c0, p);
-      if (n >= 2) store_contact(s, ncon + pre + 1, c1, p);
-      ncon += tot;
-    }
-    if (ncon > MAXCON) { overflow = 1; ncon = MAXCON; }
-    // limit rows: joints (lower side first), then tendons
+    int ncon = s.ncon;
     int nrow = 0;
-    {
+    {   // joint limits (lower side first, MuJoCo side = -1 then +1)
       bool lo = false, hi = false;
-      if (lane < m->njnt && m->jnt_limited[lane]) {
-        T q = s.qpos[m->jnt_qposadr[lane]];
-        lo = (q - m->jnt_range[lane][0]) < m->jnt_margin[lane];
-        hi = (m->jnt_range[lane][1] - q) < m->jnt_margin[lane];
+      if (sl < m->njnt && m->jnt_limited[sl]) {
+        T q = s.qpos[m->jnt_qposadr[sl]];
+        lo = (q - m->jnt_range[sl][0]) < m->jnt_margin[sl];
+        hi = (m->jnt_range[sl][1] - q) < m->jnt_margin[sl];
       }
-      uint64_t ml = __ballot(lo), mh = __ballot(hi);
-      int pre = lanes_below(ml, lane) + lanes_below(mh, lane);
-      if (lo) { s.row_kind[pre] = RK_JLO; s.row_id[pre] = lane; }
-      if (hi) { s.row_kind[pre + lo] = RK_JHI; s.row_id[pre + lo] = lane; }
-      nrow = __popcll(ml) + __popcll(mh);
+      uint32_t ml = hballot(lo, up), mh = hballot(hi, up);
+      int pre = below(ml, sl) + below(mh, sl);
+      if (lo) s.row_kid[pre] = (RK_JLO << 16) | sl;
+      if (hi) s.row_kid[pre + lo] = (RK_JHI << 16) | sl;
+      nrow = __popc(ml) + __popc(mh);
     }
-    {
+    {   // tendon limits
       bool lo = false, hi = false;
-      if (lane < m->ntendon && m->ten_limited[lane]) {
+      if (sl < m->ntendon && m->ten_limited[sl]) {
         T L = 0;
-        for (int w = 0; w < m->ten_nwrap[lane]; w++) L += m->ten_wrapcoef[lane][w] * s.qpos[m->ten_wrapqadr[lane][w]];
-        lo = (L - m->ten_range[lane][0]) < m->ten_margin[lane];
-        hi = (m->ten_range[lane][1] - L) < m->ten_margin[lane];
+        for (int w = 0; w < m->ten_nwrap[sl]; w++) L += m->ten_wrapcoef[sl][w] * s.qpos[m->ten_wrapqadr[sl][w]];
+        lo = (L - m->ten_range[sl][0]) < m->ten_margin[sl];
+        hi = (m->ten_range[sl][1] - L) < m->ten_margin[sl];
       }
-      uint64_t ml = __ballot(lo), mh = __ballot(hi);
-      int pre = nrow + lanes_below(ml, lane) + lanes_below(mh, lane);
-      if (lo) { s.row_kind[pre] = RK_TLO; s.row_id[pre] = lane; }
-      if (hi) { s.row_kind[pre + lo] = RK_THI; s.row_id[pre + lo] = lane; }
-      nrow += __popcll(ml) + __popcll(mh);
+      uint32_t ml = hballot(lo, up), mh = hballot(hi, up);
+      int pre = nrow + below(ml, sl) + below(mh, sl);
+      if (lo) s.row_kid[pre] = (RK_TLO << 16) | sl;
+      if (hi) s.row_kid[pre + lo] = (RK_THI << 16) | sl;
+      nrow += __popc(ml) + __popc(mh);
     }
     int nlim = nrow;
-    {
-      bool isc = lane < ncon;
-      bool pyr = isc && m->pair_dim[s.con_pair[lane]] == 3;
-      uint64_t mc = __ballot(isc), mp = __ballot(pyr);
-      int pre = nrow + lanes_below(mc, lane) + 3 * lanes_below(mp, lane);
-      int tot = __popcll(mc) + 3 * __popcll(mp);
+    {   // contacts: 1 row (condim 1) or 4 pyramid rows (condim 3)
+      bool isc = sl < ncon;
+      bool pyr = isc && m->pair_dim[s.con_pair[sl]] == 3;
+      uint32_t mc = hballot(isc, up), mp = hballot(pyr, up);
+      int pre = nrow + below(mc, sl) + 3 * below(mp, sl);
+      int tot = __popc(mc) + 3 * __popc(mp);
       if (nrow + tot > MAXEFC) {   // drop whole contacts that do not fit (counted as overflow)
         overflow = 1;
-        int fit = 0;
+        int fit = 0, nr = nrow;
         for (int c = 0; c < ncon; c++) {
           int need = (m->pair_dim[s.con_pair[c]] == 3) ? 4 : 1;
-          if (nrow + need > MAXEFC) break;
-          nrow += need;
+          if (nr + need > MAXEFC) break;
+          nr += need;
           fit++;
         }
         ncon = fit;
-        isc = lane < ncon;
-        tot = nrow - nlim;
-        nrow = nlim;
+        isc = sl < ncon;
+        tot = nr - nrow;
       }
       if (isc) {
-        s.con_adr[lane] = pre;
-        if (!pyr) { s.row_kind[pre] = RK_CN; s.row_id[pre] = lane; }
-        else for (int q = 0; q < 4; q++) { s.row_kind[pre + q] = RK_P0 + q; s.row_id[pre + q] = lane; }
+        s.con_adr[sl] = pre;
+        if (!pyr) s.row_kid[pre] = (RK_CN << 16) | sl;
+        else for (int q = 0; q < 4; q++) s.row_kid[pre + q] = ((RK_P0 + q) << 16) | sl;
       }
       nrow += tot;
     }
-    if (lane == 0) { s.ncon = ncon; s.nefc = nrow; s.nlim = nlim; }
-    // velocity of rows for aref uses J qvel: map qvel through J
-    if (lane < NV) s.vx[lane] = s.qvel[lane];
-    __syncthreads();
-    map_vx(m, s, lane, m->nv, nb);
-    for (int r = lane; r < nrow; r += WAVE) {
-      int kind = s.row_kind[r], id = s.row_id[r];
-      T pos, margin, dA;
-      const T *sr, *si;
-      if (kind <= RK_JHI) {
-        T q = s.qpos[m->jnt_qposadr[id]];
-        pos = kind == RK_JLO ? q - m->jnt_range[id][0] : m->jnt_range[id][1] - q;
-        margin = m->jnt_margin[id];
-        sr = m->jnt_solref[id]; si = m->jnt_solimp[id];
-        dA = m->dof_invweight0[m->jnt_dofadr[id]];
-      } else if (kind <= RK_THI) {
-        T L = 0;
-        for (int w = 0; w < m->ten_nwrap[id]; w++) L += m->ten_wrapcoef[id][w] * s.qpos[m->ten_wrapqadr[id][w]];
-        pos = kind == RK_TLO ? L - m->ten_range[id][0] : m->ten_range[id][1] - L;
-        margin = m->ten_margin[id];
-        sr = m->ten_solref[id]; si = m->ten_solimp[id];
-        dA = m->ten_invweight0[id];
-      } else {
-        int p = s.con_pair[id];
-        pos = s.con_dist[id];
-        margin = m->pair_margin[p];
-        sr = m->pair_solref[p]; si = m->pair_solimp[p];
-        T tran = m->body_invweight_tran[m->pair_b1[p]] + m->body_invweight_tran[m->pair_b2[p]];
-        T mu = m->pair_mu[p];
-        dA = kind == RK_CN ? tran : tran + mu * mu * tran;
+    if (sl == 0) { s.ncon = ncon; s.nefc = nrow; s.nlim = nlim; }
+    if (sl < NV) s.vx[sl] = s.qvel[sl];
+    WSYNC();
+    map_vx(m, s, sl, m->nv, nb);     // row velocities J qvel for aref
+#pragma unroll
+    for (int q = 0; q < RPL; q++) {
+      int r = sl + HL * q;
+      D[q] = 0;
+      ar[q] = 0;
+      if (r < nrow) {
+        int kid = s.row_kid[r];
+        int kind = rk_kind(kid), id = rk_id(kid);
+        T pos, margin, dA;
+        const T *sr, *si;
+        if (kind <= RK_JHI) {
+          T qv = s.qpos[m->jnt_qposadr[id]];
+          pos = kind == RK_JLO ? qv - m->jnt_range[id][0] : m->jnt_range[id][1] - qv;
+          margin = m->jnt_margin[id];
+          sr = m->jnt_solref[id]; si = m->jnt_solimp[id];
+          dA = m->dof_invweight0[m->jnt_dofadr[id]];
+        } else if (kind <= RK_THI) {
+          T L = 0;
+          for (int w = 0; w < m->ten_nwrap[id]; w++) L += m->ten_wrapcoef[id][w] * s.qpos[m->ten_wrapqadr[id][w]];
+          pos = kind == RK_TLO ? L - m->ten_range[id][0] : m->ten_range[id][1] - L;
+          margin = m->ten_margin[id];
+          sr = m->ten_solref[id]; si = m->ten_solimp[id];
+          dA = m->ten_invweight0[id];
+        } else {
+          int p = s.con_pair[id];
+          pos = s.con_dist[id];
+          margin = m->pair_margin[p];
+          sr = m->pair_solref[p]; si = m->pair_solimp[p];
+          T tran = m->body_invweight_tran[m->pair_b1[p]] + m->body_invweight_tran[m->pair_b2[p]];
+          T mu = m->pair_mu[p];
+          dA = kind == RK_CN ? tran : tran + mu * mu * tran;
+        }
+        T imp = impedance(si, pos, margin);
+        T dmax = fmin(T(0.9999), fmax(T(0.0001), si[1]));
+        T K, B;
+        if (sr[0] > 0) {
+          T tc = fmax(sr[0], 2 * m->timestep), dr = sr[1];
+          K = T(1) / (dmax * dmax * tc * tc * dr * dr);
+          B = T(2) / (dmax * tc);
+        } else {
+          K = -sr[0] / (dmax * dmax);
+          B = -sr[1] / dmax;
+        }
+        T R = fmax(T(1e-15), (1 - imp) * dA / imp);
+        D[q] = T(1) / R;
+        s.row_D[r] = D[q];
+        ar[q] = -B * row_Jx(m, s, r) - K * imp * (pos - margin);
       }
-      T imp = impedance(si, pos, margin);
-      T dmax = fmin(T(0.9999), fmax(T(0.0001), si[1]));
-      T K, B;
-      if (sr[0] > 0) {
-        T tc = fmax(sr[0], 2 * m->timestep), dr = sr[1];
-        K = T(1) / (dmax * dmax * tc * tc * dr * dr);
-        B = T(2) / (dmax * tc);
-      } else {
-        K = -sr[0] / (dmax * dmax);
-        B = -sr[1] / dmax;
-      }
-      T R = fmax(T(1e-15), (1 - imp) * dA / imp);
-      s.row_D[r] = T(1) / R;
-      T vel = row_Jx(m, s, r);
-      s.row_aref[r] = -B * vel - K * imp * (pos - margin);
     }
-    __syncthreads();
+    WSYNC();
     return overflow;
   }
 
   // primal Newton (mj_solNewton semantics), warm-started; x = qacc
-  __device__ void solve(T xws, int maxit, T tol) {
-    int nv = m->nv;
-    int nefc = s.nefc;
-    T x = lane < NV ? xws : T(0);
-    int r0 = lane, r1 = lane + WAVE;
-    bool v0 = r0 < nefc, v1 = r1 < nefc;
-    T D0 = v0 ? s.row_D[r0] : T(0), D1 = v1 ? s.row_D[r1] : T(0);
-    T ar0 = v0 ? s.row_aref[r0] : T(0), ar1 = v1 ? s.row_aref[r1] : T(0);
-    uint32_t anci = lane < NV ? m->dof_ancmask[lane] : 0u;
-    T scale = m->newton_scale;
-    // jar = J x - aref
-    if (lane < NV) s.vx[lane] = x;
-    __syncthreads();
-    map_vx(m, s, lane, nv, nb);
-    T jar0 = v0 ? row_Jx(m, s, r0) - ar0 : T(0);
-    T jar1 = v1 ? row_Jx(m, s, r1) - ar1 : T(0);
+  __device__ __forceinline__ void solve(T xws, int maxit, T tol, const T (&D)[RPL], const T (&ar)[RPL]) {
+    const int nv = m->nv;
+    const int nefc = s.nefc, nlim = s.nlim, ncon = s.ncon;
+    T x = sl < NV ? xws : T(0);
+    bool vr[RPL];
+#pragma unroll
+    for (int q = 0; q < RPL; q++) vr[q] = sl + HL * q < nefc;
+    const uint32_t anci = sl < NV ? m->dof_ancmask[sl] : 0u;
+    const T scale = m->newton_scale;
+    if (sl < NV) s.vx[sl] = x;
+    WSYNC();
+    map_vx(m, s, sl, nv, nb);
+    T jar[RPL], Js[RPL];
+#pragma unroll
+    for (int q = 0; q < RPL; q++) jar[q] = vr[q] ? row_Jx(m, s, sl + HL * q) - ar[q] : T(0);
+    HS_STAMP(clk, 6);
+    bool done = false;      // this half-wave's solver has converged
     int it = 0;
-    bool done = false;
-    for (; it < maxit && !done; it++) {
-      bool a0 = v0 && jar0 < 0, a1 = v1 && jar1 < 0;
-      if (v0) s.row_f[r0] = a0 ? -D0 * jar0 : T(0);
-      if (v1) s.row_f[r1] = a1 ? -D1 * jar1 : T(0);
-      __syncthreads();
-      contact_aggregates(m, s, lane);
-      T Mx = matvec_rows(Mr, x);
-      T jtf = jtf_lane(m, s, lane, cd);
-      T g = lane < NV ? Mx - fsmooth - jtf : T(0);
-      T gn = sqrt(wsum(g * g));
-      if (scale * gn < tol) break;
-      // Hessian lower rows: M + contact (tree form) + limits (diag) + dense rank-1 rows
+    for (; it < maxit; it++) {
+      bool act[RPL];
+#pragma unroll
+      for (int q = 0; q < RPL; q++) {
+        act[q] = vr[q] && jar[q] < 0;
+        if (vr[q]) s.row_f[sl + HL * q] = act[q] ? -D[q] * jar[q] : T(0);
+      }
+      WSYNC();
+      contact_aggregates(m, s, sl);
+      HS_STAMP(clk, 7);
+      T Mx = matvec_rows(Mr, x, up);
+      T jtf = jtf_lane(m, s, sl, cd);
+      T g = sl < NV ? Mx - fsmooth - jtf : T(0);
+      T gn = sqrt(hsum(g * g));
+      done = done || (scale * gn < tol);
+      HS_STAMP(clk, 8);
+      if (__ballot(!done) == 0) break;       // both envs of the wave converged
+      // Hessian lower rows: M + contact (tree form) + joint limits (diag) + dense rank-1 rows
       T H[NV];
       {
         T aug[6] = {0, 0, 0, 0, 0, 0};
         T dadd = 0;
-        for (int c = 0; c < s.ncon; c++) {
+        for (int c = 0; c < ncon; c++) {
           int p = s.con_pair[c];
           if (m->pair_b1[p] != 0) continue;
-          if (!bit(m->body_chainmask[m->pair_b2[p]], lane)) continue;
+          if (!bit(m->body_chainmask[m->pair_b2[p]], sl)) continue;
           T r[3] = {s.con_pos[c][0] - s.com[0], s.con_pos[c][1] - s.com[1], s.con_pos[c][2] - s.com[2]};
           T w[3];
           cross3(cd, r, w);
@@ -913,108 +963,146 @@ struct Stepper {
           cross3(r, z, rz);
           for (int k = 0; k < 3; k++) { aug[k] += rz[k]; aug[3 + k] += z[k]; }
         }
-        for (int r = 0; r < s.nlim; r++) {
-          int kind = s.row_kind[r];
-          if (kind <= RK_JHI && s.row_f[r] != T(0) && m->jnt_dofadr[s.row_id[r]] == lane) dadd += s.row_D[r];
+        for (int r = 0; r < nlim; r++) {
+          int kid = s.row_kid[r];
+          if (rk_kind(kid) <= RK_JHI && s.row_f[r] != T(0) && m->jnt_dofadr[rk_id(kid)] == sl) dadd += s.row_D[r];
         }
 #pragma unroll
         for (int j = 0; j < NV; j++) {
           T cj[6];
           for (int k = 0; k < 6; k++) cj[k] = s.cdof[j][k];
-          bool rel = bit(anci, j);
-          H[j] = Mr[j] + (rel ? dot6(cj, aug) : T(0)) + ((j == lane) ? dadd : T(0));
+          H[j] = Mr[j] + (bit(anci, j) ? dot6(cj, aug) : T(0)) + ((j == sl) ? dadd : T(0));
+          SCHED_FENCE();
         }
-        // dense rank-1 rows: tendon limits and body-body contacts
-        for (int r = 0; r < nefc; r++) {
-          int kind = s.row_kind[r];
-          if (s.row_f[r] == T(0) || kind <= RK_JHI) continue;
-          T jr = 0;
-          int id = s.row_id[r];
-          if (kind <= RK_THI) {
-            for (int w = 0; w < m->ten_nwrap[id]; w++)
-              if (m->ten_wrapdof[id][w] == lane) jr += m->ten_wrapcoef[id][w];
-            if (kind == RK_THI) jr = -jr;
-          } else {
-            int p = s.con_pair[id];
-            int b1 = m->pair_b1[p];
-            if (b1 == 0) continue;
-            int in2 = bit(m->body_chainmask[m->pair_b2[p]], lane), in1 = bit(m->body_chainmask[b1], lane);
-            if (in1 != in2) {
-              T rr[3] = {s.con_pos[id][0] - s.com[0], s.con_pos[id][1] - s.com[1], s.con_pos[id][2] - s.com[2]};
-              T w[3], u[3];
-              cross3(cd, rr, w);
-              T jp[3] = {cd[3] + w[0], cd[4] + w[1], cd[5] + w[2]};
-              row_u(m, s, kind, id, u);
-              jr = in2 ? dot3(u, jp) : -dot3(u, jp);
+        // dense rank-1 rows (tendon limits, body-body contacts); loop bound = max over both halves
+        int nmax = max(nefc, __shfl_xor(nefc, HL));
+        for (int r = 0; r < nmax; r++) {
+          T jr = 0, Dr = 0;
+          if (r < nefc && s.row_f[r] != T(0)) {
+            int kid = s.row_kid[r];
+            int kind = rk_kind(kid), id = rk_id(kid);
+            if (kind == RK_TLO || kind == RK_THI) {
+              for (int w = 0; w < m->ten_nwrap[id]; w++)
+                if (m->ten_wrapdof[id][w] == sl) jr += m->ten_wrapcoef[id][w];
+              if (kind == RK_THI) jr = -jr;
+              Dr = s.row_D[r];
+            } else if (kind >= RK_CN) {
+              int p = s.con_pair[id];
+              int b1 = m->pair_b1[p];
+              if (b1 != 0) {
+                int in2 = bit(m->body_chainmask[m->pair_b2[p]], sl), in1 = bit(m->body_chainmask[b1], sl);
+                if (in1 != in2) {
+                  T rr[3] = {s.con_pos[id][0] - s.com[0], s.con_pos[id][1] - s.com[1], s.con_pos[id][2] - s.com[2]};
+                  T w[3], u[3];
+                  cross3(cd, rr, w);
+                  T jp[3] = {cd[3] + w[0], cd[4] + w[1], cd[5] + w[2]};
+                  row_u(m, s, kind, id, u);
+                  jr = in2 ? dot3(u, jp) : -dot3(u, jp);
+                }
+                Dr = s.row_D[r];
+              }
             }
           }
-          if (lane >= NV) jr = 0;
-          T dj = s.row_D[r] * jr;
+          if (sl >= NV) jr = 0;
+          if (__ballot(Dr != T(0)) == 0) continue;   // no dense row at this index in either half
+          T dj = Dr * jr;
 #pragma unroll
-          for (int j = 0; j < NV; j++) H[j] += dj * rl(jr, j);
+          for (int j = 0; j < NV; j++) H[j] += dj * bc(jr, j, up);
         }
       }
-      chol_rows<NV>(H, lane);
-      T sdir = -chol_solve<NV>(H, g, lane);
-      if (lane >= NV) sdir = 0;
-      // exact line search along sdir
-      T Ms = matvec_rows(Mr, sdir);
-      T A0 = wsum(lane < NV ? sdir * Ms : T(0));
-      T B0 = wsum(lane < NV ? sdir * (Mx - fsmooth) : T(0));
-      __syncthreads();
-      if (lane < NV) s.vx[lane] = sdir;
-      __syncthreads();
-      map_vx(m, s, lane, nv, nb);
-      T Js0 = v0 ? row_Jx(m, s, r0) : T(0), Js1 = v1 ? row_Jx(m, s, r1) : T(0);
-      T lo = 0, hi = T(1e30), alpha = 1;
-      T d0 = B0 + wsum((a0 ? D0 * jar0 * Js0 : T(0)) + (a1 ? D1 * jar1 * Js1 : T(0)));
-      T ltol = (sizeof(T) == 8 ? T(1e-12) : T(1e-6)) * fabs(d0);
-      for (int ls = 0; ls < 40; ls++) {
-        T j0 = jar0 + alpha * Js0, j1 = jar1 + alpha * Js1;
-        bool b0 = v0 && j0 < 0, b1 = v1 && j1 < 0;
-        T d1 = B0 + alpha * A0 + wsum((b0 ? D0 * j0 * Js0 : T(0)) + (b1 ? D1 * j1 * Js1 : T(0)));
-        if (fabs(d1) <= ltol) break;
-        T d2 = A0 + wsum((b0 ? D0 * Js0 * Js0 : T(0)) + (b1 ? D1 * Js1 * Js1 : T(0)));
-        if (d1 < 0) lo = alpha; else hi = alpha;
-        T an = d2 > 0 ? alpha - d1 / d2 : T(-1);
-        if (!(an > lo && an < hi)) an = hi < T(1e29) ? T(0.5) * (lo + hi) : T(2) * alpha;
-        if (hi - lo <= (sizeof(T) == 8 ? T(1e-15) : T(1e-7)) * hi) break;
-        alpha = an;
+      HS_STAMP(clk, 9);
+      chol_rows<NV>(H, sl, up);
+      T sdir = -chol_solve<NV>(H, g, sl, up);
+      if (sl >= NV) sdir = 0;
+      HS_STAMP(clk, 10);
+      // exact line search along sdir (piecewise-quadratic cost)
+      T Ms = matvec_rows(Mr, sdir, up);
+      T A0 = hsum(sl < NV ? sdir * Ms : T(0));
+      T B0 = hsum(sl < NV ? sdir * (Mx - fsmooth) : T(0));
+      if (sl < NV) s.vx[sl] = sdir;
+      WSYNC();
+      map_vx(m, s, sl, nv, nb);
+#pragma unroll
+      for (int q = 0; q < RPL; q++) Js[q] = vr[q] ? row_Jx(m, s, sl + HL * q) : T(0);
+      // alpha = 1 is exact when no row changes state on [0, 1] (jar is linear in alpha)
+      bool same1 = true;
+#pragma unroll
+      for (int q = 0; q < RPL; q++) same1 = same1 && (!vr[q] || ((jar[q] + Js[q] < 0) == act[q]));
+      bool lsdone = done || (hballot(!same1, up) == 0);
+      T alpha = 1, lo = 0, hi = T(1e30);
+      T d0 = 0;
+      {
+        T c = 0;
+#pragma unroll
+        for (int q = 0; q < RPL; q++) c += act[q] ? D[q] * jar[q] * Js[q] : T(0);
+        d0 = B0 + hsum(c);
       }
-      x += alpha * sdir;
-      T nj0 = jar0 + alpha * Js0, nj1 = jar1 + alpha * Js1;
-      bool changed = ((v0 && ((nj0 < 0) != a0)) || (v1 && ((nj1 < 0) != a1)));
-      jar0 = nj0;
-      jar1 = nj1;
-      uint64_t anychg = __ballot(changed);
-      if (anychg == 0 && fabs(alpha - T(1)) < T(1e-3)) done = true;
-      __syncthreads();
+      const T ltol = (sizeof(T) == 8 ? T(1e-10) : T(1e-5)) * fabs(d0);
+      for (int ls = 0; ls < 30; ls++) {
+        if (__ballot(!lsdone) == 0) break;
+        T c1 = 0, c2 = 0;
+#pragma unroll
+        for (int q = 0; q < RPL; q++) {
+          T jq = jar[q] + alpha * Js[q];
+          bool a = vr[q] && jq < 0;
+          c1 += a ? D[q] * jq * Js[q] : T(0);
+          c2 += a ? D[q] * Js[q] * Js[q] : T(0);
+        }
+        T d1 = B0 + alpha * A0 + hsum(c1);
+        T d2 = A0 + hsum(c2);
+        if (!lsdone) {
+          if (fabs(d1) <= ltol) {
+            lsdone = true;
+          } else {
+            if (d1 < 0) lo = alpha; else hi = alpha;
+            T an = d2 > 0 ? alpha - d1 / d2 : T(-1);
+            if (!(an > lo && an < hi)) an = hi < T(1e29) ? T(0.5) * (lo + hi) : T(2) * alpha;
+            if (hi - lo <= (sizeof(T) == 8 ? T(1e-14) : T(1e-6)) * hi) lsdone = true;
+            else alpha = an;
+          }
+        }
+      }
+      HS_STAMP(clk, 11);
+      if (!done) {
+        x += alpha * sdir;
+        bool changed = false;
+#pragma unroll
+        for (int q = 0; q < RPL; q++) {
+          T nj = jar[q] + alpha * Js[q];
+          changed = changed || (vr[q] && ((nj < 0) != act[q]));
+          jar[q] = nj;
+        }
+        if (hballot(changed, up) == 0 && fabs(alpha - T(1)) < T(1e-3)) done = true;
+      }
+      if (__ballot(!done) == 0) { it++; break; }
     }
     niter = it;
     // final forces -> qfrc_constraint
-    if (v0) s.row_f[r0] = jar0 < 0 ? -D0 * jar0 : T(0);
-    if (v1) s.row_f[r1] = jar1 < 0 ? -D1 * jar1 : T(0);
-    __syncthreads();
-    contact_aggregates(m, s, lane);
-    fcon = lane < NV ? jtf_lane(m, s, lane, cd) : T(0);
+#pragma unroll
+    for (int q = 0; q < RPL; q++)
+      if (vr[q]) s.row_f[sl + HL * q] = jar[q] < 0 ? -D[q] * jar[q] : T(0);
+    WSYNC();
+    contact_aggregates(m, s, sl);
+    fcon = sl < NV ? jtf_lane(m, s, sl, cd) : T(0);
     qacc = x;
-    __syncthreads();
+    WSYNC();
+    HS_STAMP(clk, 12);
   }
 
   // mj_Euler with implicit damping, mj_integratePos
-  __device__ void euler(T& time) {
+  __device__ __forceinline__ void euler(T& time) {
     T h = m->timestep;
     T He[NV];
-    T damp = lane < NV ? m->dof_damping[lane] : T(0);
+    T damp = sl < NV ? m->dof_damping[sl] : T(0);
 #pragma unroll
-    for (int j = 0; j < NV; j++) He[j] = Mr[j] + ((j == lane) ? h * damp : T(0));
-    chol_rows<NV>(He, lane);
-    T a = chol_solve<NV>(He, fsmooth + fcon, lane);
-    if (lane < NV) s.qvel[lane] += h * a;
-    __syncthreads();
-    if (lane < m->njnt) {
-      int qa = m->jnt_qposadr[lane], da = m->jnt_dofadr[lane];
-      if (m->jnt_type[lane] == JNT_FREE) {
+    for (int j = 0; j < NV; j++) He[j] = Mr[j] + ((j == sl) ? h * damp : T(0));
+    chol_rows<NV>(He, sl, up);
+    T a = chol_solve<NV>(He, fsmooth + fcon, sl, up);
+    if (sl < NV) s.qvel[sl] += h * a;
+    WSYNC();
+    if (sl < m->njnt) {
+      int qa = m->jnt_qposadr[sl], da = m->jnt_dofadr[sl];
+      if (m->jnt_type[sl] == JNT_FREE) {
         for (int k = 0; k < 3; k++) s.qpos[qa + k] += h * s.qvel[da + k];
         T w[3] = {s.qvel[da + 3], s.qvel[da + 4], s.qvel[da + 5]};
         T ang = h * normalize3(w);
@@ -1029,7 +1117,7 @@ struct Stepper {
       }
     }
     time += h;
-    __syncthreads();
+    WSYNC();
   }
 };
 
@@ -1048,42 +1136,57 @@ __device__ __forceinline__ T uniform_pm(uint64_t seed, int env, uint32_t episode
 }
 
 template <typename T>
-__device__ void reset_state(const DevModel<T>* __restrict__ m, Scratch<T>& s, int lane, T& time, T& xws) {
-  if (lane < m->nq) s.qpos[lane] = m->qpos0[lane];
-  if (lane < m->nv) s.qvel[lane] = 0;
-  if (lane < m->nu) s.ctrl[lane] = 0;
+__device__ __forceinline__ void reset_state(const DevModel<T>* __restrict__ m, Scratch<T>& s, int sl, T& time, T& xws) {
+  if (sl < m->nq) s.qpos[sl] = m->qpos0[sl];
+  if (sl + HL < m->nq) s.qpos[sl + HL] = m->qpos0[sl + HL];
+  if (sl < m->nv) s.qvel[sl] = 0;
+  if (sl < m->nu) s.ctrl[sl] = 0;
   xws = 0;
   time = 0;
-  __syncthreads();
+  WSYNC();
 }
 
 template <typename T, int NV>
-__device__ void physics_step(Stepper<T, NV>& st, const StepParams& p, T& time, T& xws, int* warn) {
+__device__ __forceinline__ void physics_step(Stepper<T, NV>& st, const StepParams& p, T& time, T& xws, int* warn) {
   const DevModel<T>* __restrict__ m = st.m;
   Scratch<T>& s = st.s;
-  int lane = st.lane;
+  const int sl = st.sl;
+  const bool up = st.up;
   // mj_checkPos / mj_checkVel (auto-reset to qpos0, time 0)
-  bool bq = lane < m->nq && isbad(s.qpos[lane]);
-  bool bv = lane < m->nv && isbad(s.qvel[lane]);
-  if (__ballot(bq)) { warn[WARN_BADQPOS]++; reset_state(m, s, lane, time, xws); }
-  else if (__ballot(bv)) { warn[WARN_BADQVEL]++; reset_state(m, s, lane, time, xws); }
+  bool bq = (sl < m->nq && isbad(s.qpos[sl])) || (sl + HL < m->nq && isbad(s.qpos[sl + HL]));
+  bool bv = sl < m->nv && isbad(s.qvel[sl]);
+  if (hballot(bq, up)) { warn[WARN_BADQPOS]++; reset_state(m, s, sl, time, xws); }
+  else if (hballot(bv, up)) { warn[WARN_BADQVEL]++; reset_state(m, s, sl, time, xws); }
+  T D[RPL], ar[RPL];
   for (int attempt = 0; attempt < 2; attempt++) {
+    HS_STAMP(st.clk, 0);
     st.kinematics();
+    HS_STAMP(st.clk, 1);
+    if (st.collision()) warn[WARN_OVERFLOW]++;
+    HS_STAMP(st.clk, 4);
     st.mass_matrix();
+    HS_STAMP(st.clk, 2);
     st.velocity_forces();
-    if (st.collide_and_rows()) warn[WARN_OVERFLOW]++;
-    st.solve(xws, p.max_newton, sizeof(T) == 8 ? T(1e-13) : T(1e-7));
-    bool ba = lane < m->nv && isbad(st.qacc);
-    if (!__ballot(ba) || attempt == 1) break;
-    warn[WARN_BADQACC]++;   // mj_checkAcc: reset and redo mj_forward
-    reset_state(m, s, lane, time, xws);
+    HS_STAMP(st.clk, 3);
+    if (st.rows(D, ar)) warn[WARN_OVERFLOW]++;
+    HS_STAMP(st.clk, 5);
+    st.solve(xws, p.max_newton, sizeof(T) == 8 ? T(1e-13) : T(1e-7), D, ar);
+    bool ba = sl < m->nv && isbad(st.qacc);
+    bool redo = hballot(ba, up) != 0 && attempt == 0;
+    if (__ballot(redo) == 0) break;          // wave-uniform loop control
+    if (redo) {                               // mj_checkAcc: reset and redo mj_forward
+      warn[WARN_BADQACC]++;
+      reset_state(m, s, sl, time, xws);
+    }
   }
   st.euler(time);
+  HS_STAMP(st.clk, 13);
   xws = st.qacc;
 }
 
 template <typename T>
-__device__ T compute_reward(const DevModel<T>* __restrict__ m, const Scratch<T>& s, const StepParams& p, T time) {
+__device__ __forceinline__ T compute_reward(const DevModel<T>* __restrict__ m, const Scratch<T>& s, const StepParams& p, T time,
+                            T energy_sum) {
   // quaternion_to_euler (utils.py:3-21): pitch = arcsin(2(wy - zx)), not clamped
   T w = s.qpos[3], x = s.qpos[4], y = s.qpos[5], z = s.qpos[6];
   T roll = atan2(2 * (w * x + y * z), 1 - 2 * (x * x + y * y));
@@ -1116,155 +1219,77 @@ __device__ T compute_reward(const DevModel<T>* __restrict__ m, const Scratch<T>&
     T comv = T(0);   // subtree_linvel is lazy in MuJoCo -> 0
     T com = T(0.7) * exp(T(-10) * (dist / T(k[3]))) + T(0.3) * exp(T(-0.1) * comv);
     T foot = T(0);   // min(0,0)/(0+0+1e-8)
-    T jp = 0;
-    for (int i = 6; i < m->nv; i++) { T t = s.qfrc_act[i] * s.qvel[i]; jp += t * t; }
-    T energy = exp(T(-0.01) * jp);
+    T energy = exp(T(-0.01) * energy_sum);
     T alive = 1 - exp(T(-0.5) * time);
     return T(k[5]) * posture + T(k[6]) * com + T(k[7]) * foot + T(k[4]) * energy + T(k[8]) * alive;
   }
   return T(0);
 }
 
+// custom_env.py:232-261 layout; qfrc_actuator comes from registers (sub-lane i holds dof i)
 template <typename T>
-__device__ void write_obs(const DevModel<T>* __restrict__ m, const Scratch<T>& s, int lane, T* out, int obs_dim) {
-  int nq = m->nq, nv = m->nv, nb = m->nbody;
-  int o1 = nq - 2, o2 = o1 + nv, o3 = o2 + 10 * nb, o4 = o3 + 6 * nb;
-  for (int k = lane; k < obs_dim; k += WAVE) {
+__device__ __forceinline__ void write_obs(const DevModel<T>* __restrict__ m, const Scratch<T>& s, int sl, T qfa, T* out,
+                          int obs_dim) {
+  int nq = m->nq, nv = m->nv;
+  int o1 = nq - 2, o2 = o1 + nv, o3 = o2 + 10 * m->nbody, o4 = o3 + 6 * m->nbody;
+  for (int k = sl; k < o4; k += HL) {
     T v;
     if (k < o1) v = s.qpos[2 + k];
     else if (k < o2) v = s.qvel[k - o1];
     else if (k < o3) { int q = k - o2; v = s.cinert[q / 10][q % 10]; }
-    else if (k < o4) { int q = k - o3; v = s.cvel[q / 6][q % 6]; }
-    else v = s.qfrc_act[k - o4];
+    else { int q = k - o3; v = s.cvel[q / 6][q % 6]; }
     out[k] = v;
   }
+  if (sl < nv && o4 + sl < obs_dim) out[o4 + sl] = qfa;
 }
 
 template <typename T, int NV>
 __device__ void dump_debug(const Stepper<T, NV>& st, T* dbg) {
   const Scratch<T>& s = st.s;
-  const DevModel<T>* m = st.m;
-  int lane = st.lane;
-  for (int k = lane; k < MAXBODY * 3; k += WAVE) dbg[k] = s.xpos[k / 3][k % 3];
-  for (int k = lane; k < MAXBODY * 4; k += WAVE) dbg[100 + k] = s.xquat[k / 4][k % 4];
-  for (int k = lane; k < MAXBODY * 10; k += WAVE) dbg[200 + k] = s.cinert[k / 10][k % 10];
-  for (int k = lane; k < MAXDOF * 6; k += WAVE) dbg[500 + k] = s.cdof[k / 6][k % 6];
-  if (lane < NV)
-    for (int j = 0; j < NV; j++) dbg[700 + lane * MAXDOF + j] = st.Mr[j];
-  for (int k = lane; k < MAXBODY * 6; k += WAVE) dbg[1800 + k] = s.cvel[k / 6][k % 6];
-  for (int k = lane; k < MAXDOF * 6; k += WAVE) dbg[2000 + k] = s.cdofdot[k / 6][k % 6];
-  if (lane < NV) {
-    dbg[2280 + lane] = s.qfrc_act[lane];
-    dbg[2320 + lane] = st.fsmooth;
-    dbg[2360 + lane] = st.fcon;
-    dbg[2400 + lane] = st.qacc;
+  int sl = st.sl;
+  for (int k = sl; k < MAXBODY * 3; k += HL) dbg[k] = s.xpos[k / 3][k % 3];
+  for (int k = sl; k < MAXBODY * 10; k += HL) dbg[200 + k] = s.cinert[k / 10][k % 10];
+  for (int k = sl; k < MAXDOF * 6; k += HL) dbg[500 + k] = s.cdof[k / 6][k % 6];
+  if (sl < NV)
+    for (int j = 0; j < NV; j++) dbg[700 + sl * MAXDOF + j] = st.Mr[j];
+  for (int k = sl; k < MAXBODY * 6; k += HL) dbg[1800 + k] = s.cvel[k / 6][k % 6];
+  if (sl < NV) {
+    dbg[2280 + sl] = st.qfa;
+    dbg[2320 + sl] = st.fsmooth;
+    dbg[2360 + sl] = st.fcon;
+    dbg[2400 + sl] = st.qacc;
   }
-  if (lane == 0) {
+  if (sl == 0) {
     dbg[2500] = s.com[0]; dbg[2501] = s.com[1]; dbg[2502] = s.com[2];
     dbg[2503] = s.ncon; dbg[2504] = s.nefc; dbg[2505] = st.niter; dbg[2506] = s.nlim;
   }
-  for (int c = lane; c < s.ncon; c += WAVE) {
+  for (int c = sl; c < s.ncon; c += HL) {
     T* o = dbg + 2600 + 11 * c;
     for (int k = 0; k < 3; k++) { o[k] = s.con_pos[c][k]; o[3 + k] = s.con_n[c][k]; o[6 + k] = s.con_t1[c][k]; }
     o[9] = s.con_dist[c];
     o[10] = s.con_pair[c];
   }
-  for (int r = lane; r < s.nefc; r += WAVE) {
+  for (int r = sl; r < s.nefc; r += HL) {
     T* o = dbg + 3200 + 6 * r;
-    o[0] = s.row_kind[r]; o[1] = s.row_id[r]; o[2] = s.row_D[r]; o[3] = s.row_aref[r]; o[4] = s.row_f[r];
+    o[0] = rk_kind(s.row_kid[r]); o[1] = rk_id(s.row_kid[r]); o[2] = s.row_D[r]; o[4] = s.row_f[r];
   }
-  for (int k = lane; k < MAXGEOM * 3; k += WAVE) { dbg[4000 + k] = s.gpos[k / 3][k % 3]; dbg[4100 + k] = s.gax[k / 3][k % 3]; }
-  for (int k = lane; k < MAXBODY * 3; k += WAVE) dbg[4200 + k] = s.xipos[k / 3][k % 3];
-  (void)m;
 }
 
-// ------------------------------------------------------------------ the kernel
+// per-env commit of state + aux (one half-wave)
 template <typename T, int NV>
-__global__ __launch_bounds__(64) void step_kernel(const DevModel<T>* __restrict__ m, EnvBuffers<T> b,
-                                                  const float* __restrict__ actions,
-                                                  const uint8_t* __restrict__ reset_mask,
-                                                  const T* __restrict__ nz_q, const T* __restrict__ nz_v,
-                                                  StepParams p, int nenv) {
-  __shared__ Scratch<T> s;
-  const int env = blockIdx.x;
-  const int lane = threadIdx.x;
-  if (env >= nenv) return;
-  if (p.mode == MODE_RESET && reset_mask && !reset_mask[env]) return;
-  const int nq = m->nq, nv = m->nv, nu = m->nu;
-  Stepper<T, NV> st(m, s, lane);
-  int warn[NWARN] = {0, 0, 0, 0};
-  T time = b.time[env];
-  T xws = (lane < nv) ? b.qacc_ws[(size_t)env * nv + lane] : T(0);
-  if (lane < nq) s.qpos[lane] = b.qpos[(size_t)env * nq + lane];
-  if (lane < nv) s.qvel[lane] = b.qvel[(size_t)env * nv + lane];
-  if (lane < nu) s.ctrl[lane] = b.ctrl[(size_t)env * nu + lane];
-  __syncthreads();
-
-  bool do_reset = p.mode == MODE_RESET;
-  int step_count = b.step_count[env];
-  uint32_t episode = b.episode[env];
-  T total = b.total_reward[env];
-  if (p.mode == MODE_ENV_STEP || p.mode == MODE_PHYSICS) {
-    for (int sub = 0; sub < p.nsub; sub++) {
-      // data.ctrl[:] = action each substep (custom_env.py:159); mj_resetData may have zeroed it
-      if (lane < nu && actions) s.ctrl[lane] = (T)actions[(size_t)env * nu + lane];
-      __syncthreads();
-      physics_step(st, p, time, xws, warn);
-      if (b.dbg && env == 0) dump_debug(st, b.dbg);
-    }
-    write_obs(m, s, lane, b.obs + (size_t)env * p.obs_dim, p.obs_dim);
-    if (p.mode == MODE_ENV_STEP) {
-      step_count += 1;
-      bool trunc = step_count >= p.max_steps;
-      T r = trunc ? T(0) : compute_reward(m, s, p, time);
-      total += r;
-      bool term = (double)time >= p.duration;
-      if (lane == 0) {
-        b.reward[env] = r;
-        b.terminated[env] = term;
-        b.truncated[env] = trunc;
-      }
-      if ((term || trunc) && p.autoreset) {
-        write_obs(m, s, lane, b.terminal_obs + (size_t)env * p.obs_dim, p.obs_dim);
-        do_reset = true;
-      }
-    }
+__device__ __forceinline__ void commit(const DevModel<T>* __restrict__ m, const EnvBuffers<T>& b, const Stepper<T, NV>& st,
+                       int env, T time, T xws, int step_count, uint32_t episode, T total, const int* warn) {
+  const Scratch<T>& s = st.s;
+  const int sl = st.sl, nq = m->nq, nv = m->nv, nu = m->nu;
+  if (sl < nq) b.qpos[(size_t)env * nq + sl] = s.qpos[sl];
+  if (sl + HL < nq) b.qpos[(size_t)env * nq + sl + HL] = s.qpos[sl + HL];
+  if (sl < nv) {
+    b.qvel[(size_t)env * nv + sl] = s.qvel[sl];
+    b.qacc_ws[(size_t)env * nv + sl] = xws;
+    b.aux[(size_t)env * AUXDIM + sl] = st.qacc;
   }
-  if (do_reset) {
-    // custom_env.py:97-130: mj_resetData; qpos = init (z=1.282, upright); += U(+-0.01) noise with
-    // z noise x0.1 and no quaternion noise; qvel = U(+-0.01); one mj_step with ctrl = 0.
-    episode += 1;
-    T sc = (T)p.noise_scale;
-    if (lane < nq) {
-      T q = m->qpos0[lane];
-      if (m->jnt_type[0] == JNT_FREE) {
-        if (lane == 2) q = (T)p.init_height;
-        if (lane >= 3 && lane < 7) q = lane == 3 ? T(1) : T(0);
-      }
-      T nzq = nz_q ? nz_q[(size_t)env * nq + lane] : uniform_pm<T>(p.seed, env, episode, lane, sc);
-      if (m->jnt_type[0] == JNT_FREE) {
-        if (lane == 2) nzq *= T(0.1);
-        if (lane >= 3 && lane < 7) nzq = 0;
-      }
-      s.qpos[lane] = q + nzq;
-    }
-    if (lane < nv) s.qvel[lane] = nz_v ? nz_v[(size_t)env * nv + lane] : uniform_pm<T>(p.seed, env, episode, 64 + lane, sc);
-    if (lane < nu) s.ctrl[lane] = 0;
-    xws = 0;
-    time = 0;
-    __syncthreads();
-    physics_step(st, p, time, xws, warn);
-    if (b.dbg && env == 0) dump_debug(st, b.dbg);
-    write_obs(m, s, lane, b.obs + (size_t)env * p.obs_dim, p.obs_dim);
-    step_count = 0;
-    total = 0;
-  }
-  // write back state
-  if (lane < nq) b.qpos[(size_t)env * nq + lane] = s.qpos[lane];
-  if (lane < nv) { b.qvel[(size_t)env * nv + lane] = s.qvel[lane]; b.qacc_ws[(size_t)env * nv + lane] = xws; }
-  if (lane < nu) b.ctrl[(size_t)env * nu + lane] = s.ctrl[lane];
-  if (lane < nv) b.aux[(size_t)env * AUXDIM + lane] = st.qacc;
-  if (lane == 0) {
+  if (sl < nu) b.ctrl[(size_t)env * nu + sl] = s.ctrl[sl];
+  if (sl == 0) {
     b.time[env] = time;
     b.step_count[env] = step_count;
     b.episode[env] = episode;
@@ -1276,6 +1301,124 @@ __global__ __launch_bounds__(64) void step_kernel(const DevModel<T>* __restrict_
   }
 }
 
+// ------------------------------------------------------------------ the kernel
+template <typename T, int NV>
+__global__ __launch_bounds__(64, 2) void step_kernel(const DevModel<T>* __restrict__ m, EnvBuffers<T> b,
+                                                  const float* __restrict__ actions,
+                                                  const uint8_t* __restrict__ reset_mask,
+                                                  const T* __restrict__ nz_q, const T* __restrict__ nz_v,
+                                                  StepParams p, int nenv) {
+  __shared__ Scratch<T> smem[2];
+  const int lane = threadIdx.x;
+  const bool up = lane >= HL;
+  const int sl = lane & (HL - 1);
+  const int env_raw = 2 * blockIdx.x + (up ? 1 : 0);
+  bool active = env_raw < nenv;                       // ghost half for odd N
+  const int env = active ? env_raw : nenv - 1;
+  if (p.mode == MODE_RESET && reset_mask && !reset_mask[env]) active = false;
+  if (__ballot(active) == 0) return;                  // wave-uniform exit
+  Scratch<T>& s = smem[up ? 1 : 0];
+  const int nq = m->nq, nv = m->nv, nu = m->nu;
+  Stepper<T, NV> st(m, s, lane);
+  int warn[NWARN] = {0, 0, 0, 0};
+  T time = b.time[env];
+  T xws = (sl < nv) ? b.qacc_ws[(size_t)env * nv + sl] : T(0);
+  if (sl < nq) s.qpos[sl] = b.qpos[(size_t)env * nq + sl];
+  if (sl + HL < nq) s.qpos[sl + HL] = b.qpos[(size_t)env * nq + sl + HL];
+  if (sl < nv) s.qvel[sl] = b.qvel[(size_t)env * nv + sl];
+  if (sl < nu) s.ctrl[sl] = b.ctrl[(size_t)env * nu + sl];
+  WSYNC();
+  st.clk.start();
+  st.qfa = 0;
+  st.qacc = 0;
+  st.niter = 0;
+
+  // Both halves always run the same instruction stream; a half that is inactive (ghost env,
+  // masked reset) or not resetting while its partner resets computes on scratch but commits
+  // nothing (its real state was committed before the shared reset pass).
+  bool do_reset = p.mode == MODE_RESET && active;
+  int step_count = b.step_count[env];
+  uint32_t episode = b.episode[env];
+  T total = b.total_reward[env];
+  T* obs_out = b.obs + (size_t)env * p.obs_dim;
+  const int nsub = (p.mode == MODE_RESET) ? 0 : p.nsub;
+  bool in_reset = false;
+  // One loop, ONE inlined physics_step call site: substeps 0..nsub-1 apply the action; after the
+  // last one the env bookkeeping runs; if any half of the wave must reset, one more substep
+  // runs with the reset state (a half that is not resetting has already committed and computes
+  // on scratch only).
+  for (int sub = 0;; sub++) {
+    if (sub == nsub && !in_reset) {
+      if (nsub > 0) {
+        if (active) write_obs(m, s, sl, st.qfa, obs_out, p.obs_dim);
+        if (p.mode == MODE_ENV_STEP) {
+          step_count += 1;
+          bool trunc = step_count >= p.max_steps;
+          T e = (sl >= 6 && sl < nv) ? st.qfa * s.qvel[sl] : T(0);
+          T esum = hsum(e * e);
+          T r = trunc ? T(0) : compute_reward(m, s, p, time, esum);
+          total += r;
+          bool term = (double)time >= p.duration;
+          if (sl == 0 && active) {
+            b.reward[env] = r;
+            b.terminated[env] = term;
+            b.truncated[env] = trunc;
+          }
+          if ((term || trunc) && p.autoreset && active) {
+            write_obs(m, s, sl, st.qfa, b.terminal_obs + (size_t)env * p.obs_dim, p.obs_dim);
+            do_reset = true;
+          }
+        }
+        if (active && !do_reset) {
+          commit(m, b, st, env, time, xws, step_count, episode, total, warn);
+          active = false;   // committed; a reset pass below is scratch work for this half
+        }
+      }
+      if (__ballot(do_reset) == 0) break;
+      // custom_env.py:97-130: mj_resetData; qpos = init (z=1.282, upright); += U(+-0.01) noise
+      // with z noise x0.1 and no quaternion noise; qvel = U(+-0.01); one mj_step with ctrl = 0.
+      in_reset = true;
+      T sc = (T)p.noise_scale;
+      uint32_t ep = episode + 1;
+      for (int k = sl; k < nq; k += HL) {
+        T q = m->qpos0[k];
+        T nzq = nz_q ? nz_q[(size_t)env * nq + k] : uniform_pm<T>(p.seed, env, ep, k, sc);
+        if (m->jnt_type[0] == JNT_FREE) {
+          if (k == 2) { q = (T)p.init_height; nzq *= T(0.1); }
+          if (k >= 3 && k < 7) { q = k == 3 ? T(1) : T(0); nzq = 0; }
+        }
+        s.qpos[k] = q + nzq;
+      }
+      if (sl < nv) s.qvel[sl] = nz_v ? nz_v[(size_t)env * nv + sl] : uniform_pm<T>(p.seed, env, ep, 64 + sl, sc);
+      if (sl < nu) s.ctrl[sl] = 0;
+      xws = 0;
+      time = 0;
+      episode = ep;
+      WSYNC();
+    } else if (sub > nsub) {
+      if (do_reset && active) {
+        if (b.dbg && env == 0) dump_debug(st, b.dbg);
+        write_obs(m, s, sl, st.qfa, obs_out, p.obs_dim);
+        commit(m, b, st, env, time, xws, 0, episode, T(0), warn);
+      }
+      break;
+    } else {
+      // data.ctrl[:] = action each substep (custom_env.py:159); mj_resetData may have zeroed it
+      if (sl < nu && actions) s.ctrl[sl] = (T)actions[(size_t)env * nu + sl];
+      WSYNC();
+    }
+    physics_step(st, p, time, xws, warn);
+    if (b.dbg && env == 0 && active && !in_reset) dump_debug(st, b.dbg);
+  }
+#ifdef HS_TIMING
+  HS_STAMP(st.clk, 14);
+  if (sl == 0 && b.dbg) {
+    for (int k = 0; k < 15; k++) atomicAdd(&b.dbg[8000 + k], (T)st.clk.acc[k]);
+    atomicAdd(&b.dbg[8015], (T)st.niter);
+  }
+#endif
+}
+
 }  // namespace
 
 template <typename T>
@@ -1283,7 +1426,7 @@ hipError_t launch_step(const DevModel<T>* dmodel, int nv, const EnvBuffers<T>& b
                        const uint8_t* reset_mask, const T* noise_qpos, const T* noise_qvel,
                        const StepParams& p, int nenv, hipStream_t stream) {
   if (nenv <= 0) return hipSuccess;
-  dim3 grid(nenv), block(WAVE);
+  dim3 grid((nenv + 1) / 2), block(WAVE);
   switch (nv) {
     case 27:
       hipLaunchKernelGGL((step_kernel<T, 27>), grid, block, 0, stream, dmodel, b, actions, reset_mask, noise_qpos,

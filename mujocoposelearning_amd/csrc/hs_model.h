@@ -12,17 +12,17 @@
 namespace hs {
 
 // Engine capacity (compile time).  hs_batch_create rejects models that exceed it.
-constexpr int MAXBODY = 24;   // bodies incl. world
+constexpr int MAXBODY = 20;   // bodies incl. world (<= 32: one half-wave lane per body)
 constexpr int MAXDOF = 32;    // <= 32 so dof sets fit a 32-bit mask and one lane per dof
 constexpr int MAXQ = 40;
-constexpr int MAXJNT = 24;
-constexpr int MAXGEOM = 24;
+constexpr int MAXJNT = 24;    // <= 32
+constexpr int MAXGEOM = 24;   // <= 32
 constexpr int MAXTEN = 4;
 constexpr int MAXWRAP = 4;    // joints per fixed tendon
 constexpr int MAXU = 24;
 constexpr int MAXPAIR = 192;  // static candidate geom pairs
-constexpr int MAXCON = 48;    // contacts per env (overflow counted in a warning word)
-constexpr int MAXEFC = 128;   // constraint rows per env (2 per lane)
+constexpr int MAXCON = 32;    // contacts per env (one half-wave lane each; overflow -> warning word)
+constexpr int MAXEFC = 128;   // constraint rows per env (4 per half-wave lane)
 constexpr int MAXLEVEL = 16;
 
 enum GeomType { GEOM_PLANE = 0, GEOM_SPHERE = 2, GEOM_CAPSULE = 3 };
@@ -37,7 +37,7 @@ struct DevModel {
   T newton_scale;                     // 1 / (meaninertia * nv)  (MuJoCo solver scaling)
   T total_mass;
   int level_adr[MAXLEVEL + 1], level_body[MAXBODY];   // bodies grouped by tree depth
-  int body_parentid[MAXBODY], body_jntadr[MAXBODY], body_jntnum[MAXBODY];
+  int body_parentid[MAXBODY], body_jntadr[MAXBODY], body_jntnum[MAXBODY], body_depth[MAXBODY];
   int body_dofadr[MAXBODY], body_dofnum[MAXBODY];
   uint32_t body_chainmask[MAXBODY];   // dofs on the path world -> body (incl. own)
   uint32_t body_descmask[MAXBODY];    // bodies in the subtree rooted at body (incl. self)

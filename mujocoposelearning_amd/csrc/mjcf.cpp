@@ -910,6 +910,7 @@ bool build_dev_model(const HostModel& m, DevModel<T>& d, std::string& err) {
   d.level_adr[maxd] = n;
   for (int b = 0; b < m.nbody; b++) {
     d.body_parentid[b] = m.body_parentid[b];
+    d.body_depth[b] = depth[b];
     d.body_jntadr[b] = m.body_jntadr[b];
     d.body_jntnum[b] = m.body_jntnum[b];
     d.body_dofadr[b] = m.body_dofadr[b];

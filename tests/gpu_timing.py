@@ -1,0 +1,48 @@
+"""Per-phase cycle breakdown of the step kernel (diagnostic build libhsim_timing.so)."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["HSIM_LIB"] = os.path.join(ROOT, "mujocoposelearning_amd", "libhsim_timing.so")
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from mujocoposelearning_amd.batch import HsBatch  # noqa: E402
+from mujocoposelearning_amd.model import HsModel  # noqa: E402
+
+NAMES = ["load", "kinematics", "mass_matrix", "vel+rne", "collision", "rows+aref", "newton:init Jx",
+         "newton:rowf+aggr", "newton:gradient", "newton:hessian", "newton:chol+solve", "newton:linesearch",
+         "newton:final frc", "euler", "obs+writeback"]
+
+
+def main(n=4096, steps=20, prec="fp32"):
+    model = HsModel(os.path.join(ROOT, "tests", "golden", "humanoid.xml"))
+    b = HsBatch(model, n, precision=prec, seed=1)
+    b.configure(frame_skip=3, duration=10.0, reward_id=0)
+    b.reset()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    for k in range(5):
+        b.step(torch.rand(n, 21, device="cuda", generator=g) * 2 - 1)
+    b.set_debug(True)
+    b.t["aux"].zero_()
+    torch.cuda.synchronize()
+    dbg0 = b.get_debug()[8000:8016].copy()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for k in range(steps):
+        b.step(torch.rand(n, 21, device="cuda", generator=g) * 2 - 1)
+    ev1.record()
+    torch.cuda.synchronize()
+    ms = ev0.elapsed_time(ev1) / steps
+    d = b.get_debug()[8000:8016] - dbg0
+    tot = d[:15].sum()
+    per = d[:15] / (n * steps * 3)
+    print(f"[{prec}] N={n}: {ms:.3f} ms/launch; cycles per env-substep (wave lifetime) {tot / (n * steps * 3):,.0f}; "
+          f"newton iters/substep {d[15] / (n * steps):.2f}")
+    for name, c, f in zip(NAMES, per, d[:15] / tot):
+        print(f"  {name:20s} {c:10,.0f} cyc  {100 * f:5.1f}%")
+
+
+if __name__ == "__main__":
+    main(prec=sys.argv[1] if len(sys.argv) > 1 else "fp32")

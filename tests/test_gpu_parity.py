@@ -102,9 +102,12 @@ def test_stage_dump_fp64(model):
               ("cdof", dbg[500:500 + nv * 6].reshape(nv, 6), o.get("cdof")),
               ("qM", dbg[700:700 + 1024].reshape(32, 32)[:nv, :nv], o.get("qM")),
               ("cvel", dbg[1800:1800 + nb * 6].reshape(nb, 6), o.get("cvel")),
-              ("cdof_dot", dbg[2000:2000 + nv * 6].reshape(nv, 6), o.get("cdof_dot")),
+              ("qfrc_actuator", dbg[2280:2280 + nv], o.get("qfrc_actuator")),
               ("qfrc_smooth", dbg[2320:2320 + nv], o.get("qfrc_smooth")),
-              ("qfrc_constraint", dbg[2360:2360 + nv], o.get("qfrc_constraint"))]
+              ("qfrc_constraint", dbg[2360:2360 + nv], o.get("qfrc_constraint")),
+              ("qacc", dbg[2400:2400 + nv], o.get("qacc"))]
+    # cdof_dot / cfrc live in a phase-aliased LDS union and are gone by dump time; the
+    # smooth-force check above covers them (qfrc_bias = RNE over cdof_dot and cfrc).
     for name, g, r in checks:
         assert np.abs(g - r).max() <= 1e-9 * (1 + np.abs(r).max()), name
 
