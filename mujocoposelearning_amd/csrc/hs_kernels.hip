@@ -83,6 +83,20 @@ __device__ __forceinline__ uint32_t hballot(bool p, bool upper) {
   uint64_t m = __ballot(p);
   return upper ? (uint32_t)(m >> 32) : (uint32_t)m;
 }
+// Hide a (uniform) pointer's value from the optimiser.  The model pointer is const __restrict__,
+// so without this LICM hoists every per-lane model load (m->dof_bodyid[sl], ...) out of the
+// substep / Newton loops and keeps each one live in a VGPR for the whole kernel.
+template <typename P>
+__device__ __forceinline__ P* opaque(P* p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+// Same for a per-lane value: stops lane-invariant compare masks (j <= sl, bit(mask, sl), ...)
+// being hoisted out of the loops as dozens of 64-bit SGPR masks (which then spill).
+__device__ __forceinline__ int opaque_v(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
 __device__ __forceinline__ int below(uint32_t m, int sl) { return __popc(m & ((1u << sl) - 1u)); }
 __device__ __forceinline__ bool bit(uint32_t mask, int i) { return i < 32 && ((mask >> i) & 1u); }
 template <typename T>
@@ -523,7 +537,7 @@ struct PhaseClock {
 template <typename T, int NV>
 struct Stepper {
   PhaseClock clk;
-  const DevModel<T>* __restrict__ m;
+  const DevModel<T>* m;
   Scratch<T>& s;
   int sl, nb;
   bool up;        // upper half-wave (second env of the wave)
@@ -538,8 +552,15 @@ struct Stepper {
   __device__ Stepper(const DevModel<T>* mm, Scratch<T>& ss, int lane)
       : m(mm), s(ss), sl(lane & (HL - 1)), nb(mm->nbody), up(lane >= HL) {}
 
+  // start of a pipeline phase: nothing lane-invariant is carried over from the previous phase
+  __device__ __forceinline__ void phase_begin() {
+    m = opaque(m);
+    sl = opaque_v(sl);
+  }
+
   // mj_kinematics + mj_comPos
   __device__ __forceinline__ void kinematics() {
+    phase_begin();
     if (sl == 0) {
       for (int k = 0; k < 3; k++) s.xpos[0][k] = 0;
       s.u.k.xquat[0][0] = 1; s.u.k.xquat[0][1] = s.u.k.xquat[0][2] = s.u.k.xquat[0][3] = 0;
@@ -669,6 +690,7 @@ struct Stepper {
 
   // mj_collision: one static pair per sub-lane per pass, ordered compaction into contacts
   __device__ __forceinline__ int collision() {
+    phase_begin();
     int ncon = 0;
     for (int base = 0; base < m->npair; base += HL) {
       int p = base + sl;
@@ -690,6 +712,7 @@ struct Stepper {
 
   // mj_crb -> Mr rows (registers)
   __device__ __forceinline__ void mass_matrix() {
+    phase_begin();
     if (sl > 0 && sl < nb) {
       uint32_t dm = m->body_descmask[sl];
       T a[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -724,6 +747,7 @@ struct Stepper {
 
   // mj_comVel (cvel, cdof_dot), mj_passive, mj_fwdActuation, mj_rne -> fsmooth
   __device__ __forceinline__ void velocity_forces() {
+    phase_begin();
     int nv = m->nv;
     if (sl < nb) {
       T v[6] = {0, 0, 0, 0, 0, 0};
@@ -793,6 +817,7 @@ struct Stepper {
 
   // mj_makeConstraint + mj_makeImpedance + reference (aref); row q of this lane: r = sl + 32 q
   __device__ __forceinline__ int rows(T (&D)[RPL], T (&ar)[RPL]) {
+    phase_begin();
     int overflow = 0;
     int ncon = s.ncon;
     int nrow = 0;
@@ -909,6 +934,7 @@ struct Stepper {
 
   // primal Newton (mj_solNewton semantics), warm-started; x = qacc
   __device__ __forceinline__ void solve(T xws, int maxit, T tol, const T (&D)[RPL], const T (&ar)[RPL]) {
+    phase_begin();
     const int nv = m->nv;
     const int nefc = s.nefc, nlim = s.nlim, ncon = s.ncon;
     T x = sl < NV ? xws : T(0);
@@ -927,6 +953,8 @@ struct Stepper {
     bool done = false;      // this half-wave's solver has converged
     int it = 0;
     for (; it < maxit; it++) {
+      m = opaque(m);
+      sl = opaque_v(sl);
       bool act[RPL];
 #pragma unroll
       for (int q = 0; q < RPL; q++) {
@@ -1091,6 +1119,7 @@ struct Stepper {
 
   // mj_Euler with implicit damping, mj_integratePos
   __device__ __forceinline__ void euler(T& time) {
+    phase_begin();
     T h = m->timestep;
     T He[NV];
     T damp = sl < NV ? m->dof_damping[sl] : T(0);
@@ -1244,7 +1273,7 @@ __device__ __forceinline__ void write_obs(const DevModel<T>* __restrict__ m, con
 }
 
 template <typename T, int NV>
-__device__ void dump_debug(const Stepper<T, NV>& st, T* dbg) {
+__device__ __forceinline__ void dump_debug(const Stepper<T, NV>& st, T* dbg) {
   const Scratch<T>& s = st.s;
   int sl = st.sl;
   for (int k = sl; k < MAXBODY * 3; k += HL) dbg[k] = s.xpos[k / 3][k % 3];
@@ -1348,15 +1377,17 @@ __global__ __launch_bounds__(64, 2) void step_kernel(const DevModel<T>* __restri
   // runs with the reset state (a half that is not resetting has already committed and computes
   // on scratch only).
   for (int sub = 0;; sub++) {
+    st.m = opaque(st.m);
+    st.sl = opaque_v(st.sl);
     if (sub == nsub && !in_reset) {
       if (nsub > 0) {
-        if (active) write_obs(m, s, sl, st.qfa, obs_out, p.obs_dim);
+        if (active) write_obs(st.m, s, sl, st.qfa, obs_out, p.obs_dim);
         if (p.mode == MODE_ENV_STEP) {
           step_count += 1;
           bool trunc = step_count >= p.max_steps;
           T e = (sl >= 6 && sl < nv) ? st.qfa * s.qvel[sl] : T(0);
           T esum = hsum(e * e);
-          T r = trunc ? T(0) : compute_reward(m, s, p, time, esum);
+          T r = trunc ? T(0) : compute_reward(st.m, s, p, time, esum);
           total += r;
           bool term = (double)time >= p.duration;
           if (sl == 0 && active) {
@@ -1365,12 +1396,12 @@ __global__ __launch_bounds__(64, 2) void step_kernel(const DevModel<T>* __restri
             b.truncated[env] = trunc;
           }
           if ((term || trunc) && p.autoreset && active) {
-            write_obs(m, s, sl, st.qfa, b.terminal_obs + (size_t)env * p.obs_dim, p.obs_dim);
+            write_obs(st.m, s, sl, st.qfa, b.terminal_obs + (size_t)env * p.obs_dim, p.obs_dim);
             do_reset = true;
           }
         }
         if (active && !do_reset) {
-          commit(m, b, st, env, time, xws, step_count, episode, total, warn);
+          commit(st.m, b, st, env, time, xws, step_count, episode, total, warn);
           active = false;   // committed; a reset pass below is scratch work for this half
         }
       }
@@ -1398,8 +1429,8 @@ __global__ __launch_bounds__(64, 2) void step_kernel(const DevModel<T>* __restri
     } else if (sub > nsub) {
       if (do_reset && active) {
         if (b.dbg && env == 0) dump_debug(st, b.dbg);
-        write_obs(m, s, sl, st.qfa, obs_out, p.obs_dim);
-        commit(m, b, st, env, time, xws, 0, episode, T(0), warn);
+        write_obs(st.m, s, sl, st.qfa, obs_out, p.obs_dim);
+        commit(st.m, b, st, env, time, xws, 0, episode, T(0), warn);
       }
       break;
     } else {
