@@ -101,7 +101,7 @@ def main():
     ap.add_argument("--precision", default="fp32", choices=["fp32", "fp64"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-rollout", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=25000)
+    ap.add_argument("--cpu-steps", type=int, default=60000, help="vec steps of the CPU baseline (~13 s)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -195,7 +195,7 @@ def main():
             except Exception:
                 traffic = None
         out = {
-            "metric": "env steps/sec (whole node), humanoid 'stand' task",
+            "metric": "env steps/sec (whole node), humanoid 'stand' task, 1/2/4/8 MI355X",
             "value": value,
             "unit": "env_steps/s",
             "n_gpus": world,

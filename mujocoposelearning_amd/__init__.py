@@ -21,6 +21,12 @@ def __getattr__(name):
     if name in ("HsModel", "load_model"):
         from . import model
         return getattr(model, name)
+    if name in ("PPO", "ActorCritic"):
+        from . import ppo
+        return getattr(ppo, name)
+    if name == "train_humanoid":
+        from .train import train_humanoid
+        return train_humanoid
     if name == "HsBatch":
         from .batch import HsBatch
         return HsBatch

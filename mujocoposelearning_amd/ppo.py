@@ -90,11 +90,22 @@ def gae(rewards, values, dones, last_values, last_dones, gamma, lam):
 
 
 class PPO:
-    """PPO over a HumanoidVecEnv's device fast path."""
+    """PPO over a device vec-env (HumanoidVecEnv's fast path).
+
+    The env protocol: ``num_envs``, ``obs_dim``, ``act_dim``, ``device``, ``reset_tensors()``,
+    ``step_tensors(actions) -> (obs, reward, terminated, truncated)`` on device, and
+    ``terminal_obs`` (pre-reset obs of envs that just finished).  ``world_size``/``rank``
+    default to the initialised torch.distributed group (one process per GPU, envs sharded).
+    """
 
     def __init__(self, env, learning_rate=3e-4, n_steps=2048, batch_size=64, n_epochs=10, gamma=0.99,
                  gae_lambda=0.95, clip_range=0.2, ent_coef=0.0, vf_coef=0.5, max_grad_norm=0.5,
-                 policy_kwargs=None, seed=0, world_size=1, rank=0):
+                 policy_kwargs=None, seed=0, world_size=None, rank=None):
+        import torch.distributed as dist
+        if world_size is None:
+            world_size = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        if rank is None:
+            rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
         pk = dict(policy_kwargs or {})
         net = pk.get("net_arch", {"pi": [64, 64], "vf": [64, 64]})
         if isinstance(net, (list, tuple)):
@@ -103,16 +114,17 @@ class PPO:
         if isinstance(act, str):
             act = getattr(nn, act)
         self.env = env
-        self.device = env.batch.device
-        torch.manual_seed(seed + rank)
-        self.policy = ActorCritic(env.batch.obs_dim, env.model.nu, net["pi"], net["vf"], act,
+        self.device = torch.device(env.device)
+        torch.manual_seed(seed)          # identical initial weights on every rank
+        self.policy = ActorCritic(env.obs_dim, env.act_dim, net["pi"], net["vf"], act,
                                   pk.get("log_std_init", 0.0)).to(self.device)
+        torch.manual_seed(seed + 7919 * rank)   # per-rank exploration noise / minibatch order
         self.opt = torch.optim.Adam(self.policy.parameters(), lr=learning_rate, eps=1e-5)
         self.n_steps, self.batch_size, self.n_epochs = n_steps, batch_size, n_epochs
         self.gamma, self.gae_lambda, self.clip_range = gamma, gae_lambda, clip_range
         self.ent_coef, self.vf_coef, self.max_grad_norm = ent_coef, vf_coef, max_grad_norm
         self.world_size, self.rank = world_size, rank
-        N, T, D, A = env.num_envs, n_steps, env.batch.obs_dim, env.model.nu
+        N, T, D, A = env.num_envs, n_steps, env.obs_dim, env.act_dim
         f, dev = torch.float32, self.device
         self.buf = dict(obs=torch.zeros(T, N, D, dtype=f, device=dev), act=torch.zeros(T, N, A, dtype=f, device=dev),
                         rew=torch.zeros(T, N, dtype=f, device=dev), start=torch.zeros(T, N, dtype=f, device=dev),
@@ -138,7 +150,7 @@ class PPO:
             r = rew.float()
             done = (term | trunc).float()
             if bool(trunc.any()):   # SB3 timeout bootstrap: r += gamma * V(terminal_obs)
-                tv = pol.value(env.batch.terminal_obs.float())
+                tv = pol.value(env.terminal_obs.float())
                 r = r + self.gamma * tv * (trunc.float() * (1 - term.float()))
             b["rew"][t] = r
             self.ep_acc += rew.double()

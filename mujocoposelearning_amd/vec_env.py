@@ -69,6 +69,25 @@ class HumanoidVecEnv(_Base):
         self.render_mode = None
 
     # ---------------------------------------------------------------- device fast path
+    # Protocol the on-device trainer (ppo.PPO) relies on: num_envs, obs_dim, act_dim, device,
+    # reset_tensors(), step_tensors(actions), terminal_obs.
+    @property
+    def obs_dim(self):
+        return self.batch.obs_dim
+
+    @property
+    def act_dim(self):
+        return self.model.nu
+
+    @property
+    def device(self):
+        return self.batch.device
+
+    @property
+    def terminal_obs(self):
+        """[N, obs_dim] device tensor: pre-reset obs of envs whose episode ended in the last step."""
+        return self.batch.terminal_obs
+
     def reset_tensors(self):
         return self.batch.reset()
 

@@ -1,0 +1,179 @@
+"""CPU tests of the on-device PPO module (ppo.py) and the train_humanoid mirror (train.py).
+
+SB3 is not installed here: PPO parity with SB3 2.3.2 is unpinned.  The tests
+check the restated pieces that have an exact definition (GAE reverse scan, parameter count of
+the [256,256] MlpPolicy, SB3's init) and the multi-process behaviour (one gradient all-reduce
+per optimizer step over gloo, identical weights on every rank).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from mujocoposelearning_amd.ppo import PPO, ActorCritic, gae
+from mujocoposelearning_amd.train import _resolve_activation, env_config_from_kwargs, shard_envs
+
+
+class ToyEnv:
+    """Device vec-env protocol stand-in on the CPU: reward = -|a - tanh(W obs)|^2, episodes of
+    ``horizon`` steps ending by truncation (exercises the timeout bootstrap)."""
+
+    def __init__(self, n=16, obs_dim=6, act_dim=3, horizon=8, seed=0):
+        g = torch.Generator().manual_seed(1234)          # same task on every rank
+        self.W = torch.randn(act_dim, obs_dim, generator=g) * 0.5
+        self.g = torch.Generator().manual_seed(seed)
+        self.num_envs, self.obs_dim, self.act_dim, self.device = n, obs_dim, act_dim, torch.device("cpu")
+        self.horizon = horizon
+        self.t = torch.zeros(n, dtype=torch.long)
+        self.obs = torch.randn(n, obs_dim, generator=self.g)
+        self.terminal_obs = torch.zeros(n, obs_dim)
+
+    def reset_tensors(self):
+        self.t.zero_()
+        self.obs = torch.randn(self.num_envs, self.obs_dim, generator=self.g)
+        return self.obs
+
+    def step_tensors(self, a):
+        target = torch.tanh(self.obs @ self.W.T)
+        rew = -((a - target) ** 2).sum(-1)
+        self.t += 1
+        trunc = self.t >= self.horizon
+        term = torch.zeros_like(trunc)
+        nxt = torch.randn(self.num_envs, self.obs_dim, generator=self.g)
+        self.terminal_obs = nxt.clone()
+        fresh = torch.randn(self.num_envs, self.obs_dim, generator=self.g)
+        self.obs = torch.where(trunc[:, None], fresh, nxt)
+        self.t[trunc] = 0
+        return self.obs, rew, term, trunc
+
+
+def _sb3_gae(rewards, values, episode_starts, last_values, dones, gamma, lam):
+    """SB3 2.3.2 RolloutBuffer.compute_returns_and_advantage (stable_baselines3/common/buffers.py),
+    restated with scalar loops."""
+    T, N = rewards.shape
+    adv = np.zeros((T, N))
+    for n in range(N):
+        last = 0.0
+        for step in reversed(range(T)):
+            if step == T - 1:
+                nnt, nv = 1.0 - dones[n], last_values[n]
+            else:
+                nnt, nv = 1.0 - episode_starts[step + 1, n], values[step + 1, n]
+            delta = rewards[step, n] + gamma * nv * nnt - values[step, n]
+            last = delta + gamma * lam * nnt * last
+            adv[step, n] = last
+    return adv, adv + values
+
+
+def test_gae_matches_sb3_restatement():
+    rng = np.random.default_rng(0)
+    T, N = 37, 5
+    r, v = rng.normal(size=(T, N)), rng.normal(size=(T, N))
+    starts = (rng.uniform(size=(T, N)) < 0.1).astype(np.float64)
+    lv, ld = rng.normal(size=N), (rng.uniform(size=N) < 0.3).astype(np.float64)
+    ea, er = _sb3_gae(r, v, starts, lv, ld, 0.99, 0.95)
+    t = lambda x: torch.tensor(x, dtype=torch.float64)
+    adv, ret = gae(t(r), t(v), t(starts), t(lv), t(ld), 0.99, 0.95)
+    np.testing.assert_allclose(adv.numpy(), ea, rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(ret.numpy(), er, rtol=1e-12, atol=1e-12)
+
+
+def test_policy_param_count_and_init():
+    # pi 161,578 + vf 156,417 = 317,995 parameters at net_arch [256, 256]
+    p = ActorCritic(352, 21, [256, 256], [256, 256])
+    assert sum(x.numel() for x in p.parameters()) == 317_995
+    assert torch.all(p.log_std == 0)
+    for lin in (p.action_net, p.value_net):
+        assert torch.all(lin.bias == 0)
+    w = p.action_net.weight                  # orthogonal init with gain 0.01 (rows orthonormal * gain)
+    np.testing.assert_allclose((w @ w.T).detach().numpy(), 1e-4 * np.eye(21), atol=1e-9)
+
+
+def test_shard_envs_and_config_mirror():
+    for n, w in ((32768, 8), (8192, 8), (10, 3), (5, 5)):
+        ranges = [shard_envs(n, w, r) for r in range(w)]
+        assert ranges[0][0] == 0 and ranges[-1][1] == n
+        assert all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
+        sizes = [b - a for a, b in ranges]
+        assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        shard_envs(3, 4, 0)
+    cfg = env_config_from_kwargs({"reward_function": "stand", "frame_skip": 3})
+    assert cfg["duration"] == 10.0 and cfg["reward_config"] == {"type": "stand"} and cfg["frame_skip"] == 3
+    assert env_config_from_kwargs({})["reward_config"]["type"] == "walk"      # train_sb3.py:189 default
+    kw = _resolve_activation({"policy_kwargs": {"activation_fn": "ReLU", "net_arch": {"pi": [8], "vf": [8]}}})
+    assert kw["policy_kwargs"]["activation_fn"] is torch.nn.ReLU
+
+
+def test_ppo_learns_toy_task():
+    env = ToyEnv(n=32)
+    model = PPO(env, learning_rate=3e-3, n_steps=16, batch_size=64, n_epochs=4,
+                policy_kwargs={"net_arch": {"pi": [32, 32], "vf": [32, 32]}, "activation_fn": torch.nn.Tanh})
+    rets = []      # mean raw episode return of the last 100 episodes, per iteration
+    model.learn(total_timesteps=32 * 16 * 25,
+                callback=lambda m: rets.append(m.logger["ep_rew_mean"]) or True)
+    first, last = np.mean(rets[:3]), np.mean(rets[-3:])
+    assert model.num_timesteps == 32 * 16 * 25
+    assert last > first + 2.0, (first, last)
+    assert model.ep_returns, "truncated episodes must be recorded"
+
+
+def test_save_load_roundtrip(tmp_path):
+    env = ToyEnv(n=4)
+    kw = dict(n_steps=4, batch_size=8, n_epochs=1, policy_kwargs={"net_arch": [8, 8]})
+    a = PPO(env, **kw)
+    a.learn(16)
+    path = tmp_path / "m.pt"
+    a.save(path)
+    b = PPO(ToyEnv(n=4), seed=5, **kw).load(path)
+    for pa, pb in zip(a.policy.parameters(), b.policy.parameters()):
+        assert torch.equal(pa, pb)
+    assert b.num_timesteps == a.num_timesteps
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _dist_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    calls = []
+    real = dist.all_reduce
+
+    def counting(t, *a, **k):
+        calls.append(t.numel())
+        return real(t, *a, **k)
+    dist.all_reduce = counting
+    try:
+        env = ToyEnv(n=8, seed=100 + rank)            # different data per rank (env shard)
+        model = PPO(env, n_steps=8, batch_size=16, n_epochs=2,
+                    policy_kwargs={"net_arch": {"pi": [16, 16], "vf": [16, 16]}})
+        assert model.world_size == world and model.rank == rank
+        model.learn(total_timesteps=8 * 8 * world * 2)
+        flat = torch.cat([p.detach().reshape(-1) for p in model.policy.parameters()])
+        torch.save({"flat": flat, "calls": calls, "steps": model.num_timesteps}, os.path.join(out_dir, f"r{rank}.pt"))
+    finally:
+        dist.all_reduce = real
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_one_allreduce_per_step_identical_weights(tmp_path):
+    world, port = 2, _free_port()
+    mp.start_processes(_dist_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    r = [torch.load(tmp_path / f"r{i}.pt", weights_only=True) for i in range(world)]
+    assert torch.equal(r[0]["flat"], r[1]["flat"]), "ranks diverged: gradient all-reduce missing"
+    n_params = r[0]["flat"].numel()
+    # 2 iterations x 2 epochs x (64 samples / 16 per minibatch) = 16 optimizer steps, one bucket each
+    for x in r:
+        assert x["calls"] == [n_params] * 16
+        assert x["steps"] == 8 * 8 * world * 2
