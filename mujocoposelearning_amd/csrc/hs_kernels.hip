@@ -23,6 +23,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <type_traits>
 
 #include "hs_kernels.h"
 #include "hs_model.h"
@@ -43,41 +44,70 @@ constexpr int RPL = MAXEFC / HL;  // constraint rows per lane
 #define WSYNC() __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup")
 
 // ------------------------------------------------------------------ cross-lane helpers
-__device__ __forceinline__ float rl(float v, int l) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+// compile-time loop: f(std::integral_constant<int, i>) for i in [B, E)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
 }
-__device__ __forceinline__ double rl(double v, int l) {
-  long long x = __double_as_longlong(v);
-  int lo = __builtin_amdgcn_readlane((int)(x & 0xffffffffll), l);
-  int hi = __builtin_amdgcn_readlane((int)(x >> 32), l);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
 }
-// value of sub-lane k (compile-time / uniform) of the caller's half-wave
-template <typename T>
-__device__ __forceinline__ T bc(T v, int k, bool upper) {
-  T a = rl(v, k), b = rl(v, k + HL);
-  return upper ? b : a;
+// v_permlane16_swap(v, v): .first = rows {0,0,2,2}, .second = rows {1,1,3,3} (row = 16 lanes),
+// i.e. every lane of a 32-lane half sees the half's low row in .first and its high row in .second.
+struct RowPair { uint32_t lo, hi; };
+__device__ __forceinline__ RowPair rowswap(uint32_t v) {
+  auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  return {r[0], r[1]};
+}
+// value of sub-lane K (compile-time) of the caller's 32-lane half: DPP row_newbcast + one
+// permlane16 swap -- 3 VALU ops, no SGPR round trip, and bcast<K> / bcast<K+16> share both ops.
+template <int K>
+__device__ __forceinline__ uint32_t bcast32(uint32_t v) {
+  RowPair r = rowswap(dpp32<0x150 + (K & 15)>(v));
+  return K < 16 ? r.lo : r.hi;
+}
+template <int K>
+__device__ __forceinline__ float bcast(float v) {
+  return __uint_as_float(bcast32<K>(__float_as_uint(v)));
+}
+template <int K>
+__device__ __forceinline__ double bcast(double v) {
+  uint64_t x = (uint64_t)__double_as_longlong(v);
+  uint64_t lo = bcast32<K>((uint32_t)x), hi = bcast32<K>((uint32_t)(x >> 32));
+  return __longlong_as_double((long long)((hi << 32) | lo));
 }
 template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+  return __uint_as_float(dpp32<CTRL>(__float_as_uint(v)));
 }
 template <int CTRL>
 __device__ __forceinline__ double dpp(double v) {
-  long long x = __double_as_longlong(v);
-  int lo = __builtin_amdgcn_mov_dpp((int)(x & 0xffffffffll), CTRL, 0xF, 0xF, false);
-  int hi = __builtin_amdgcn_mov_dpp((int)(x >> 32), CTRL, 0xF, 0xF, false);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+  uint64_t x = (uint64_t)__double_as_longlong(v);
+  uint64_t lo = dpp32<CTRL>((uint32_t)x), hi = dpp32<CTRL>((uint32_t)(x >> 32));
+  return __longlong_as_double((long long)((hi << 32) | lo));
 }
-// sum over each 32-lane half (result in every lane of the half)
+__device__ __forceinline__ float rows_sum(float v) {
+  RowPair r = rowswap(__float_as_uint(v));
+  return __uint_as_float(r.lo) + __uint_as_float(r.hi);
+}
+__device__ __forceinline__ double rows_sum(double v) {
+  uint64_t x = (uint64_t)__double_as_longlong(v);
+  RowPair l = rowswap((uint32_t)x), h = rowswap((uint32_t)(x >> 32));
+  return __longlong_as_double((long long)(((uint64_t)h.lo << 32) | l.lo)) +
+         __longlong_as_double((long long)(((uint64_t)h.hi << 32) | l.hi));
+}
+// sum over each 32-lane half (result in every lane of the half); all-VALU, no LDS permute
 template <typename T>
 __device__ __forceinline__ T hsum(T v) {
   v += dpp<0xB1>(v);    // quad_perm [1,0,3,2]
   v += dpp<0x4E>(v);    // quad_perm [2,3,0,1]
   v += dpp<0x141>(v);   // row_half_mirror
   v += dpp<0x140>(v);   // row_mirror
-  v += __shfl_xor(v, 16);
-  return v;
+  return rows_sum(v);   // + the other 16-lane row of the half
 }
 __device__ __forceinline__ uint32_t hballot(bool p, bool upper) {
   uint64_t m = __ballot(p);
@@ -182,43 +212,50 @@ __device__ __forceinline__ void cross_force(const T* v, const T* f, T* r) {
 
 // ------------------------------------------------------------------ row-per-lane dense algebra
 // Cholesky A = L L' of an NV x NV SPD matrix held row-per-lane in each half (sub-lane i: row i);
-// the lower part becomes L, the upper part scratch.
+// the lower part becomes L, the upper part scratch.  Broadcasts are DPP/permlane (bcast<K>).
 template <int NV, typename T>
-__device__ __forceinline__ void chol_rows(T (&A)[NV], int sl, bool up) {
-#pragma unroll
-  for (int k = 0; k < NV; k++) {
-    T akk = bc(A[k], k, up);
+__device__ __forceinline__ void chol_rows(T (&A)[NV], int sl) {
+  static_for<0, NV>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    const int sl_k = opaque_v(sl);     // fresh compare per step (no 64-bit mask kept live)
+    T akk = bcast<k>(A[k]);
     T lkk = sqrt(akk > T(1e-30) ? akk : T(1e-30));
-    T lik = (sl == k) ? lkk : A[k] * (T(1) / lkk);
+    T lik = (sl_k == k) ? lkk : A[k] * (T(1) / lkk);
     A[k] = lik;
-#pragma unroll
-    for (int j = k + 1; j < NV; j++) A[j] -= lik * bc(lik, j, up);
+    static_for<k + 1, NV>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      A[j] -= lik * bcast<j>(lik);
+    });
     SCHED_FENCE();
-  }
+  });
 }
 // solve (L L') x = b; sub-lane i holds b_i; returns x_i
 template <int NV, typename T>
-__device__ __forceinline__ T chol_solve(const T (&L)[NV], T b, int sl, bool up) {
-#pragma unroll
-  for (int k = 0; k < NV; k++) {
-    T yk = bc(b, k, up) / bc(L[k], k, up);
-    b = (sl == k) ? yk : ((sl > k) ? b - L[k] * yk : b);
-  }
+__device__ __forceinline__ T chol_solve(const T (&L)[NV], T b, int sl) {
+  static_for<0, NV>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    const int sl_k = opaque_v(sl);
+    T yk = bcast<k>(b) / bcast<k>(L[k]);
+    b = (sl_k == k) ? yk : ((sl_k > k) ? b - L[k] * yk : b);
+  });
   T x = 0;
-#pragma unroll
-  for (int k = NV - 1; k >= 0; k--) {
-    T part = (sl > k && sl < NV) ? L[k] * x : T(0);
+  static_for<0, NV>([&](auto kc) {
+    constexpr int k = NV - 1 - decltype(kc)::value;
+    const int sl_k = opaque_v(sl);
+    T part = (sl_k > k && sl_k < NV) ? L[k] * x : T(0);
     T ssum = hsum(part);
-    T xk = (bc(b, k, up) - ssum) / bc(L[k], k, up);
-    x = (sl == k) ? xk : x;
-  }
+    T xk = (bcast<k>(b) - ssum) / bcast<k>(L[k]);
+    x = (sl_k == k) ? xk : x;
+  });
   return x;
 }
 template <int NV, typename T>
-__device__ __forceinline__ T matvec_rows(const T (&A)[NV], T x, bool up) {
+__device__ __forceinline__ T matvec_rows(const T (&A)[NV], T x) {
   T acc = 0;
-#pragma unroll
-  for (int j = 0; j < NV; j++) acc += A[j] * bc(x, j, up);
+  static_for<0, NV>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    acc += A[j] * bcast<j>(x);
+  });
   return acc;
 }
 
@@ -964,7 +1001,7 @@ struct Stepper {
       WSYNC();
       contact_aggregates(m, s, sl);
       HS_STAMP(clk, 7);
-      T Mx = matvec_rows(Mr, x, up);
+      T Mx = matvec_rows(Mr, x);
       T jtf = jtf_lane(m, s, sl, cd);
       T g = sl < NV ? Mx - fsmooth - jtf : T(0);
       T gn = sqrt(hsum(g * g));
@@ -1034,17 +1071,19 @@ struct Stepper {
           if (sl >= NV) jr = 0;
           if (__ballot(Dr != T(0)) == 0) continue;   // no dense row at this index in either half
           T dj = Dr * jr;
-#pragma unroll
-          for (int j = 0; j < NV; j++) H[j] += dj * bc(jr, j, up);
+          static_for<0, NV>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            H[j] += dj * bcast<j>(jr);
+          });
         }
       }
       HS_STAMP(clk, 9);
-      chol_rows<NV>(H, sl, up);
-      T sdir = -chol_solve<NV>(H, g, sl, up);
+      chol_rows<NV>(H, sl);
+      T sdir = -chol_solve<NV>(H, g, sl);
       if (sl >= NV) sdir = 0;
       HS_STAMP(clk, 10);
       // exact line search along sdir (piecewise-quadratic cost)
-      T Ms = matvec_rows(Mr, sdir, up);
+      T Ms = matvec_rows(Mr, sdir);
       T A0 = hsum(sl < NV ? sdir * Ms : T(0));
       T B0 = hsum(sl < NV ? sdir * (Mx - fsmooth) : T(0));
       if (sl < NV) s.vx[sl] = sdir;
@@ -1125,8 +1164,8 @@ struct Stepper {
     T damp = sl < NV ? m->dof_damping[sl] : T(0);
 #pragma unroll
     for (int j = 0; j < NV; j++) He[j] = Mr[j] + ((j == sl) ? h * damp : T(0));
-    chol_rows<NV>(He, sl, up);
-    T a = chol_solve<NV>(He, fsmooth + fcon, sl, up);
+    chol_rows<NV>(He, sl);
+    T a = chol_solve<NV>(He, fsmooth + fcon, sl);
     if (sl < NV) s.qvel[sl] += h * a;
     WSYNC();
     if (sl < m->njnt) {

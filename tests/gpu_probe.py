@@ -62,7 +62,44 @@ def divergence(prec, tape, nsub=1000, seed=0):
     print(f"[{prec} tape={tape}] " + " ".join(f"{s}:{eq:.1e}/{ev:.1e}/c{nc}" for s, eq, ev, nc in errs))
 
 
+def tail(n=4096, steps=300, prec="fp32"):
+    """Distribution of per-env Newton iterations / contacts over an episode, and the launch-time
+    sensitivity to the Newton iteration cap (the launch ends with its slowest wave)."""
+    model = HsModel(XML)
+    for cap in (100, 30, 15):
+        b = HsBatch(model, n, precision=prec, seed=1)
+        b.configure(frame_skip=3, duration=10.0, reward_id=0, max_newton=cap)
+        b.reset()
+        g = torch.Generator(device="cuda").manual_seed(0)
+        acts = torch.rand(steps, n, model.nu, device="cuda", generator=g) * 2 - 1
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ms = []
+        rows = []
+        for k in range(steps):
+            e0.record()
+            b.step(acts[k])
+            e1.record()
+            torch.cuda.synchronize()
+            ms.append(e0.elapsed_time(e1))
+            if cap == 100 and k in (5, 30, 60, 100, 200, 299):
+                it = b.aux[:, 37].float()
+                nc = b.aux[:, 35].float()
+                ne = b.aux[:, 36].float()
+                q = torch.tensor([0.5, 0.9, 0.99, 1.0], device=it.device)
+                rows.append(f"  step {k:3d}: newton p50/p90/p99/max {torch.quantile(it, q).tolist()}  "
+                            f"ncon mean/max {nc.mean().item():.1f}/{nc.max().item():.0f}  "
+                            f"nefc mean/max {ne.mean().item():.1f}/{ne.max().item():.0f}")
+        ms = np.array(ms)
+        print(f"[{prec}] N={n} max_newton={cap}: ms/step mean {ms.mean():.3f} (steps 0-99 {ms[:100].mean():.3f}, "
+              f"100-299 {ms[100:].mean():.3f})  warnings {b.warning.sum(0).tolist()}")
+        for r in rows:
+            print(r)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "tail":
+        tail()
+        sys.exit(0)
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
     if which in ("all", "tp"):
         for n in (1024, 4096, 16384):
