@@ -117,10 +117,17 @@ __device__ __forceinline__ uint32_t hballot(bool p, bool upper) {
 // so without this LICM hoists every per-lane model load (m->dof_bodyid[sl], ...) out of the
 // substep / Newton loops and keeps each one live in a VGPR for the whole kernel.
 template <typename P>
-__device__ __forceinline__ P* opaque(P* p) {
+__device__ __forceinline__ P opaque(P p) {
   asm volatile("" : "+s"(p));
   return p;
 }
+// The model lives in the constant address space: it is never written by the kernel, so reads at
+// a wave-uniform index become scalar loads (s_load via the scalar cache) even through an
+// opaque()-laundered pointer; lane-varying reads stay vector loads.
+template <typename T>
+using MPtr = const __attribute__((address_space(4))) DevModel<T>*;
+template <typename T>
+using CPtr = const __attribute__((address_space(4))) T*;      // pointer into the model
 // Same for a per-lane value: stops lane-invariant compare masks (j <= sl, bit(mask, sl), ...)
 // being hoisted out of the loops as dozens of 64-bit SGPR masks (which then spill).
 __device__ __forceinline__ int opaque_v(int x) {
@@ -340,7 +347,7 @@ __device__ __forceinline__ void make_frame(Con<T>& c) {
 
 // number of contacts (0..2) for static pair p (mjc_* primitives)
 template <typename T>
-__device__ __forceinline__ int collide_pair(const DevModel<T>* __restrict__ m, const Scratch<T>& s, int p, Con<T>& c0, Con<T>& c1) {
+__device__ __forceinline__ int collide_pair(MPtr<T> m, const Scratch<T>& s, int p, Con<T>& c0, Con<T>& c1) {
   int g1 = m->pair_g1[p], g2 = m->pair_g2[p], fn = m->pair_fn[p];
   const T* p1 = s.u.k.gpos[g1];
   const T* p2 = s.u.k.gpos[g2];
@@ -408,7 +415,7 @@ __device__ __forceinline__ void store_contact(Scratch<T>& s, int slot, const Con
 
 // impedance (mj_makeImpedance getimpedance), MuJoCo clamps d0/dmax to [1e-4, 0.9999]
 template <typename T>
-__device__ __forceinline__ T impedance(const T* si, T pos, T margin) {
+__device__ __forceinline__ T impedance(CPtr<T> si, T pos, T margin) {
   T s0 = fmin(T(0.9999), fmax(T(0.0001), si[0])), s1 = fmin(T(0.9999), fmax(T(0.0001), si[1]));
   if (s0 == s1 || si[2] <= T(1e-15)) return T(0.5) * (s0 + s1);
   T x = (pos - margin) / si[2];
@@ -424,7 +431,7 @@ __device__ __forceinline__ T impedance(const T* si, T pos, T margin) {
 // ------------------------------------------------------------------ J x for all rows
 // s.vx (generalized vector) -> body spatial velocities -> contact frame velocities
 template <typename T>
-__device__ __forceinline__ void map_vx(const DevModel<T>* __restrict__ m, Scratch<T>& s, int sl, int nv, int nb) {
+__device__ __forceinline__ void map_vx(MPtr<T> m, Scratch<T>& s, int sl, int nv, int nb) {
   if (sl < nb) {
     T v[6] = {0, 0, 0, 0, 0, 0};
     if (sl > 0) {
@@ -459,7 +466,7 @@ __device__ __forceinline__ void map_vx(const DevModel<T>* __restrict__ m, Scratc
 }
 
 template <typename T>
-__device__ __forceinline__ T row_Jx(const DevModel<T>* __restrict__ m, const Scratch<T>& s, int r) {
+__device__ __forceinline__ T row_Jx(MPtr<T> m, const Scratch<T>& s, int r) {
   int kid = s.row_kid[r];
   int kind = rk_kind(kid), id = rk_id(kid);
   if (kind <= RK_JHI) {
@@ -480,7 +487,7 @@ __device__ __forceinline__ T row_Jx(const DevModel<T>* __restrict__ m, const Scr
 
 // world-frame force direction u of a contact row
 template <typename T>
-__device__ __forceinline__ void row_u(const DevModel<T>* __restrict__ m, const Scratch<T>& s, int kind, int c, T* u) {
+__device__ __forceinline__ void row_u(MPtr<T> m, const Scratch<T>& s, int kind, int c, T* u) {
   if (kind == RK_CN) { for (int k = 0; k < 3; k++) u[k] = s.con_n[c][k]; return; }
   int sub = kind - RK_P0;
   T mu = m->pair_mu[s.con_pair[c]];
@@ -493,7 +500,7 @@ __device__ __forceinline__ void row_u(const DevModel<T>* __restrict__ m, const S
 
 // per-contact aggregates from current row forces: U = sum D u u' (active rows), F = sum f u
 template <typename T>
-__device__ __forceinline__ void contact_aggregates(const DevModel<T>* __restrict__ m, Scratch<T>& s, int sl) {
+__device__ __forceinline__ void contact_aggregates(MPtr<T> m, Scratch<T>& s, int sl) {
   if (sl < s.ncon) {
     int adr = s.con_adr[sl];
     int nr = m->pair_dim[s.con_pair[sl]] == 1 ? 1 : 4;
@@ -518,7 +525,7 @@ __device__ __forceinline__ void contact_aggregates(const DevModel<T>* __restrict
 
 // (J' f)_i for dof sub-lane i (contacts via point Jacobians, limits via sparse rows)
 template <typename T>
-__device__ __forceinline__ T jtf_lane(const DevModel<T>* __restrict__ m, const Scratch<T>& s, int sl, const T* cd) {
+__device__ __forceinline__ T jtf_lane(MPtr<T> m, const Scratch<T>& s, int sl, const T* cd) {
   T acc = 0;
   for (int c = 0; c < s.ncon; c++) {
     int p = s.con_pair[c];
@@ -574,7 +581,7 @@ struct PhaseClock {
 template <typename T, int NV>
 struct Stepper {
   PhaseClock clk;
-  const DevModel<T>* m;
+  MPtr<T> m;
   Scratch<T>& s;
   int sl, nb;
   bool up;        // upper half-wave (second env of the wave)
@@ -586,7 +593,7 @@ struct Stepper {
   T qfa;          // qfrc_actuator_i (obs / kneeling reward)
   int niter;
 
-  __device__ Stepper(const DevModel<T>* mm, Scratch<T>& ss, int lane)
+  __device__ Stepper(MPtr<T> mm, Scratch<T>& ss, int lane)
       : m(mm), s(ss), sl(lane & (HL - 1)), nb(mm->nbody), up(lane >= HL) {}
 
   // start of a pipeline phase: nothing lane-invariant is carried over from the previous phase
@@ -673,7 +680,7 @@ struct Stepper {
     if (sl == 0) { s.com[0] = c0; s.com[1] = c1; s.com[2] = c2; }
     if (b > 0 && b < nb) {   // cinert (mju_inertCom)
       const T* R = s.xmat[b];
-      const T* I6 = m->body_inert[b];
+      CPtr<T> I6 = m->body_inert[b];
       T I[9] = {I6[0], I6[3], I6[4], I6[3], I6[1], I6[5], I6[4], I6[5], I6[2]};
       T A[9];
       for (int r = 0; r < 3; r++)
@@ -925,7 +932,8 @@ struct Stepper {
         int kid = s.row_kid[r];
         int kind = rk_kind(kid), id = rk_id(kid);
         T pos, margin, dA;
-        const T *sr, *si;
+        CPtr<T> sr;
+        CPtr<T> si;
         if (kind <= RK_JHI) {
           T qv = s.qpos[m->jnt_qposadr[id]];
           pos = kind == RK_JLO ? qv - m->jnt_range[id][0] : m->jnt_range[id][1] - qv;
@@ -1204,7 +1212,7 @@ __device__ __forceinline__ T uniform_pm(uint64_t seed, int env, uint32_t episode
 }
 
 template <typename T>
-__device__ __forceinline__ void reset_state(const DevModel<T>* __restrict__ m, Scratch<T>& s, int sl, T& time, T& xws) {
+__device__ __forceinline__ void reset_state(MPtr<T> m, Scratch<T>& s, int sl, T& time, T& xws) {
   if (sl < m->nq) s.qpos[sl] = m->qpos0[sl];
   if (sl + HL < m->nq) s.qpos[sl + HL] = m->qpos0[sl + HL];
   if (sl < m->nv) s.qvel[sl] = 0;
@@ -1216,7 +1224,7 @@ __device__ __forceinline__ void reset_state(const DevModel<T>* __restrict__ m, S
 
 template <typename T, int NV>
 __device__ __forceinline__ void physics_step(Stepper<T, NV>& st, const StepParams& p, T& time, T& xws, int* warn) {
-  const DevModel<T>* __restrict__ m = st.m;
+  MPtr<T> m = st.m;
   Scratch<T>& s = st.s;
   const int sl = st.sl;
   const bool up = st.up;
@@ -1253,7 +1261,7 @@ __device__ __forceinline__ void physics_step(Stepper<T, NV>& st, const StepParam
 }
 
 template <typename T>
-__device__ __forceinline__ T compute_reward(const DevModel<T>* __restrict__ m, const Scratch<T>& s, const StepParams& p, T time,
+__device__ __forceinline__ T compute_reward(MPtr<T> m, const Scratch<T>& s, const StepParams& p, T time,
                             T energy_sum) {
   // quaternion_to_euler (utils.py:3-21): pitch = arcsin(2(wy - zx)), not clamped
   T w = s.qpos[3], x = s.qpos[4], y = s.qpos[5], z = s.qpos[6];
@@ -1296,7 +1304,7 @@ __device__ __forceinline__ T compute_reward(const DevModel<T>* __restrict__ m, c
 
 // custom_env.py:232-261 layout; qfrc_actuator comes from registers (sub-lane i holds dof i)
 template <typename T>
-__device__ __forceinline__ void write_obs(const DevModel<T>* __restrict__ m, const Scratch<T>& s, int sl, T qfa, T* out,
+__device__ __forceinline__ void write_obs(MPtr<T> m, const Scratch<T>& s, int sl, T qfa, T* out,
                           int obs_dim) {
   int nq = m->nq, nv = m->nv;
   int o1 = nq - 2, o2 = o1 + nv, o3 = o2 + 10 * m->nbody, o4 = o3 + 6 * m->nbody;
@@ -1345,7 +1353,7 @@ __device__ __forceinline__ void dump_debug(const Stepper<T, NV>& st, T* dbg) {
 
 // per-env commit of state + aux (one half-wave)
 template <typename T, int NV>
-__device__ __forceinline__ void commit(const DevModel<T>* __restrict__ m, const EnvBuffers<T>& b, const Stepper<T, NV>& st,
+__device__ __forceinline__ void commit(MPtr<T> m, const EnvBuffers<T>& b, const Stepper<T, NV>& st,
                        int env, T time, T xws, int step_count, uint32_t episode, T total, const int* warn) {
   const Scratch<T>& s = st.s;
   const int sl = st.sl, nq = m->nq, nv = m->nv, nu = m->nu;
@@ -1371,7 +1379,7 @@ __device__ __forceinline__ void commit(const DevModel<T>* __restrict__ m, const 
 
 // ------------------------------------------------------------------ the kernel
 template <typename T, int NV>
-__global__ __launch_bounds__(64, 2) void step_kernel(const DevModel<T>* __restrict__ m, EnvBuffers<T> b,
+__global__ __launch_bounds__(64, 2) void step_kernel(MPtr<T> m, EnvBuffers<T> b,
                                                   const float* __restrict__ actions,
                                                   const uint8_t* __restrict__ reset_mask,
                                                   const T* __restrict__ nz_q, const T* __restrict__ nz_v,
@@ -1499,7 +1507,7 @@ hipError_t launch_step(const DevModel<T>* dmodel, int nv, const EnvBuffers<T>& b
   dim3 grid((nenv + 1) / 2), block(WAVE);
   switch (nv) {
     case 27:
-      hipLaunchKernelGGL((step_kernel<T, 27>), grid, block, 0, stream, dmodel, b, actions, reset_mask, noise_qpos,
+      hipLaunchKernelGGL((step_kernel<T, 27>), grid, block, 0, stream, (MPtr<T>)dmodel, b, actions, reset_mask, noise_qpos,
                          noise_qvel, p, nenv);
       break;
     default:
