@@ -219,15 +219,19 @@ __device__ __forceinline__ void cross_force(const T* v, const T* f, T* r) {
 
 // ------------------------------------------------------------------ row-per-lane dense algebra
 // Cholesky A = L L' of an NV x NV SPD matrix held row-per-lane in each half (sub-lane i: row i);
-// the lower part becomes L, the upper part scratch.  Broadcasts are DPP/permlane (bcast<K>).
+// the lower part becomes L, the upper part scratch; dinv (sub-lane i) = 1 / L_ii.  Broadcasts are
+// DPP/permlane (bcast<K>); the only divide per step is the pivot reciprocal.
 template <int NV, typename T>
-__device__ __forceinline__ void chol_rows(T (&A)[NV], int sl) {
+__device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl) {
   static_for<0, NV>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
     const int sl_k = opaque_v(sl);     // fresh compare per step (no 64-bit mask kept live)
     T akk = bcast<k>(A[k]);
-    T lkk = sqrt(akk > T(1e-30) ? akk : T(1e-30));
-    T lik = (sl_k == k) ? lkk : A[k] * (T(1) / lkk);
+    akk = akk > T(1e-30) ? akk : T(1e-30);
+    T lkk = sqrt(akk);
+    T r = T(1) / lkk;
+    T lik = (sl_k == k) ? lkk : A[k] * r;
+    dinv = (sl_k == k) ? r : dinv;
     A[k] = lik;
     static_for<k + 1, NV>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
@@ -236,14 +240,16 @@ __device__ __forceinline__ void chol_rows(T (&A)[NV], int sl) {
     SCHED_FENCE();
   });
 }
-// solve (L L') x = b; sub-lane i holds b_i; returns x_i
+// solve (L L') x = b; sub-lane i holds b_i; returns x_i.  Sub-lane k finishes y_k / x_k itself
+// (times its own 1/L_kk) and one broadcast hands it to the half.
 template <int NV, typename T>
-__device__ __forceinline__ T chol_solve(const T (&L)[NV], T b, int sl) {
+__device__ __forceinline__ T chol_solve(const T (&L)[NV], T dinv, T b, int sl) {
   static_for<0, NV>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
     const int sl_k = opaque_v(sl);
-    T yk = bcast<k>(b) / bcast<k>(L[k]);
-    b = (sl_k == k) ? yk : ((sl_k > k) ? b - L[k] * yk : b);
+    T yk = bcast<k>(b * dinv);
+    b = (sl_k > k) ? b - L[k] * yk : b;
+    b = (sl_k == k) ? yk : b;
   });
   T x = 0;
   static_for<0, NV>([&](auto kc) {
@@ -251,7 +257,7 @@ __device__ __forceinline__ T chol_solve(const T (&L)[NV], T b, int sl) {
     const int sl_k = opaque_v(sl);
     T part = (sl_k > k && sl_k < NV) ? L[k] * x : T(0);
     T ssum = hsum(part);
-    T xk = (bcast<k>(b) - ssum) / bcast<k>(L[k]);
+    T xk = bcast<k>((b - ssum) * dinv);
     x = (sl_k == k) ? xk : x;
   });
   return x;
@@ -1086,8 +1092,9 @@ struct Stepper {
         }
       }
       HS_STAMP(clk, 9);
-      chol_rows<NV>(H, sl);
-      T sdir = -chol_solve<NV>(H, g, sl);
+      T hdinv = 0;
+      chol_rows<NV>(H, hdinv, sl);
+      T sdir = -chol_solve<NV>(H, hdinv, g, sl);
       if (sl >= NV) sdir = 0;
       HS_STAMP(clk, 10);
       // exact line search along sdir (piecewise-quadratic cost)
@@ -1172,8 +1179,9 @@ struct Stepper {
     T damp = sl < NV ? m->dof_damping[sl] : T(0);
 #pragma unroll
     for (int j = 0; j < NV; j++) He[j] = Mr[j] + ((j == sl) ? h * damp : T(0));
-    chol_rows<NV>(He, sl);
-    T a = chol_solve<NV>(He, fsmooth + fcon, sl);
+    T edinv = 0;
+    chol_rows<NV>(He, edinv, sl);
+    T a = chol_solve<NV>(He, edinv, fsmooth + fcon, sl);
     if (sl < NV) s.qvel[sl] += h * a;
     WSYNC();
     if (sl < m->njnt) {
