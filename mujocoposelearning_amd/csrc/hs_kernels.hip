@@ -34,6 +34,7 @@ namespace {
 constexpr int WAVE = 64;
 constexpr int HL = 32;            // lanes per env
 constexpr int RPL = MAXEFC / HL;  // constraint rows per lane
+static_assert(MAXDOF == HL, "one dof per sub-lane (lim_row slots, dof masks)");
 
 // scheduling fence: keeps the machine scheduler from hoisting loads across iterations of fully
 // unrolled loops (which otherwise inflates VGPR pressure far past the occupancy target)
@@ -283,8 +284,6 @@ struct Scratch {
   T qvel[MAXDOF];
   T ctrl[MAXU];
   T vx[MAXDOF];
-  T xpos[MAXBODY][3];
-  T xmat[MAXBODY][9];
   T com[4];
   T cinert[MAXBODY][10];
   T cdof[MAXDOF][6];
@@ -298,13 +297,18 @@ struct Scratch {
   T con_F[MAXCON][3];
   int con_pair[MAXCON];
   int con_adr[MAXCON];
+  uint32_t con_m1[MAXCON];    // dof chain masks of the contact's bodies (m1 = 0: world)
+  uint32_t con_m2[MAXCON];
+  T con_mu[MAXCON];
+  uint16_t lim_row[MAXDOF];   // joint-limit rows of a dof: (lo row + 1) | (hi row + 1) << 8
+  uint32_t dense_mask[MAXEFC / HL];   // rows added as dense rank-1 Hessian terms (tendons, body-body)
   int row_kid[MAXEFC];
   T row_D[MAXEFC];
   T row_f[MAXEFC];
-  int ncon, nefc, nlim, pad;
+  int ncon, nefc, nlim, njl;   // njl: joint-limit rows (tendon rows are [njl, nlim))
   union {   // phase-local arrays (aliased)
-    struct { T xquat[MAXBODY][4]; T xanchor[MAXJNT][3]; T xaxis[MAXJNT][3];
-             T gpos[MAXGEOM][3]; T gax[MAXGEOM][3]; } k;          // kinematics + collision
+    struct { T xpos[MAXBODY][3]; T xmat[MAXBODY][9]; T xquat[MAXBODY][4]; T xanchor[MAXJNT][3];
+             T xaxis[MAXJNT][3]; T gpos[MAXGEOM][3]; T gax[MAXGEOM][3]; } k;   // kinematics + collision
     struct { T crb[MAXBODY][10]; T buf[MAXDOF][6]; } c;          // composite rigid body
     struct { T cdofdot[MAXDOF][6]; T cfrc[MAXBODY][6]; T csub[MAXBODY][6]; } r;   // RNE
     struct { T bvel[MAXBODY][6]; } n;                             // J x mapping (rows, Newton)
@@ -412,11 +416,15 @@ __device__ __forceinline__ int collide_pair(MPtr<T> m, const Scratch<T>& s, int 
 }
 
 template <typename T>
-__device__ __forceinline__ void store_contact(Scratch<T>& s, int slot, const Con<T>& c, int p) {
+__device__ __forceinline__ void store_contact(MPtr<T> m, Scratch<T>& s, int slot, const Con<T>& c, int p) {
   if (slot >= MAXCON) return;
   for (int k = 0; k < 3; k++) { s.con_pos[slot][k] = c.pos[k]; s.con_n[slot][k] = c.n[k]; s.con_t1[slot][k] = c.t1[k]; }
   s.con_dist[slot] = c.dist;
   s.con_pair[slot] = p;
+  int b1 = m->pair_b1[p];
+  s.con_m1[slot] = b1 ? m->body_chainmask[b1] : 0u;
+  s.con_m2[slot] = m->body_chainmask[m->pair_b2[p]];
+  s.con_mu[slot] = m->pair_mu[p];
 }
 
 // impedance (mj_makeImpedance getimpedance), MuJoCo clamps d0/dmax to [1e-4, 0.9999]
@@ -471,24 +479,20 @@ __device__ __forceinline__ void map_vx(MPtr<T> m, Scratch<T>& s, int sl, int nv,
   WSYNC();
 }
 
+// Row descriptor kept in registers by the row's lane for the whole solve (no LDS / model
+// lookups per use): desc = kind << 16 | j with j = dof (joint limits), tendon id or contact id;
+// coef = +-1 (limits), +-mu (pyramid rows), 0 (frictionless contact normal).
 template <typename T>
-__device__ __forceinline__ T row_Jx(MPtr<T> m, const Scratch<T>& s, int r) {
-  int kid = s.row_kid[r];
-  int kind = rk_kind(kid), id = rk_id(kid);
-  if (kind <= RK_JHI) {
-    T v = s.vx[m->jnt_dofadr[id]];
-    return kind == RK_JLO ? v : -v;
-  }
+__device__ __forceinline__ T row_Jx(MPtr<T> m, const Scratch<T>& s, int desc, T coef) {
+  int kind = rk_kind(desc), j = rk_id(desc);
+  if (kind <= RK_JHI) return coef * s.vx[j];
   if (kind <= RK_THI) {
     T v = 0;
-    for (int w = 0; w < m->ten_nwrap[id]; w++) v += m->ten_wrapcoef[id][w] * s.vx[m->ten_wrapdof[id][w]];
-    return kind == RK_TLO ? v : -v;
+    for (int w = 0; w < m->ten_nwrap[j]; w++) v += m->ten_wrapcoef[j][w] * s.vx[m->ten_wrapdof[j][w]];
+    return coef * v;
   }
-  if (kind == RK_CN) return s.con_v[id][0];
-  int sub = kind - RK_P0;
-  T mu = m->pair_mu[s.con_pair[id]];
-  T sg = (sub & 1) ? -mu : mu;
-  return s.con_v[id][0] + sg * s.con_v[id][1 + (sub >> 1)];
+  int comp = kind == RK_CN ? 1 : 1 + ((kind - RK_P0) >> 1);
+  return s.con_v[j][0] + coef * s.con_v[j][comp];
 }
 
 // world-frame force direction u of a contact row
@@ -496,7 +500,7 @@ template <typename T>
 __device__ __forceinline__ void row_u(MPtr<T> m, const Scratch<T>& s, int kind, int c, T* u) {
   if (kind == RK_CN) { for (int k = 0; k < 3; k++) u[k] = s.con_n[c][k]; return; }
   int sub = kind - RK_P0;
-  T mu = m->pair_mu[s.con_pair[c]];
+  T mu = s.con_mu[c];
   T sg = (sub & 1) ? -mu : mu;
   T t[3];
   if (sub >> 1) cross3(s.con_n[c], s.con_t1[c], t);
@@ -529,14 +533,13 @@ __device__ __forceinline__ void contact_aggregates(MPtr<T> m, Scratch<T>& s, int
   WSYNC();
 }
 
-// (J' f)_i for dof sub-lane i (contacts via point Jacobians, limits via sparse rows)
+// (J' f)_i for dof sub-lane i (contacts via point Jacobians, joint limits via the dof's
+// limit-row slots, tendon limits via rows [njl, nlim))
 template <typename T>
 __device__ __forceinline__ T jtf_lane(MPtr<T> m, const Scratch<T>& s, int sl, const T* cd) {
   T acc = 0;
   for (int c = 0; c < s.ncon; c++) {
-    int p = s.con_pair[c];
-    int b1 = m->pair_b1[p], b2 = m->pair_b2[p];
-    int in2 = bit(m->body_chainmask[b2], sl), in1 = b1 ? bit(m->body_chainmask[b1], sl) : 0;
+    int in2 = bit(s.con_m2[c], sl), in1 = bit(s.con_m1[c], sl);
     if (in1 != in2) {
       T r[3] = {s.con_pos[c][0] - s.com[0], s.con_pos[c][1] - s.com[1], s.con_pos[c][2] - s.com[2]};
       T w[3];
@@ -546,16 +549,17 @@ __device__ __forceinline__ T jtf_lane(MPtr<T> m, const Scratch<T>& s, int sl, co
       acc += in2 ? v : -v;
     }
   }
-  for (int r = 0; r < s.nlim; r++) {
-    int kid = s.row_kid[r];
-    int kind = rk_kind(kid), id = rk_id(kid);
-    T f = s.row_f[r];
-    if (kind <= RK_JHI) {
-      if (m->jnt_dofadr[id] == sl) acc += kind == RK_JLO ? f : -f;
-    } else {
-      for (int w = 0; w < m->ten_nwrap[id]; w++)
-        if (m->ten_wrapdof[id][w] == sl) acc += (kind == RK_TLO ? f : -f) * m->ten_wrapcoef[id][w];
-    }
+  if (sl < MAXDOF) {
+    int lr = s.lim_row[sl];
+    int lo = (lr & 0xff) - 1, hi = (lr >> 8) - 1;
+    if (lo >= 0) acc += s.row_f[lo];
+    if (hi >= 0) acc -= s.row_f[hi];
+  }
+  for (int r = s.njl; r < s.nlim; r++) {
+    int id = rk_id(s.row_kid[r]);
+    T f = rk_kind(s.row_kid[r]) == RK_TLO ? s.row_f[r] : -s.row_f[r];
+    for (int w = 0; w < m->ten_nwrap[id]; w++)
+      if (m->ten_wrapdof[id][w] == sl) acc += f * m->ten_wrapcoef[id][w];
   }
   return acc;
 }
@@ -598,6 +602,7 @@ struct Stepper {
   T qacc;         // solver output qacc_i
   T qfa;          // qfrc_actuator_i (obs / kneeling reward)
   int niter;
+  T* dbg = nullptr;   // stage-dump target (env 0 in debug mode only)
 
   __device__ Stepper(MPtr<T> mm, Scratch<T>& ss, int lane)
       : m(mm), s(ss), sl(lane & (HL - 1)), nb(mm->nbody), up(lane >= HL) {}
@@ -612,9 +617,9 @@ struct Stepper {
   __device__ __forceinline__ void kinematics() {
     phase_begin();
     if (sl == 0) {
-      for (int k = 0; k < 3; k++) s.xpos[0][k] = 0;
+      for (int k = 0; k < 3; k++) s.u.k.xpos[0][k] = 0;
       s.u.k.xquat[0][0] = 1; s.u.k.xquat[0][1] = s.u.k.xquat[0][2] = s.u.k.xquat[0][3] = 0;
-      for (int k = 0; k < 9; k++) s.xmat[0][k] = (k % 4 == 0) ? T(1) : T(0);
+      for (int k = 0; k < 9; k++) s.u.k.xmat[0][k] = (k % 4 == 0) ? T(1) : T(0);
     }
     const int b = sl;
     const int depth = (b > 0 && b < nb) ? m->body_depth[b] : -1;
@@ -633,8 +638,8 @@ struct Stepper {
           int p = m->body_parentid[b];
           T bp[3] = {m->body_pos[b][0], m->body_pos[b][1], m->body_pos[b][2]};
           T bq[4] = {m->body_quat[b][0], m->body_quat[b][1], m->body_quat[b][2], m->body_quat[b][3]};
-          mv3(s.xmat[p], bp, pos);
-          for (int k = 0; k < 3; k++) pos[k] += s.xpos[p][k];
+          mv3(s.u.k.xmat[p], bp, pos);
+          for (int k = 0; k < 3; k++) pos[k] += s.u.k.xpos[p][k];
           T pq[4] = {s.u.k.xquat[p][0], s.u.k.xquat[p][1], s.u.k.xquat[p][2], s.u.k.xquat[p][3]};
           mulq(pq, bq, q);
           for (int j = ja; j < ja + jn; j++) {
@@ -658,8 +663,8 @@ struct Stepper {
         }
         normalize4(q);
         for (int k = 0; k < 4; k++) s.u.k.xquat[b][k] = q[k];
-        for (int k = 0; k < 3; k++) s.xpos[b][k] = pos[k];
-        quat2mat(q, s.xmat[b]);
+        for (int k = 0; k < 3; k++) s.u.k.xpos[b][k] = pos[k];
+        quat2mat(q, s.u.k.xmat[b]);
       }
       WSYNC();
     }
@@ -668,15 +673,15 @@ struct Stepper {
       T gp[3] = {m->geom_pos[g][0], m->geom_pos[g][1], m->geom_pos[g][2]};
       T gz[3] = {m->geom_zaxis[g][0], m->geom_zaxis[g][1], m->geom_zaxis[g][2]};
       T w[3];
-      mv3(s.xmat[gb], gp, w);
-      for (int k = 0; k < 3; k++) s.u.k.gpos[g][k] = s.xpos[gb][k] + w[k];
-      mv3(s.xmat[gb], gz, s.u.k.gax[g]);
+      mv3(s.u.k.xmat[gb], gp, w);
+      for (int k = 0; k < 3; k++) s.u.k.gpos[g][k] = s.u.k.xpos[gb][k] + w[k];
+      mv3(s.u.k.xmat[gb], gz, s.u.k.gax[g]);
     }
     T mx = 0, my = 0, mz = 0, xi[3] = {0, 0, 0};
     if (b > 0 && b < nb) {
       T ip[3] = {m->body_ipos[b][0], m->body_ipos[b][1], m->body_ipos[b][2]}, w[3];
-      mv3(s.xmat[b], ip, w);
-      for (int k = 0; k < 3; k++) xi[k] = s.xpos[b][k] + w[k];
+      mv3(s.u.k.xmat[b], ip, w);
+      for (int k = 0; k < 3; k++) xi[k] = s.u.k.xpos[b][k] + w[k];
       T mb = m->body_mass[b];
       mx = mb * xi[0]; my = mb * xi[1]; mz = mb * xi[2];
     }
@@ -685,7 +690,7 @@ struct Stepper {
     T c0 = hsum(mx) * inv, c1 = hsum(my) * inv, c2 = hsum(mz) * inv;
     if (sl == 0) { s.com[0] = c0; s.com[1] = c1; s.com[2] = c2; }
     if (b > 0 && b < nb) {   // cinert (mju_inertCom)
-      const T* R = s.xmat[b];
+      const T* R = s.u.k.xmat[b];
       CPtr<T> I6 = m->body_inert[b];
       T I[9] = {I6[0], I6[3], I6[4], I6[3], I6[1], I6[5], I6[4], I6[5], I6[2]};
       T A[9];
@@ -724,7 +729,7 @@ struct Stepper {
           cd[3] = k == 0 ? T(1) : T(0); cd[4] = k == 1 ? T(1) : T(0); cd[5] = k == 2 ? T(1) : T(0);
         } else {
           int c = k - 3;
-          ax[0] = s.xmat[db][c]; ax[1] = s.xmat[db][3 + c]; ax[2] = s.xmat[db][6 + c];
+          ax[0] = s.u.k.xmat[db][c]; ax[1] = s.u.k.xmat[db][3 + c]; ax[2] = s.u.k.xmat[db][6 + c];
         }
       } else {
         ax[0] = s.u.k.xaxis[j][0]; ax[1] = s.u.k.xaxis[j][1]; ax[2] = s.u.k.xaxis[j][2];
@@ -736,6 +741,8 @@ struct Stepper {
       for (int k = 0; k < 6; k++) s.cdof[sl][k] = cd[k];
     }
     WSYNC();
+    if (dbg)    // stage dump (env 0, debug mode): xpos is phase-local, so dump it here
+      for (int k = sl; k < MAXBODY * 3; k += HL) dbg[k] = s.u.k.xpos[k / 3][k % 3];
   }
 
   // mj_collision: one static pair per sub-lane per pass, ordered compaction into contacts
@@ -749,8 +756,8 @@ struct Stepper {
       if (p < m->npair) n = collide_pair(m, s, p, c0, c1);
       uint32_t m1 = hballot(n >= 1, up), m2 = hballot(n >= 2, up);
       int pre = below(m1, sl) + below(m2, sl);
-      if (n >= 1) store_contact(s, ncon + pre, c0, p);
-      if (n >= 2) store_contact(s, ncon + pre + 1, c1, p);
+      if (n >= 1) store_contact(m, s, ncon + pre, c0, p);
+      if (n >= 2) store_contact(m, s, ncon + pre + 1, c1, p);
       ncon += __popc(m1) + __popc(m2);
     }
     int overflow = ncon > MAXCON;
@@ -866,7 +873,7 @@ struct Stepper {
   }
 
   // mj_makeConstraint + mj_makeImpedance + reference (aref); row q of this lane: r = sl + 32 q
-  __device__ __forceinline__ int rows(T (&D)[RPL], T (&ar)[RPL]) {
+  __device__ __forceinline__ int rows(T (&D)[RPL], T (&ar)[RPL], int (&rd)[RPL], T (&rc)[RPL]) {
     phase_begin();
     int overflow = 0;
     int ncon = s.ncon;
@@ -883,7 +890,11 @@ struct Stepper {
       if (lo) s.row_kid[pre] = (RK_JLO << 16) | sl;
       if (hi) s.row_kid[pre + lo] = (RK_JHI << 16) | sl;
       nrow = __popc(ml) + __popc(mh);
+      s.lim_row[sl] = 0;                       // MAXDOF == HL: one slot per sub-lane
+      if (lo || hi)
+        s.lim_row[m->jnt_dofadr[sl]] = (uint16_t)((lo ? pre + 1 : 0) | (hi ? (pre + lo + 1) << 8 : 0));
     }
+    const int njl = nrow;
     {   // tendon limits
       bool lo = false, hi = false;
       if (sl < m->ntendon && m->ten_limited[sl]) {
@@ -925,7 +936,7 @@ struct Stepper {
       }
       nrow += tot;
     }
-    if (sl == 0) { s.ncon = ncon; s.nefc = nrow; s.nlim = nlim; }
+    if (sl == 0) { s.ncon = ncon; s.nefc = nrow; s.nlim = nlim; s.njl = njl; }
     if (sl < NV) s.vx[sl] = s.qvel[sl];
     WSYNC();
     map_vx(m, s, sl, m->nv, nb);     // row velocities J qvel for aref
@@ -934,6 +945,9 @@ struct Stepper {
       int r = sl + HL * q;
       D[q] = 0;
       ar[q] = 0;
+      rd[q] = 0;
+      rc[q] = 0;
+      bool dense = false;
       if (r < nrow) {
         int kid = s.row_kid[r];
         int kind = rk_kind(kid), id = rk_id(kid);
@@ -945,7 +959,10 @@ struct Stepper {
           pos = kind == RK_JLO ? qv - m->jnt_range[id][0] : m->jnt_range[id][1] - qv;
           margin = m->jnt_margin[id];
           sr = m->jnt_solref[id]; si = m->jnt_solimp[id];
-          dA = m->dof_invweight0[m->jnt_dofadr[id]];
+          int dof = m->jnt_dofadr[id];
+          dA = m->dof_invweight0[dof];
+          rd[q] = (kind << 16) | dof;
+          rc[q] = kind == RK_JLO ? T(1) : T(-1);
         } else if (kind <= RK_THI) {
           T L = 0;
           for (int w = 0; w < m->ten_nwrap[id]; w++) L += m->ten_wrapcoef[id][w] * s.qpos[m->ten_wrapqadr[id][w]];
@@ -953,14 +970,20 @@ struct Stepper {
           margin = m->ten_margin[id];
           sr = m->ten_solref[id]; si = m->ten_solimp[id];
           dA = m->ten_invweight0[id];
+          rd[q] = kid;
+          rc[q] = kind == RK_TLO ? T(1) : T(-1);
+          dense = true;
         } else {
           int p = s.con_pair[id];
           pos = s.con_dist[id];
           margin = m->pair_margin[p];
           sr = m->pair_solref[p]; si = m->pair_solimp[p];
           T tran = m->body_invweight_tran[m->pair_b1[p]] + m->body_invweight_tran[m->pair_b2[p]];
-          T mu = m->pair_mu[p];
+          T mu = s.con_mu[id];
           dA = kind == RK_CN ? tran : tran + mu * mu * tran;
+          rd[q] = kid;
+          rc[q] = kind == RK_CN ? T(0) : (((kind - RK_P0) & 1) ? -mu : mu);
+          dense = s.con_m1[id] != 0u;
         }
         T imp = impedance(si, pos, margin);
         T dmax = fmin(T(0.9999), fmax(T(0.0001), si[1]));
@@ -976,15 +999,18 @@ struct Stepper {
         T R = fmax(T(1e-15), (1 - imp) * dA / imp);
         D[q] = T(1) / R;
         s.row_D[r] = D[q];
-        ar[q] = -B * row_Jx(m, s, r) - K * imp * (pos - margin);
+        ar[q] = -B * row_Jx(m, s, rd[q], rc[q]) - K * imp * (pos - margin);
       }
+      uint32_t dm = hballot(dense, up);
+      if (sl == 0) s.dense_mask[q] = dm;
     }
     WSYNC();
     return overflow;
   }
 
   // primal Newton (mj_solNewton semantics), warm-started; x = qacc
-  __device__ __forceinline__ void solve(T xws, int maxit, T tol, const T (&D)[RPL], const T (&ar)[RPL]) {
+  __device__ __forceinline__ void solve(T xws, int maxit, T tol, const T (&D)[RPL], const T (&ar)[RPL],
+                                        const int (&rd)[RPL], const T (&rc)[RPL]) {
     phase_begin();
     const int nv = m->nv;
     const int nefc = s.nefc, nlim = s.nlim, ncon = s.ncon;
@@ -999,7 +1025,7 @@ struct Stepper {
     map_vx(m, s, sl, nv, nb);
     T jar[RPL], Js[RPL];
 #pragma unroll
-    for (int q = 0; q < RPL; q++) jar[q] = vr[q] ? row_Jx(m, s, sl + HL * q) - ar[q] : T(0);
+    for (int q = 0; q < RPL; q++) jar[q] = vr[q] ? row_Jx(m, s, rd[q], rc[q]) - ar[q] : T(0);
     HS_STAMP(clk, 6);
     bool done = false;      // this half-wave's solver has converged
     int it = 0;
@@ -1028,9 +1054,8 @@ struct Stepper {
         T aug[6] = {0, 0, 0, 0, 0, 0};
         T dadd = 0;
         for (int c = 0; c < ncon; c++) {
-          int p = s.con_pair[c];
-          if (m->pair_b1[p] != 0) continue;
-          if (!bit(m->body_chainmask[m->pair_b2[p]], sl)) continue;
+          if (s.con_m1[c] != 0u) continue;           // body-body: dense rank-1 rows below
+          if (!bit(s.con_m2[c], sl)) continue;
           T r[3] = {s.con_pos[c][0] - s.com[0], s.con_pos[c][1] - s.com[1], s.con_pos[c][2] - s.com[2]};
           T w[3];
           cross3(cd, r, w);
@@ -1042,9 +1067,11 @@ struct Stepper {
           cross3(r, z, rz);
           for (int k = 0; k < 3; k++) { aug[k] += rz[k]; aug[3 + k] += z[k]; }
         }
-        for (int r = 0; r < nlim; r++) {
-          int kid = s.row_kid[r];
-          if (rk_kind(kid) <= RK_JHI && s.row_f[r] != T(0) && m->jnt_dofadr[rk_id(kid)] == sl) dadd += s.row_D[r];
+        {   // active joint-limit rows of this dof (diagonal)
+          int lr = s.lim_row[sl];
+          int lo = (lr & 0xff) - 1, hi = (lr >> 8) - 1;
+          if (lo >= 0 && s.row_f[lo] != T(0)) dadd += s.row_D[lo];
+          if (hi >= 0 && s.row_f[hi] != T(0)) dadd += s.row_D[hi];
         }
 #pragma unroll
         for (int j = 0; j < NV; j++) {
@@ -1053,23 +1080,30 @@ struct Stepper {
           H[j] = Mr[j] + (bit(anci, j) ? dot6(cj, aug) : T(0)) + ((j == sl) ? dadd : T(0));
           SCHED_FENCE();
         }
-        // dense rank-1 rows (tendon limits, body-body contacts); loop bound = max over both halves
-        int nmax = max(nefc, __shfl_xor(nefc, HL));
-        for (int r = 0; r < nmax; r++) {
+        // dense rank-1 rows (tendon limits, body-body contacts): only the rows flagged in
+        // dense_mask; the loop runs max(#rows of either half) times (wave-uniform control)
+        uint32_t dm[RPL];
+#pragma unroll
+        for (int q = 0; q < RPL; q++) dm[q] = s.dense_mask[q];
+        for (;;) {
+          int r = -1;
+#pragma unroll
+          for (int q = RPL - 1; q >= 0; q--)
+            if (dm[q]) r = HL * q + __builtin_ctz(dm[q]);
+          if (__ballot(r >= 0) == 0) break;
           T jr = 0, Dr = 0;
-          if (r < nefc && s.row_f[r] != T(0)) {
-            int kid = s.row_kid[r];
-            int kind = rk_kind(kid), id = rk_id(kid);
-            if (kind == RK_TLO || kind == RK_THI) {
-              for (int w = 0; w < m->ten_nwrap[id]; w++)
-                if (m->ten_wrapdof[id][w] == sl) jr += m->ten_wrapcoef[id][w];
-              if (kind == RK_THI) jr = -jr;
+          if (r >= 0) {
+            dm[r / HL] &= dm[r / HL] - 1u;           // consume the row
+            if (s.row_f[r] != T(0)) {
+              int kid = s.row_kid[r];
+              int kind = rk_kind(kid), id = rk_id(kid);
               Dr = s.row_D[r];
-            } else if (kind >= RK_CN) {
-              int p = s.con_pair[id];
-              int b1 = m->pair_b1[p];
-              if (b1 != 0) {
-                int in2 = bit(m->body_chainmask[m->pair_b2[p]], sl), in1 = bit(m->body_chainmask[b1], sl);
+              if (kind == RK_TLO || kind == RK_THI) {
+                for (int w = 0; w < m->ten_nwrap[id]; w++)
+                  if (m->ten_wrapdof[id][w] == sl) jr += m->ten_wrapcoef[id][w];
+                if (kind == RK_THI) jr = -jr;
+              } else {
+                int in2 = bit(s.con_m2[id], sl), in1 = bit(s.con_m1[id], sl);
                 if (in1 != in2) {
                   T rr[3] = {s.con_pos[id][0] - s.com[0], s.con_pos[id][1] - s.com[1], s.con_pos[id][2] - s.com[2]};
                   T w[3], u[3];
@@ -1078,12 +1112,10 @@ struct Stepper {
                   row_u(m, s, kind, id, u);
                   jr = in2 ? dot3(u, jp) : -dot3(u, jp);
                 }
-                Dr = s.row_D[r];
               }
             }
           }
           if (sl >= NV) jr = 0;
-          if (__ballot(Dr != T(0)) == 0) continue;   // no dense row at this index in either half
           T dj = Dr * jr;
           static_for<0, NV>([&](auto jc) {
             constexpr int j = decltype(jc)::value;
@@ -1105,7 +1137,7 @@ struct Stepper {
       WSYNC();
       map_vx(m, s, sl, nv, nb);
 #pragma unroll
-      for (int q = 0; q < RPL; q++) Js[q] = vr[q] ? row_Jx(m, s, sl + HL * q) : T(0);
+      for (int q = 0; q < RPL; q++) Js[q] = vr[q] ? row_Jx(m, s, rd[q], rc[q]) : T(0);
       // alpha = 1 is exact when no row changes state on [0, 1] (jar is linear in alpha)
       bool same1 = true;
 #pragma unroll
@@ -1241,7 +1273,8 @@ __device__ __forceinline__ void physics_step(Stepper<T, NV>& st, const StepParam
   bool bv = sl < m->nv && isbad(s.qvel[sl]);
   if (hballot(bq, up)) { warn[WARN_BADQPOS]++; reset_state(m, s, sl, time, xws); }
   else if (hballot(bv, up)) { warn[WARN_BADQVEL]++; reset_state(m, s, sl, time, xws); }
-  T D[RPL], ar[RPL];
+  T D[RPL], ar[RPL], rc[RPL];
+  int rd[RPL];
   for (int attempt = 0; attempt < 2; attempt++) {
     HS_STAMP(st.clk, 0);
     st.kinematics();
@@ -1252,9 +1285,9 @@ __device__ __forceinline__ void physics_step(Stepper<T, NV>& st, const StepParam
     HS_STAMP(st.clk, 2);
     st.velocity_forces();
     HS_STAMP(st.clk, 3);
-    if (st.rows(D, ar)) warn[WARN_OVERFLOW]++;
+    if (st.rows(D, ar, rd, rc)) warn[WARN_OVERFLOW]++;
     HS_STAMP(st.clk, 5);
-    st.solve(xws, p.max_newton, sizeof(T) == 8 ? T(1e-13) : T(1e-7), D, ar);
+    st.solve(xws, p.max_newton, sizeof(T) == 8 ? T(1e-13) : T(1e-7), D, ar, rd, rc);
     bool ba = sl < m->nv && isbad(st.qacc);
     bool redo = hballot(ba, up) != 0 && attempt == 0;
     if (__ballot(redo) == 0) break;          // wave-uniform loop control
@@ -1331,7 +1364,6 @@ template <typename T, int NV>
 __device__ __forceinline__ void dump_debug(const Stepper<T, NV>& st, T* dbg) {
   const Scratch<T>& s = st.s;
   int sl = st.sl;
-  for (int k = sl; k < MAXBODY * 3; k += HL) dbg[k] = s.xpos[k / 3][k % 3];
   for (int k = sl; k < MAXBODY * 10; k += HL) dbg[200 + k] = s.cinert[k / 10][k % 10];
   for (int k = sl; k < MAXDOF * 6; k += HL) dbg[500 + k] = s.cdof[k / 6][k % 6];
   if (sl < NV)
@@ -1404,6 +1436,7 @@ __global__ __launch_bounds__(64, 2) void step_kernel(MPtr<T> m, EnvBuffers<T> b,
   Scratch<T>& s = smem[up ? 1 : 0];
   const int nq = m->nq, nv = m->nv, nu = m->nu;
   Stepper<T, NV> st(m, s, lane);
+  if (b.dbg && env == 0 && active) st.dbg = b.dbg;
   int warn[NWARN] = {0, 0, 0, 0};
   T time = b.time[env];
   T xws = (sl < nv) ? b.qacc_ws[(size_t)env * nv + sl] : T(0);
@@ -1464,6 +1497,7 @@ __global__ __launch_bounds__(64, 2) void step_kernel(MPtr<T> m, EnvBuffers<T> b,
       // custom_env.py:97-130: mj_resetData; qpos = init (z=1.282, upright); += U(+-0.01) noise
       // with z noise x0.1 and no quaternion noise; qvel = U(+-0.01); one mj_step with ctrl = 0.
       in_reset = true;
+      st.dbg = nullptr;
       T sc = (T)p.noise_scale;
       uint32_t ep = episode + 1;
       for (int k = sl; k < nq; k += HL) {
