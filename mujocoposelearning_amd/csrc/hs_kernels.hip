@@ -220,23 +220,31 @@ __device__ __forceinline__ void cross_force(const T* v, const T* f, T* r) {
 
 // ------------------------------------------------------------------ row-per-lane dense algebra
 // Cholesky A = L L' of an NV x NV SPD matrix held row-per-lane in each half (sub-lane i: row i);
-// the lower part becomes L, the upper part scratch; dinv (sub-lane i) = 1 / L_ii.  Broadcasts are
-// DPP/permlane (bcast<K>); the only divide per step is the pivot reciprocal.
+// the lower part becomes L, the upper part scratch; dinv (sub-lane i) = 1 / L_ii.  Step k
+// publishes column k (a_ik, one ds_write) in the env's LDS vector `col`; every lane reads the
+// pivot and a_jk (j > k) back as broadcast ds_reads, so the update is pure FMAs:
+//   A_ij -= (a_ik / a_kk) a_jk.
+template <typename T>
+__device__ __forceinline__ T rsqrt_t(T x) { return T(1) / sqrt(x); }
+template <>
+__device__ __forceinline__ float rsqrt_t<float>(float x) { return __builtin_amdgcn_rsqf(x); }
+
 template <int NV, typename T>
-__device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl) {
+__device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T* col) {
   static_for<0, NV>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
     const int sl_k = opaque_v(sl);     // fresh compare per step (no 64-bit mask kept live)
-    T akk = bcast<k>(A[k]);
+    col[sl_k] = A[k];
+    T akk = col[k];
     akk = akk > T(1e-30) ? akk : T(1e-30);
-    T lkk = sqrt(akk);
-    T r = T(1) / lkk;
-    T lik = (sl_k == k) ? lkk : A[k] * r;
+    T r = rsqrt_t(akk);                // 1 / L_kk
+    T lik = (sl_k == k) ? akk * r : A[k] * r;
     dinv = (sl_k == k) ? r : dinv;
+    T f = A[k] * (r * r);              // a_ik / a_kk
     A[k] = lik;
     static_for<k + 1, NV>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
-      A[j] -= lik * bcast<j>(lik);
+      A[j] = fma(-f, col[j], A[j]);
     });
     SCHED_FENCE();
   });
@@ -263,12 +271,13 @@ __device__ __forceinline__ T chol_solve(const T (&L)[NV], T dinv, T b, int sl) {
   });
   return x;
 }
+// (A v)_i for a row-per-lane matrix and a vector in LDS (broadcast ds_reads)
 template <int NV, typename T>
-__device__ __forceinline__ T matvec_rows(const T (&A)[NV], T x) {
+__device__ __forceinline__ T matvec_lds(const T (&A)[NV], const T* v) {
   T acc = 0;
   static_for<0, NV>([&](auto jc) {
     constexpr int j = decltype(jc)::value;
-    acc += A[j] * bcast<j>(x);
+    acc = fma(A[j], v[j], acc);
   });
   return acc;
 }
@@ -283,7 +292,7 @@ struct Scratch {
   T qpos[MAXQ];
   T qvel[MAXDOF];
   T ctrl[MAXU];
-  T vx[MAXDOF];
+  alignas(16) T vx[MAXDOF];   // generalized vector for J x; Cholesky column buffer
   T com[4];
   T cinert[MAXBODY][10];
   T cdof[MAXDOF][6];
@@ -444,19 +453,17 @@ __device__ __forceinline__ T impedance(CPtr<T> si, T pos, T margin) {
 
 // ------------------------------------------------------------------ J x for all rows
 // s.vx (generalized vector) -> body spatial velocities -> contact frame velocities
-template <typename T>
-__device__ __forceinline__ void map_vx(MPtr<T> m, Scratch<T>& s, int sl, int nv, int nb) {
-  if (sl < nb) {
+template <int NV, typename T>
+__device__ __forceinline__ void map_vx(MPtr<T> m, Scratch<T>& s, int sl, int nb) {
+  if (sl < nb) {   // body spatial velocity = sum over the body's dof chain of cdof_j x_j
     T v[6] = {0, 0, 0, 0, 0, 0};
-    if (sl > 0) {
-      uint32_t ch = m->body_chainmask[sl];
-      for (int j = 0; j < nv; j++) {
-        if ((ch >> j) & 1u) {
-          T xj = s.vx[j];
-          for (int k = 0; k < 6; k++) v[k] += s.cdof[j][k] * xj;
-        }
-      }
-    }
+    const uint32_t ch = sl > 0 ? m->body_chainmask[sl] : 0u;
+    static_for<0, NV>([&](auto jc) {      // unrolled + predicated: no per-dof branch, loads pipelined
+      constexpr int j = decltype(jc)::value;
+      T xj = bit(ch, j) ? s.vx[j] : T(0);
+#pragma unroll
+      for (int k = 0; k < 6; k++) v[k] = fma(s.cdof[j][k], xj, v[k]);
+    });
     for (int k = 0; k < 6; k++) s.u.n.bvel[sl][k] = v[k];
   }
   WSYNC();
@@ -570,8 +577,8 @@ __device__ __forceinline__ T jtf_lane(MPtr<T> m, const Scratch<T>& s, int sl, co
 #ifdef HS_TIMING
 struct PhaseClock {
   uint64_t acc[16] = {0};
-  uint64_t prev = 0;
-  __device__ __forceinline__ void start() { prev = __builtin_amdgcn_s_memtime(); }
+  uint64_t prev = 0, t0 = 0;
+  __device__ __forceinline__ void start() { prev = t0 = __builtin_amdgcn_s_memtime(); }
   __device__ __forceinline__ void stamp(int slot) {
     uint64_t now = __builtin_amdgcn_s_memtime();
     acc[slot] += now - prev;
@@ -939,7 +946,7 @@ struct Stepper {
     if (sl == 0) { s.ncon = ncon; s.nefc = nrow; s.nlim = nlim; s.njl = njl; }
     if (sl < NV) s.vx[sl] = s.qvel[sl];
     WSYNC();
-    map_vx(m, s, sl, m->nv, nb);     // row velocities J qvel for aref
+    map_vx<NV>(m, s, sl, nb);     // row velocities J qvel for aref
 #pragma unroll
     for (int q = 0; q < RPL; q++) {
       int r = sl + HL * q;
@@ -1022,7 +1029,8 @@ struct Stepper {
     const T scale = m->newton_scale;
     if (sl < NV) s.vx[sl] = x;
     WSYNC();
-    map_vx(m, s, sl, nv, nb);
+    T Mx = matvec_lds(Mr, s.vx);     // kept current below (Mx += alpha M s)
+    map_vx<NV>(m, s, sl, nb);
     T jar[RPL], Js[RPL];
 #pragma unroll
     for (int q = 0; q < RPL; q++) jar[q] = vr[q] ? row_Jx(m, s, rd[q], rc[q]) - ar[q] : T(0);
@@ -1041,7 +1049,6 @@ struct Stepper {
       WSYNC();
       contact_aggregates(m, s, sl);
       HS_STAMP(clk, 7);
-      T Mx = matvec_rows(Mr, x);
       T jtf = jtf_lane(m, s, sl, cd);
       T g = sl < NV ? Mx - fsmooth - jtf : T(0);
       T gn = sqrt(hsum(g * g));
@@ -1125,17 +1132,17 @@ struct Stepper {
       }
       HS_STAMP(clk, 9);
       T hdinv = 0;
-      chol_rows<NV>(H, hdinv, sl);
+      chol_rows<NV>(H, hdinv, sl, s.vx);
       T sdir = -chol_solve<NV>(H, hdinv, g, sl);
       if (sl >= NV) sdir = 0;
       HS_STAMP(clk, 10);
       // exact line search along sdir (piecewise-quadratic cost)
-      T Ms = matvec_rows(Mr, sdir);
-      T A0 = hsum(sl < NV ? sdir * Ms : T(0));
-      T B0 = hsum(sl < NV ? sdir * (Mx - fsmooth) : T(0));
       if (sl < NV) s.vx[sl] = sdir;
       WSYNC();
-      map_vx(m, s, sl, nv, nb);
+      T Ms = matvec_lds(Mr, s.vx);
+      T A0 = hsum(sl < NV ? sdir * Ms : T(0));
+      T B0 = hsum(sl < NV ? sdir * (Mx - fsmooth) : T(0));
+      map_vx<NV>(m, s, sl, nb);
 #pragma unroll
       for (int q = 0; q < RPL; q++) Js[q] = vr[q] ? row_Jx(m, s, rd[q], rc[q]) : T(0);
       // alpha = 1 is exact when no row changes state on [0, 1] (jar is linear in alpha)
@@ -1179,6 +1186,7 @@ struct Stepper {
       HS_STAMP(clk, 11);
       if (!done) {
         x += alpha * sdir;
+        Mx += alpha * Ms;
         bool changed = false;
 #pragma unroll
         for (int q = 0; q < RPL; q++) {
@@ -1212,7 +1220,7 @@ struct Stepper {
 #pragma unroll
     for (int j = 0; j < NV; j++) He[j] = Mr[j] + ((j == sl) ? h * damp : T(0));
     T edinv = 0;
-    chol_rows<NV>(He, edinv, sl);
+    chol_rows<NV>(He, edinv, sl, s.vx);
     T a = chol_solve<NV>(He, edinv, fsmooth + fcon, sl);
     if (sl < NV) s.qvel[sl] += h * a;
     WSYNC();
@@ -1460,6 +1468,9 @@ __global__ __launch_bounds__(64, 2) void step_kernel(MPtr<T> m, EnvBuffers<T> b,
   T* obs_out = b.obs + (size_t)env * p.obs_dim;
   const int nsub = (p.mode == MODE_RESET) ? 0 : p.nsub;
   bool in_reset = false;
+#ifdef HS_TIMING
+  int tot_iter = 0;
+#endif
   // One loop, ONE inlined physics_step call site: substeps 0..nsub-1 apply the action; after the
   // last one the env bookkeeping runs; if any half of the wave must reset, one more substep
   // runs with the reset state (a half that is not resetting has already committed and computes
@@ -1528,6 +1539,9 @@ __global__ __launch_bounds__(64, 2) void step_kernel(MPtr<T> m, EnvBuffers<T> b,
       WSYNC();
     }
     physics_step(st, p, time, xws, warn);
+#ifdef HS_TIMING
+    tot_iter += st.niter;
+#endif
     if (b.dbg && env == 0 && active && !in_reset) dump_debug(st, b.dbg);
   }
 #ifdef HS_TIMING
@@ -1536,6 +1550,10 @@ __global__ __launch_bounds__(64, 2) void step_kernel(MPtr<T> m, EnvBuffers<T> b,
     for (int k = 0; k < 15; k++) atomicAdd(&b.dbg[8000 + k], (T)st.clk.acc[k]);
     atomicAdd(&b.dbg[8015], (T)st.niter);
   }
+  // per-wave lifetime of this launch (shader cycles) -> dbg[9000 + wave] (waves < 7000)
+  if (lane == 0 && b.dbg && blockIdx.x < 2048) b.dbg[9000 + blockIdx.x] = (T)(st.clk.prev - st.clk.t0);
+  // per-env Newton iterations summed over this launch's substeps -> dbg[11100 + env]
+  if (sl == 0 && b.dbg && blockIdx.x < 2048) b.dbg[11100 + 2 * blockIdx.x + (up ? 1 : 0)] = (T)tot_iter;
 #endif
 }
 

@@ -42,6 +42,19 @@ def main(n=4096, steps=20, prec="fp32"):
           f"newton iters/substep {d[15] / (n * steps):.2f}")
     for name, c, f in zip(NAMES, per, d[:15] / tot):
         print(f"  {name:20s} {c:10,.0f} cyc  {100 * f:5.1f}%")
+    life = b.get_debug()[9000:9000 + (n + 1) // 2]        # last launch, one value per wave
+    q = np.percentile(life, [0, 10, 50, 90, 99, 100])
+    print("  wave lifetime (last launch, cycles) min/p10/p50/p90/p99/max: " + " / ".join(f"{v:,.0f}" for v in q)
+          + f"   mean {life.mean():,.0f}  (launch = max; mean/max = {life.mean() / life.max():.2f})")
+    it = b.get_debug()[11100:11100 + 2 * len(life)].reshape(-1, 2)
+    wmax, wsum = it.max(1), it.sum(1)
+    print(f"  newton iters per env per launch: mean {it.mean():.1f} max {it.max():.0f}; corr(lifetime, max-of-pair) "
+          f"{np.corrcoef(life, wmax)[0, 1]:.2f}, corr(lifetime, sum-of-pair) {np.corrcoef(life, wsum)[0, 1]:.2f}")
+    for lo, hi in ((0, 8), (8, 12), (12, 16), (16, 24), (24, 1000)):
+        sel = (wmax >= lo) & (wmax < hi)
+        if sel.any():
+            print(f"    pair-max iters [{lo},{hi}): {sel.sum():5d} waves, lifetime mean {life[sel].mean():,.0f} "
+                  f"max {life[sel].max():,.0f}")
 
 
 if __name__ == "__main__":
