@@ -143,6 +143,10 @@ __device__ __forceinline__ bool isbad(T x) {
 }
 
 // ------------------------------------------------------------------ small algebra
+// sin/cos: fp64 libm for the parity mode; the fp32 engine uses the hardware v_sin/v_cos
+// (|error| ~1e-6 on the half joint angles, inside the fp32 tolerance)
+__device__ __forceinline__ void sincos_t(double x, double& s, double& c) { sincos(x, &s, &c); }
+__device__ __forceinline__ void sincos_t(float x, float& s, float& c) { s = __sinf(x); c = __cosf(x); }
 template <typename T>
 __device__ __forceinline__ void quat2mat(const T* q, T* R) {
   T w = q[0], x = q[1], y = q[2], z = q[3];
@@ -628,44 +632,68 @@ struct Stepper {
       s.u.k.xquat[0][0] = 1; s.u.k.xquat[0][1] = s.u.k.xquat[0][2] = s.u.k.xquat[0][3] = 0;
       for (int k = 0; k < 9; k++) s.u.k.xmat[0][k] = (k % 4 == 0) ? T(1) : T(0);
     }
+    // Everything a body needs that does not depend on its parent is loaded / computed before the
+    // level loop (one model-load latency instead of one dependent chain per level; the joint
+    // half-angle rotations are computed by all bodies at once).
     const int b = sl;
-    const int depth = (b > 0 && b < nb) ? m->body_depth[b] : -1;
+    const bool isb = b > 0 && b < nb;
+    int depth = -1, par = 0, ja = 0, jn = 0, fqa = 0;
+    bool isfree = false;
+    T bp[3] = {0, 0, 0}, bq[4] = {1, 0, 0, 0};
+    T jpos[MAXJPB][3], jax[MAXJPB][3], jrot[MAXJPB][4];
+    if (isb) {
+      depth = m->body_depth[b];
+      par = m->body_parentid[b];
+      ja = m->body_jntadr[b];
+      jn = m->body_jntnum[b];
+      isfree = jn == 1 && m->jnt_type[ja] == JNT_FREE;
+      fqa = m->jnt_qposadr[ja];
+      for (int k = 0; k < 3; k++) bp[k] = m->body_pos[b][k];
+      for (int k = 0; k < 4; k++) bq[k] = m->body_quat[b][k];
+    }
+#pragma unroll
+    for (int jj = 0; jj < MAXJPB; jj++) {
+      const bool use = isb && !isfree && jj < jn;
+      const int j = use ? ja + jj : 0;
+      T ang = 0;
+      for (int k = 0; k < 3; k++) { jpos[jj][k] = use ? m->jnt_pos[j][k] : T(0); jax[jj][k] = use ? m->jnt_axis[j][k] : T(0); }
+      if (use) {
+        int qa = m->jnt_qposadr[j];
+        ang = s.qpos[qa] - m->qpos0[qa];
+      }
+      T sn, cs;
+      sincos_t(T(0.5) * ang, sn, cs);
+      jrot[jj][0] = cs; jrot[jj][1] = jax[jj][0] * sn; jrot[jj][2] = jax[jj][1] * sn; jrot[jj][3] = jax[jj][2] * sn;
+    }
     WSYNC();
     for (int L = 1; L <= m->nlevel; L++) {
       if (depth == L) {
         T pos[3], q[4];
-        int ja = m->body_jntadr[b], jn = m->body_jntnum[b];
-        if (jn == 1 && m->jnt_type[ja] == JNT_FREE) {
-          int qa = m->jnt_qposadr[ja];
-          for (int k = 0; k < 3; k++) pos[k] = s.qpos[qa + k];
-          for (int k = 0; k < 4; k++) q[k] = s.qpos[qa + 3 + k];
+        if (isfree) {
+          for (int k = 0; k < 3; k++) pos[k] = s.qpos[fqa + k];
+          for (int k = 0; k < 4; k++) q[k] = s.qpos[fqa + 3 + k];
           normalize4(q);
           for (int k = 0; k < 3; k++) { s.u.k.xanchor[ja][k] = pos[k]; s.u.k.xaxis[ja][k] = m->jnt_axis[ja][k]; }
         } else {
-          int p = m->body_parentid[b];
-          T bp[3] = {m->body_pos[b][0], m->body_pos[b][1], m->body_pos[b][2]};
-          T bq[4] = {m->body_quat[b][0], m->body_quat[b][1], m->body_quat[b][2], m->body_quat[b][3]};
-          mv3(s.u.k.xmat[p], bp, pos);
-          for (int k = 0; k < 3; k++) pos[k] += s.u.k.xpos[p][k];
-          T pq[4] = {s.u.k.xquat[p][0], s.u.k.xquat[p][1], s.u.k.xquat[p][2], s.u.k.xquat[p][3]};
+          mv3(s.u.k.xmat[par], bp, pos);
+          for (int k = 0; k < 3; k++) pos[k] += s.u.k.xpos[par][k];
+          T pq[4] = {s.u.k.xquat[par][0], s.u.k.xquat[par][1], s.u.k.xquat[par][2], s.u.k.xquat[par][3]};
           mulq(pq, bq, q);
-          for (int j = ja; j < ja + jn; j++) {
-            T R[9], ax[3], an[3], jp[3] = {m->jnt_pos[j][0], m->jnt_pos[j][1], m->jnt_pos[j][2]};
-            T la[3] = {m->jnt_axis[j][0], m->jnt_axis[j][1], m->jnt_axis[j][2]};
-            int qa = m->jnt_qposadr[j];
-            T ang = s.qpos[qa] - m->qpos0[qa];
-            quat2mat(q, R);
-            mv3(R, la, ax);
-            mv3(R, jp, an);
-            for (int k = 0; k < 3; k++) an[k] += pos[k];
-            T sn = sin(T(0.5) * ang), cs = cos(T(0.5) * ang);
-            T ql[4] = {cs, la[0] * sn, la[1] * sn, la[2] * sn};
-            mulq(q, ql, q);
-            quat2mat(q, R);
-            T v[3];
-            mv3(R, jp, v);
-            for (int k = 0; k < 3; k++) pos[k] = an[k] - v[k];
-            for (int k = 0; k < 3; k++) { s.u.k.xanchor[j][k] = an[k]; s.u.k.xaxis[j][k] = ax[k]; }
+#pragma unroll
+          for (int jj = 0; jj < MAXJPB; jj++) {
+            if (jj < jn) {
+              T R[9], ax[3], an[3];
+              quat2mat(q, R);
+              mv3(R, jax[jj], ax);
+              mv3(R, jpos[jj], an);
+              for (int k = 0; k < 3; k++) an[k] += pos[k];
+              mulq(q, jrot[jj], q);
+              quat2mat(q, R);
+              T v[3];
+              mv3(R, jpos[jj], v);
+              for (int k = 0; k < 3; k++) pos[k] = an[k] - v[k];
+              for (int k = 0; k < 3; k++) { s.u.k.xanchor[ja + jj][k] = an[k]; s.u.k.xaxis[ja + jj][k] = ax[k]; }
+            }
           }
         }
         normalize4(q);
@@ -1230,7 +1258,8 @@ struct Stepper {
         for (int k = 0; k < 3; k++) s.qpos[qa + k] += h * s.qvel[da + k];
         T w[3] = {s.qvel[da + 3], s.qvel[da + 4], s.qvel[da + 5]};
         T ang = h * normalize3(w);
-        T sn = sin(T(0.5) * ang), cs = cos(T(0.5) * ang);
+        T sn, cs;
+        sincos_t(T(0.5) * ang, sn, cs);
         T qr[4] = {cs, w[0] * sn, w[1] * sn, w[2] * sn};
         T q[4] = {s.qpos[qa + 3], s.qpos[qa + 4], s.qpos[qa + 5], s.qpos[qa + 6]};
         normalize4(q);

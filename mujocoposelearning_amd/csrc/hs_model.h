@@ -24,6 +24,7 @@ constexpr int MAXPAIR = 192;  // static candidate geom pairs
 constexpr int MAXCON = 32;    // contacts per env (one half-wave lane each; overflow -> warning word)
 constexpr int MAXEFC = 128;   // constraint rows per env (4 per half-wave lane)
 constexpr int MAXLEVEL = 16;
+constexpr int MAXJPB = 3;     // hinge joints per body (kinematics keeps their rotations in registers)
 
 enum GeomType { GEOM_PLANE = 0, GEOM_SPHERE = 2, GEOM_CAPSULE = 3 };
 enum JointType { JNT_FREE = 0, JNT_HINGE = 3 };

@@ -890,6 +890,13 @@ bool build_dev_model(const HostModel& m, DevModel<T>& d, std::string& err) {
     return false;
   for (int b = 1; b < m.nbody; b++)
     if (m.body_rootid[b] != m.body_rootid[1]) { err = "engine supports a single kinematic tree under world"; return false; }
+  for (int b = 1; b < m.nbody; b++) {   // kernel keeps a body's joint rotations in registers
+    int ja = m.body_jntadr[b], jn = m.body_jntnum[b];
+    bool has_free = false;
+    for (int j = ja; j < ja + jn; j++) has_free |= m.jnt_type[j] == JNT_FREE;
+    if (has_free && jn != 1) { err = "a free joint must be its body's only joint"; return false; }
+    if (!has_free && !cap("hinge joints per body", jn, MAXJPB)) return false;
+  }
   d.nq = m.nq; d.nv = m.nv; d.nu = m.nu; d.nbody = m.nbody; d.njnt = m.njnt; d.ngeom = m.ngeom;
   d.ntendon = m.ntendon; d.npair = (int)m.pair_geom.size();
   d.timestep = (T)m.timestep;

@@ -59,6 +59,36 @@ def main(tag="r01", n_envs=4096, precision="fp32", src=None):
               "## Resources", "",
               f"VGPR {out['vgpr']} (+{out['agpr']} AGPR), SGPR {out['sgpr']}, LDS {out['lds_bytes']} B/workgroup, "
               f"scratch {out['scratch_bytes_per_lane']} B/lane, grid {out['grid']} threads x wg {out['workgroup']}."]
+    sq = {}
+    for sub in ("sq", "sq2"):
+        f = os.path.join(src, sub, f"{sub}_counter_collection.csv")
+        if not os.path.exists(f):
+            continue
+        by = {}
+        for r in csv.DictReader(open(f)):
+            if "step_kernel" in r["Kernel_Name"]:
+                by.setdefault(r["Dispatch_Id"], {})[r["Counter_Name"]] = float(r["Counter_Value"])
+        ids = sorted(by, key=int)
+        ids = ids[7:] if len(ids) > 10 else ids
+        for k in by[ids[0]]:
+            sq[k] = statistics.mean(by[i][k] for i in ids)
+    if sq:
+        out["sq"] = sq
+        wc = sq.get("SQ_WAVE_CYCLES", 0)
+        lines += ["", "## Issue / stall picture (SQ counters, per launch; SQ cycle counters are quad-cycles)", ""]
+        for k in sorted(sq):
+            lines.append(f"- {k}: {sq[k]:,.0f}")
+        if wc:
+            lines += ["",
+                      f"- waves parked on s_waitcnt (SQ_WAIT_ANY / SQ_WAVE_CYCLES): {sq['SQ_WAIT_ANY'] / wc:.1%}",
+                      f"- issuing (SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES): {sq['SQ_ACTIVE_INST_ANY'] / wc:.1%}",
+                      f"- VALU instructions per wave per launch: {sq['SQ_INSTS_VALU'] / sq['SQ_WAVES']:,.0f}"]
+            if "GRBM_GUI_ACTIVE" in sq:
+                kc = sq["GRBM_GUI_ACTIVE"] / 8
+                life = 4 * wc / sq["SQ_WAVES"]
+                lines.append(f"- mean wave lifetime {life:,.0f} cycles vs kernel {kc:,.0f} cycles (GRBM_GUI_ACTIVE/8): "
+                             f"{life / kc:.0%} -- the rest is the Newton-iteration tail (one wave per slot at 4096 envs)")
+        json.dump(out, open(os.path.join(ROOT, "profiles", "traffic_step_kernel.json"), "w"), indent=1)
     open(os.path.join(ROOT, "profiles", f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
