@@ -101,6 +101,7 @@ def main():
     ap.add_argument("--precision", default="fp32", choices=["fp32", "fp64"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-rollout", action="store_true")
+    ap.add_argument("--no-gae", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=60000, help="vec steps of the CPU baseline (~13 s)")
     args = ap.parse_args()
 
@@ -184,6 +185,32 @@ def main():
         rollout = dict(value=n * rs * world / float(t.item()), unit="env_steps/s",
                        note="policy MLP[256,256] (pi+vf) forward + diag-Gaussian sample + clip + env step")
 
+    # GAE leg: the rollout-end reverse scan (hs_gae) over an n_steps=2048 x n-env buffer -- an
+    # HBM-bound kernel (12 B read + 8 B written per element), timed with HIP events on its stream
+    gae_res = None
+    if not args.no_gae:
+        from mujocoposelearning_amd.ppo import gae_device
+        Tg = 2048
+        gg = torch.Generator(device=dev).manual_seed(11)
+        rb = [torch.randn(Tg, n, device=dev, generator=gg) for _ in range(2)]
+        stg = (torch.rand(Tg, n, device=dev, generator=gg) < 1 / 667).float()
+        lvg, ldg = torch.randn(n, device=dev, generator=gg), torch.zeros(n, device=dev)
+        for _ in range(3):
+            gae_device(rb[0], rb[1], stg, lvg, ldg, 0.99, 0.95)
+        torch.cuda.synchronize(dev)
+        reps = 20
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            gae_device(rb[0], rb[1], stg, lvg, ldg, 0.99, 0.95)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        gms = e0.elapsed_time(e1) / reps
+        gbs = 20.0 * Tg * n / (gms * 1e-3) / 1e9
+        gae_res = {"kernel": "gae_kernel", "T": Tg, "n_envs": n, "ms_per_rollout": gms,
+                   "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": gbs / HBM_PEAK_GBS, "algo_bytes_per_element": 20}}
+
     if rank == 0:
         achieved = ALGO_BYTES_PER_ENV_STEP * n / (kernel_ms * 1e-3) / 1e9
         traffic = None
@@ -219,6 +246,7 @@ def main():
                          "note": "latency/VALU-bound kernel; HBM fraction reported per BASELINE.json"},
             "cpu_baseline": cpu_res,
             "rollout": rollout,
+            "gae": gae_res,
             "sim_stats": stats,
         }
         print(json.dumps(out))

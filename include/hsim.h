@@ -18,6 +18,8 @@
  *   hs_state_io          <- reads/writes of data.qpos/qvel/qacc_warmstart/time/ctrl (custom_env.py:105-117)
  *   hs_get_buffers       <- data.* arrays as device buffers (obs, reward, terminated, ...)
  *   hs_last_error        <- mujoco's error callback / MjModel load error string
+ *   hs_gae               <- SB3 RolloutBuffer.compute_returns_and_advantage (stable_baselines3 2.3.2
+ *                           common/buffers.py), run by PPO.learn once per rollout (train_sb3.py:229)
  *
  * Conventions: status int (0 ok, <0 error, message via hs_last_error(), thread-local); the
  * model is immutable and shareable; a batch owns (or is bound to) device buffers; every call
@@ -114,6 +116,14 @@ int hs_state_io(hs_batch* b, int dir, double* qpos, double* qvel, double* qacc_w
 int hs_set_debug(hs_batch* b, int enable);
 int hs_get_debug(hs_batch* b, double* out, int n);
 int hs_synchronize(hs_batch* b);
+
+/* GAE(gamma, lambda) reverse scan over a device rollout buffer, SB3 semantics: [T][N] float32
+ * rewards, values, episode_starts; [N] last_values, last_dones; writes [T][N] advantages and
+ * returns (= advantages + values).  All pointers are device memory on the current device;
+ * asynchronous on `stream`. */
+int hs_gae(const float* rewards, const float* values, const float* episode_starts, const float* last_values,
+           const float* last_dones, float* advantages, float* returns, int T, int N, float gamma, float gae_lambda,
+           void* stream);
 const char* hs_last_error(void);
 const char* hs_version(void);
 

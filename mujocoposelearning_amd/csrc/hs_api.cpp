@@ -343,6 +343,20 @@ int hs_get_debug(hs_batch* b, double* out, int n) {
   return 0;
 }
 
+int hs_gae(const float* rewards, const float* values, const float* episode_starts, const float* last_values,
+           const float* last_dones, float* advantages, float* returns, int T, int N, float gamma, float gae_lambda,
+           void* stream) {
+  if (T < 0 || N < 0) return fail("hs_gae: negative size");
+  if (T == 0 || N == 0) return 0;
+  if (!rewards || !values || !episode_starts || !last_values || !last_dones || !advantages || !returns)
+    return fail("hs_gae: null buffer");
+  return hip_ok(hs::launch_gae(rewards, values, episode_starts, last_values, last_dones, advantages, returns, T, N,
+                               gamma, gae_lambda, (hipStream_t)stream),
+                "gae_kernel")
+             ? 0
+             : -1;
+}
+
 int hs_synchronize(hs_batch* b) {
   if (!b) return fail("null batch");
   DeviceGuard g(b->device);

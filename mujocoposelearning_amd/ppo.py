@@ -71,8 +71,14 @@ class ActorCritic(nn.Module):
 
 
 def gae(rewards, values, dones, last_values, last_dones, gamma, lam):
-    """SB3 RolloutBuffer.compute_returns_and_advantage: reverse scan over time, vectorised over envs.
-    rewards/values/dones: [T, N] (dones[t] = episode_start flag of step t, as SB3 stores it)."""
+    """SB3 RolloutBuffer.compute_returns_and_advantage (stable_baselines3 2.3.2 common/buffers.py):
+    reverse scan over time, vectorised over envs.  rewards/values/dones: [T, N] (dones[t] = the
+    episode_start flag of step t, as SB3 stores it).  Returns (advantages, returns).
+
+    On a GPU the scan is the HIP kernel ``hs_gae`` (gae.hip, one launch per rollout); on the CPU
+    (tests, toy envs) it is this torch loop."""
+    if rewards.is_cuda:
+        return gae_device(rewards, values, dones, last_values, last_dones, gamma, lam)
     T = rewards.shape[0]
     adv = torch.zeros_like(rewards)
     last = torch.zeros_like(last_values)
@@ -87,6 +93,21 @@ def gae(rewards, values, dones, last_values, last_dones, gamma, lam):
         last = delta + gamma * lam * nonterm * last
         adv[t] = last
     return adv, adv + values
+
+
+def gae_device(rewards, values, dones, last_values, last_dones, gamma, lam):
+    """GAE through the C ABI (hs_gae) on the tensors' device and current stream; float32."""
+    from . import _lib
+    T, N = rewards.shape
+    f32 = lambda x: x.to(torch.float32).contiguous()   # noqa: E731
+    r, v, st, lv, ld = f32(rewards), f32(values), f32(dones), f32(last_values), f32(last_dones)
+    adv = torch.empty_like(r)
+    ret = torch.empty_like(r)
+    with torch.cuda.device(r.device):
+        stream = torch.cuda.current_stream(r.device).cuda_stream
+        _lib.check(_lib.lib().hs_gae(r.data_ptr(), v.data_ptr(), st.data_ptr(), lv.data_ptr(), ld.data_ptr(),
+                                     adv.data_ptr(), ret.data_ptr(), T, N, float(gamma), float(lam), stream))
+    return adv, ret
 
 
 class PPO:
