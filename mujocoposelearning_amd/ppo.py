@@ -135,6 +135,7 @@ class PPO:
         if isinstance(act, str):
             act = getattr(nn, act)
         self.env = env
+        self.policy_kwargs, self.net_arch, self.learning_rate = pk, net, learning_rate
         self.device = torch.device(env.device)
         torch.manual_seed(seed)          # identical initial weights on every rank
         self.policy = ActorCritic(env.obs_dim, env.act_dim, net["pi"], net["vf"], act,
@@ -246,13 +247,34 @@ class PPO:
                 break
         return self
 
+    @torch.no_grad()
+    def predict(self, observation, state=None, episode_start=None, deterministic=False):
+        """SB3 BaseAlgorithm.predict (render_policy.py:30): obs (obs_dim,) or (n, obs_dim) ->
+        (actions clipped to [-1, 1] as numpy, None)."""
+        obs = torch.as_tensor(np.asarray(observation), dtype=torch.float32, device=self.device)
+        single = obs.dim() == 1
+        a, _, _ = self.policy.act(obs[None] if single else obs, deterministic=deterministic)
+        a = a.clamp(-1.0, 1.0).cpu().numpy()
+        return (a[0] if single else a), None
+
+    def _data(self):
+        act = self.policy_kwargs.get("activation_fn", nn.Tanh)
+        return {"n_steps": self.n_steps, "batch_size": self.batch_size, "n_epochs": self.n_epochs,
+                "gamma": self.gamma, "gae_lambda": self.gae_lambda, "clip_range": self.clip_range,
+                "ent_coef": self.ent_coef, "vf_coef": self.vf_coef, "max_grad_norm": self.max_grad_norm,
+                "learning_rate": self.learning_rate, "num_timesteps": self.num_timesteps,
+                "n_envs": self.env.num_envs * self.world_size,
+                "policy_kwargs": {"net_arch": self.net_arch,
+                                  "activation_fn": act if isinstance(act, str) else act.__name__}}
+
     def save(self, path):
-        torch.save({"policy": self.policy.state_dict(), "optimizer": self.opt.state_dict(),
-                    "num_timesteps": self.num_timesteps}, path)
+        """SB3 checkpoint layout (train_sb3.py:234 ``model.save``): writes ``path``.zip."""
+        from .sb3_format import save_sb3_zip
+        return save_sb3_zip(path, self.policy, self.opt, self._data())
 
     def load(self, path):
-        ck = torch.load(path, map_location=self.device, weights_only=True)
-        self.policy.load_state_dict(ck["policy"])
-        self.opt.load_state_dict(ck["optimizer"])
-        self.num_timesteps = ck.get("num_timesteps", 0)
+        """Load weights + optimizer state from an SB3-layout zip (ours or SB3's own)."""
+        from .sb3_format import load_sb3_zip
+        data = load_sb3_zip(path, self.policy, self.opt, map_location=self.device)
+        self.num_timesteps = int(data.get("num_timesteps", 0))
         return self

@@ -70,6 +70,6 @@ def train_humanoid(env_kwargs: dict, ppo_kwargs: dict, xml_path: str = DEFAULT_X
     model.learn(total_timesteps=env_kwargs.get("total_timesteps", 20_000_000), callback=callback)
     if storage_path is not None and rank == 0:
         os.makedirs(storage_path, exist_ok=True)
-        model.save(os.path.join(storage_path, "final_model.pt"))
+        model.save(os.path.join(storage_path, "final_model"))     # -> final_model.zip (SB3 layout)
     env.close()
     return model

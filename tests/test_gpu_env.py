@@ -212,4 +212,4 @@ def test_train_humanoid_short_run(tmp_path):
     m = train_humanoid(env_kwargs, ppo_kwargs, xml_path=XML, storage_path=str(tmp_path))
     assert m.num_timesteps == 64 * 16 * 2
     assert np.isfinite(m.logger["policy_loss"]) and np.isfinite(m.logger["value_loss"])
-    assert (tmp_path / "final_model.pt").exists()
+    assert (tmp_path / "final_model.zip").exists()

@@ -177,3 +177,73 @@ def test_gloo_world2_one_allreduce_per_step_identical_weights(tmp_path):
     for x in r:
         assert x["calls"] == [n_params] * 16
         assert x["steps"] == 8 * 8 * world * 2
+
+
+SB3_MLP_KEYS = {   # ActorCriticPolicy state_dict of MlpPolicy, net_arch=dict(pi=[256,256], vf=[256,256])
+    "log_std": (21,),
+    "mlp_extractor.policy_net.0.weight": (256, 352), "mlp_extractor.policy_net.0.bias": (256,),
+    "mlp_extractor.policy_net.2.weight": (256, 256), "mlp_extractor.policy_net.2.bias": (256,),
+    "mlp_extractor.value_net.0.weight": (256, 352), "mlp_extractor.value_net.0.bias": (256,),
+    "mlp_extractor.value_net.2.weight": (256, 256), "mlp_extractor.value_net.2.bias": (256,),
+    "action_net.weight": (21, 256), "action_net.bias": (21,),
+    "value_net.weight": (1, 256), "value_net.bias": (1,),
+}
+
+
+def test_sb3_zip_layout_names_and_optimizer_order(tmp_path):
+    import zipfile
+    import io
+    from mujocoposelearning_amd.sb3_format import save_sb3_zip, to_sb3_names
+    p = ActorCritic(352, 21, [256, 256], [256, 256])
+    names = list(to_sb3_names(p.state_dict()))
+    assert {k: tuple(v.shape) for k, v in to_sb3_names(p.state_dict()).items()} == SB3_MLP_KEYS
+    # SB3 parameters() order: the policy's own log_std, then mlp_extractor (pi, vf), action_net, value_net
+    order = [n for n, _ in p.named_parameters()]
+    assert [k for k in to_sb3_names(dict.fromkeys(order))] == [
+        "log_std", "mlp_extractor.policy_net.0.weight", "mlp_extractor.policy_net.0.bias",
+        "mlp_extractor.policy_net.2.weight", "mlp_extractor.policy_net.2.bias", "mlp_extractor.value_net.0.weight",
+        "mlp_extractor.value_net.0.bias", "mlp_extractor.value_net.2.weight", "mlp_extractor.value_net.2.bias",
+        "action_net.weight", "action_net.bias", "value_net.weight", "value_net.bias"]
+    opt = torch.optim.Adam(p.parameters(), lr=3e-4, eps=1e-5)
+    path = save_sb3_zip(tmp_path / "final_model", p, opt, {"gamma": 0.99})
+    assert path.endswith("final_model.zip")
+    with zipfile.ZipFile(path) as z:
+        assert {"data", "policy.pth", "policy.optimizer.pth", "pytorch_variables.pth",
+                "_stable_baselines3_version", "system_info.txt"} <= set(z.namelist())
+        sd = torch.load(io.BytesIO(z.read("policy.pth")), weights_only=True)
+        assert set(sd) == set(names)
+        assert z.read("_stable_baselines3_version") == b"2.3.2"
+        od = torch.load(io.BytesIO(z.read("policy.optimizer.pth")), weights_only=True)
+        assert od["param_groups"][0]["eps"] == 1e-5 and len(od["param_groups"][0]["params"]) == 13
+
+
+def test_load_sb3_named_zip_and_predict(tmp_path):
+    """A zip written with SB3's names (as SB3's own save produces) loads into our PPO."""
+    import zipfile
+    import io
+    env = ToyEnv(n=4)
+    model = PPO(env, n_steps=4, batch_size=8, policy_kwargs={"net_arch": {"pi": [8, 8], "vf": [8, 8]}})
+    src = ActorCritic(6, 3, [8, 8], [8, 8], torch.nn.Tanh)
+    with torch.no_grad():
+        for prm in src.parameters():
+            prm.normal_()
+    sd = {k.replace("pi_net.", "mlp_extractor.policy_net.").replace("vf_net.", "mlp_extractor.value_net."): v
+          for k, v in src.state_dict().items()}
+    buf = io.BytesIO()
+    torch.save(sd, buf)
+    path = tmp_path / "sb3_model.zip"
+    with zipfile.ZipFile(path, "w") as z:
+        z.writestr("policy.pth", buf.getvalue())
+        z.writestr("data", '{"num_timesteps": 1234, "policy_class": {":type:": "<class \'abc.ABCMeta\'>", '
+                           '":serialized:": "gAWVOwAAAAAAAACM"}}')
+    model.load(path)
+    assert model.num_timesteps == 1234
+    for a, b in zip(model.policy.parameters(), src.parameters()):
+        assert torch.equal(a, b)
+    obs = np.random.default_rng(0).normal(size=(5, 6))
+    act, state = model.predict(obs, deterministic=True)
+    assert state is None and act.shape == (5, 3) and np.all(np.abs(act) <= 1)
+    mean = src(torch.tensor(obs, dtype=torch.float32))[0].clamp(-1, 1).detach().numpy()
+    np.testing.assert_allclose(act, mean, rtol=1e-6, atol=1e-6)
+    a1, _ = model.predict(obs[0], deterministic=True)
+    assert a1.shape == (3,)
