@@ -102,6 +102,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-rollout", action="store_true")
     ap.add_argument("--no-gae", action="store_true")
+    ap.add_argument("--train-iters", type=int, default=2, help="PPO iterations of the train mode (0: skip)")
+    ap.add_argument("--dist-backend", default=os.environ.get("HSIM_BENCH_BACKEND", "nccl"),
+                    help="nccl (= RCCL over xGMI; the real multi-GPU run) or gloo (multi-rank rehearsal on one GPU)")
     ap.add_argument("--cpu-steps", type=int, default=60000, help="vec steps of the CPU baseline (~13 s)")
     args = ap.parse_args()
 
@@ -114,18 +117,25 @@ def main():
 
     import torch
     import torch.distributed as dist
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    gloo = args.dist_backend == "gloo"
+    # gloo rehearsal: ranks may share a GPU; nccl: one process per GPU (LOCAL_RANK = device)
+    dev_index = local_rank % max(1, torch.cuda.device_count()) if gloo else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        dist.init_process_group("nccl", device_id=dev)
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
+    red_dev = torch.device("cpu") if gloo else dev      # device of the timing reductions
 
     from mujocoposelearning_amd.model import HsModel
     from mujocoposelearning_amd.vec_env import HumanoidVecEnv
     cfg = {"model_path": XML, "duration": DURATION, "reward_config": {"type": "stand"}, "frame_skip": FRAME_SKIP}
     model = HsModel(XML)
     n = args.envs
-    env = HumanoidVecEnv(cfg, n_envs=n, device=local_rank, precision=args.precision, seed=1000 + rank,
+    env = HumanoidVecEnv(cfg, n_envs=n, device=dev_index, precision=args.precision, seed=1000 + rank,
                          model=model)
     env.reset_tensors()
     g = torch.Generator(device=dev).manual_seed(rank)
@@ -133,6 +143,7 @@ def main():
     tape = (torch.rand(tape_len, n, model.nu, device=dev, generator=g) * 2 - 1).contiguous()
 
     def barrier():
+        torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
@@ -150,7 +161,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps          # only the step kernel runs in this region
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
@@ -179,11 +190,34 @@ def main():
                 obs, *_ = env.step_tensors(a.clamp_(-1, 1))
             barrier()
             rel = time.perf_counter() - tr0
-        t = torch.tensor([rel], dtype=torch.float64, device=dev)
+        t = torch.tensor([rel], dtype=torch.float64, device=red_dev)
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         rollout = dict(value=n * rs * world / float(t.item()), unit="env_steps/s",
                        note="policy MLP[256,256] (pi+vf) forward + diag-Gaussian sample + clip + env step")
+
+    # train mode (SURVEY 8d iii): end-to-end on-device PPO iterations (rollout with the
+    # MLP[256,256] policy + GAE + clipped-surrogate updates with the per-step gradient all-reduce)
+    train_res = None
+    if args.train_iters > 0:
+        from mujocoposelearning_amd.ppo import PPO
+        tk = dict(n_steps=32, batch_size=32768, n_epochs=4, learning_rate=3e-4,
+                  policy_kwargs={"net_arch": {"pi": [256, 256], "vf": [256, 256]}, "activation_fn": "ReLU"})
+        ppo = PPO(env, seed=0, world_size=world, rank=rank, **tk)
+        ppo.learn(ppo.num_timesteps + n * tk["n_steps"] * world)          # warm-up iteration
+        barrier()
+        t_tr = time.perf_counter()
+        ppo.learn(ppo.num_timesteps + args.train_iters * n * tk["n_steps"] * world)
+        barrier()
+        t = torch.tensor([time.perf_counter() - t_tr], dtype=torch.float64, device=red_dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ts = float(t.item())
+        train_res = dict(value=args.train_iters * n * tk["n_steps"] * world / ts, unit="env_steps/s",
+                         iterations=args.train_iters, ms_per_iteration=ts / args.train_iters * 1e3,
+                         config={k: v for k, v in tk.items() if k != "policy_kwargs"} | {"net_arch": "[256,256] ReLU"},
+                         note="rollout (policy forward + env step) + GAE + 4 epochs of minibatch updates, "
+                              "one gradient all-reduce per optimizer step")
 
     # GAE leg: the rollout-end reverse scan (hs_gae) over an n_steps=2048 x n-env buffer -- an
     # HBM-bound kernel (12 B read + 8 B written per element), timed with HIP events on its stream
@@ -247,6 +281,7 @@ def main():
             "cpu_baseline": cpu_res,
             "rollout": rollout,
             "gae": gae_res,
+            "train": train_res,
             "sim_stats": stats,
         }
         print(json.dumps(out))

@@ -192,7 +192,12 @@ class PPO:
         import torch.distributed as dist
         grads = [p.grad for p in self.flat]
         flat = torch.cat([g.reshape(-1) for g in grads])
-        dist.all_reduce(flat)            # ONE RCCL all-reduce per optimizer step
+        if flat.is_cuda and dist.get_backend() == "gloo":     # multi-rank rehearsal without RCCL
+            host = flat.cpu()
+            dist.all_reduce(host)
+            flat.copy_(host)
+        else:
+            dist.all_reduce(flat)        # ONE RCCL all-reduce per optimizer step (xGMI ring)
         flat /= self.world_size
         o = 0
         for g in grads:

@@ -62,6 +62,38 @@ def divergence(prec, tape, nsub=1000, seed=0):
     print(f"[{prec} tape={tape}] " + " ".join(f"{s}:{eq:.1e}/{ev:.1e}/c{nc}" for s, eq, ev, nc in errs))
 
 
+def streams(n=4096, steps=100):
+    """Same 4096 envs split into S independent groups, each stepped on its own HIP stream: one
+    group's Newton-iteration tail overlaps the other groups' next launches."""
+    model = HsModel(XML)
+    for S in (1, 2, 4, 8):
+        m = n // S
+        bs = []
+        for gi in range(S):
+            b = HsBatch(model, m, precision="fp32", seed=1 + gi)
+            b.configure(frame_skip=3, duration=10.0, reward_id=0)
+            b.reset()
+            bs.append(b)
+        g = torch.Generator(device="cuda").manual_seed(0)
+        tape = torch.rand(steps + 5, n, model.nu, device="cuda", generator=g) * 2 - 1
+        torch.cuda.synchronize()
+        sts = [torch.cuda.Stream() for _ in range(S)]
+
+        def run(k0, k1):
+            for k in range(k0, k1):
+                for gi, (b, st) in enumerate(zip(bs, sts)):
+                    with torch.cuda.stream(st):
+                        b.step(tape[k, gi * m:(gi + 1) * m])
+        run(0, 5)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        run(5, 5 + steps)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t
+        print(f"[fp32] N={n} as {S} groups x {m} on {S} streams: {dt / steps * 1e3:.3f} ms/step -> "
+              f"{n * steps / dt:,.0f} env-steps/s")
+
+
 def tail(n=4096, steps=300, prec="fp32"):
     """Distribution of per-env Newton iterations / contacts over an episode, and the launch-time
     sensitivity to the Newton iteration cap (the launch ends with its slowest wave)."""
@@ -97,6 +129,9 @@ def tail(n=4096, steps=300, prec="fp32"):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "streams":
+        streams()
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "tail":
         tail()
         sys.exit(0)
