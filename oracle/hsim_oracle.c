@@ -818,7 +818,70 @@ static void reset_keep_warnings(const OrcModel* m, OrcData* d) {
   d->warning_badqpos = w0; d->warning_badqvel = w1; d->warning_badqacc = w2; d->warning_overflow = w3;
 }
 
-void orc_step(const OrcModel* m, OrcData* d) {
+/* ------------------------------------------------------------------ full-state option
+ * MuJoCo 3.2.5 engine_core_smooth.c, mj_rnePostConstraint (contact part): for every contact the
+ * world-frame contact force F (mj_contactForce decodes the pyramid rows: normal = sum of the 4
+ * row forces, tangent j = mu_j (f_2j - f_2j+1)) is applied at con->pos and moved to the subtree
+ * com of the body's root (mju_transformSpatial, force: torque += (pos - com) x F); body 1 of the
+ * contact gets -[torque, F], body 2 +[torque, F]; world (body 0) is skipped.  condim <= 3 carries
+ * no contact torque.  mj_subtreeVel: the com velocity of every body (cvel moved from the root's
+ * subtree com to xipos) times its mass, summed over subtrees, divided by the subtree mass. */
+static void cross3d(const double* a, const double* b, double* r) {
+  r[0] = a[1] * b[2] - a[2] * b[1];
+  r[1] = a[2] * b[0] - a[0] * b[2];
+  r[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+void orc_contact_forces(const OrcModel* m, OrcData* d) {
+  memset(d->cfrc_ext, 0, sizeof d->cfrc_ext);
+  memset(d->subtree_linvel, 0, sizeof d->subtree_linvel);
+  for (int c = 0; c < d->ncon; c++) {
+    const OrcContact* con = &d->contact[c];
+    int adr = con->efc_address;
+    if (adr < 0) continue;
+    double fl[3] = {0, 0, 0};                     /* contact-frame force (normal, t1, t2) */
+    if (con->dim == 1) {
+      fl[0] = d->efc_force[adr];
+    } else {
+      for (int j = 0; j < 2; j++) {
+        double fp = d->efc_force[adr + 2 * j], fm = d->efc_force[adr + 2 * j + 1];
+        fl[0] += fp + fm;
+        fl[1 + j] = (fp - fm) * con->friction[j];
+      }
+    }
+    double F[3];
+    for (int k = 0; k < 3; k++) F[k] = con->frame[k] * fl[0] + con->frame[3 + k] * fl[1] + con->frame[6 + k] * fl[2];
+    for (int side = 0; side < 2; side++) {
+      int b = m->geom_bodyid[con->geom[side]];
+      if (b == 0) continue;
+      const double* com = d->subtree_com[m->body_rootid[b]];
+      double r[3] = {con->pos[0] - com[0], con->pos[1] - com[1], con->pos[2] - com[2]}, t[3];
+      cross3d(r, F, t);
+      double sg = side == 0 ? -1.0 : 1.0;
+      for (int k = 0; k < 3; k++) { d->cfrc_ext[b][k] += sg * t[k]; d->cfrc_ext[b][3 + k] += sg * F[k]; }
+    }
+  }
+  double mv[OMAXB][3];
+  for (int b = 0; b < m->nbody; b++) {
+    const double* com = d->subtree_com[m->body_rootid[b]];
+    const double* cv = d->cvel[b];
+    double r[3] = {d->xipos[b][0] - com[0], d->xipos[b][1] - com[1], d->xipos[b][2] - com[2]}, w[3];
+    cross3d(cv, r, w);                            /* angular x offset */
+    for (int k = 0; k < 3; k++) mv[b][k] = m->body_mass[b] * (cv[3 + k] + w[k]);
+  }
+  for (int b = m->nbody - 1; b > 0; b--)
+    for (int k = 0; k < 3; k++) mv[m->body_parentid[b]][k] += mv[b][k];
+  for (int b = 0; b < m->nbody; b++) {
+    double sm = m->body_subtreemass[b] > 1e-15 ? m->body_subtreemass[b] : 1e-15;
+    for (int k = 0; k < 3; k++) d->subtree_linvel[b][k] = mv[b][k] / sm;
+  }
+}
+
+static void step_impl(const OrcModel* m, OrcData* d, int full);
+
+void orc_step(const OrcModel* m, OrcData* d) { step_impl(m, d, 0); }
+
+static void step_impl(const OrcModel* m, OrcData* d, int full) {
   for (int i = 0; i < m->nq; i++)                 /* mj_checkPos */
     if (isbad(d->qpos[i])) { d->warning_badqpos++; reset_keep_warnings(m, d); break; }
   for (int i = 0; i < m->nv; i++)                 /* mj_checkVel */
@@ -826,7 +889,15 @@ void orc_step(const OrcModel* m, OrcData* d) {
   orc_forward(m, d);
   for (int i = 0; i < m->nv; i++)                 /* mj_checkAcc */
     if (isbad(d->qacc[i])) { d->warning_badqacc++; reset_keep_warnings(m, d); orc_forward(m, d); break; }
+  if (full) orc_contact_forces(m, d);
   euler(m, d);
+}
+
+void orc_step_n_full(const OrcModel* m, OrcData* d, const double* ctrl, int nsub, int full) {
+  for (int s = 0; s < nsub; s++) {
+    memcpy(d->ctrl, ctrl, sizeof(double) * m->nu);
+    step_impl(m, d, full);
+  }
 }
 
 void orc_step_n(const OrcModel* m, OrcData* d, const double* ctrl, int nsub) {

@@ -62,7 +62,7 @@ typedef struct {
   double actuator_force[OMAXU];
   double qfrc_bias[OMAXV], qfrc_passive[OMAXV], qfrc_actuator[OMAXV], qfrc_smooth[OMAXV];
   double qfrc_constraint[OMAXV];
-  double cfrc_ext[OMAXB][6], subtree_linvel[OMAXB][3];   /* lazy fields: stay zero */
+  double cfrc_ext[OMAXB][6], subtree_linvel[OMAXB][3];   /* zero unless orc_step_full */
   int ncon;
   OrcContact contact[OMAXCON];
   int nefc;
@@ -86,6 +86,11 @@ void orc_reset_data(const OrcModel* m, OrcData* d);
 void orc_forward(const OrcModel* m, OrcData* d);
 void orc_step(const OrcModel* m, OrcData* d);
 void orc_step_n(const OrcModel* m, OrcData* d, const double* ctrl, int nsub);
+/* full-state option: after mj_forward, the contact part of mj_rnePostConstraint (cfrc_ext) and
+ * mj_subtreeVel (subtree_linvel), i.e. what MuJoCo computes when those fields are requested;
+ * the reference never requests them (zeros), so this is hsim's opt-in "full_state" mode. */
+void orc_contact_forces(const OrcModel* m, OrcData* d);
+void orc_step_n_full(const OrcModel* m, OrcData* d, const double* ctrl, int nsub, int full);
 #ifdef __cplusplus
 }
 #endif

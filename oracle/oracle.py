@@ -125,6 +125,10 @@ def lib():
             getattr(_LIB, fn).restype = None
         _LIB.orc_step_n.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
         _LIB.orc_step_n.restype = None
+        _LIB.orc_step_n_full.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int]
+        _LIB.orc_step_n_full.restype = None
+        _LIB.orc_contact_forces.argtypes = [C.c_void_p, C.c_void_p]
+        _LIB.orc_contact_forces.restype = None
         assert _LIB.orc_sizeof_model() == C.sizeof(OrcModel), "OrcModel layout mismatch"
         assert _LIB.orc_sizeof_data() == C.sizeof(OrcData), "OrcData layout mismatch"
     return _LIB
@@ -203,9 +207,15 @@ class Oracle:
     def forward(self):
         self.lib.orc_forward(C.byref(self.m), C.byref(self.d))
 
-    def step(self, ctrl=None, nsub=1):
+    def step(self, ctrl=None, nsub=1, full=False):
+        """nsub x mj_step; full=True also computes cfrc_ext / subtree_linvel after mj_forward
+        (hsim's full_state option; zeros otherwise, as in the reference)."""
         c = np.zeros(self.M["nu"]) if ctrl is None else np.ascontiguousarray(ctrl, dtype=np.float64)
-        self.lib.orc_step_n(C.byref(self.m), C.byref(self.d), c.ctypes.data, int(nsub))
+        self.lib.orc_step_n_full(C.byref(self.m), C.byref(self.d), c.ctypes.data, int(nsub), int(bool(full)))
+
+    def contact_forces(self):
+        """cfrc_ext / subtree_linvel of the current (forward) state."""
+        self.lib.orc_contact_forces(C.byref(self.m), C.byref(self.d))
 
     def get(self, name):
         nb, nv, nj, ng = self.M["nbody"], self.M["nv"], self.M["njnt"], self.M["ngeom"]

@@ -263,3 +263,85 @@ def test_oracle_struct_layout_matches_c():
     L = O.lib()
     assert L.orc_sizeof_model() == C.sizeof(O.OrcModel)
     assert L.orc_sizeof_data() == C.sizeof(O.OrcData)
+
+
+# ---------------------------------------------------------------- full-state option (cfrc_ext, subtree_linvel)
+def _chain_masks(o):
+    """dof j moves body b iff j is on b's chain (body_dofadr..dofnum of b and its ancestors)."""
+    nb, nv = o.M["nbody"], o.M["nv"]
+    parent, adr, num = o.M["body_parentid"], o.M["body_dofadr"], o.M["body_dofnum"]
+    on = np.zeros((nb, nv), bool)
+    for b in range(1, nb):
+        a = b
+        while a > 0:
+            on[b, adr[a]:adr[a] + num[a]] = True
+            a = parent[a]
+    return on
+
+
+@pytest.mark.parametrize("key", ["squat", "prone", "supine"])
+def test_cfrc_ext_generalized_force_equals_contact_rows(orc, key):
+    """Power identity: sum_b cdof_j . cfrc_ext[b] over the bodies dof j moves == (J_c' f)_j, the
+    contact part of qfrc_constraint from the efc Jacobian path (an independent computation)."""
+    q = orc.M["keyframes"][key].copy()
+    q[2] -= 0.005
+    orc.qpos[:] = q
+    orc.qvel[:] = np.random.default_rng(3).normal(0, 0.5, 27)
+    orc.forward()
+    orc.contact_forces()
+    d, nv = orc.d, orc.M["nv"]
+    ne = d.nefc
+    J = np.ctypeslib.as_array(d.efc_J)[:ne, :nv]
+    f = np.ctypeslib.as_array(d.efc_force)[:ne]
+    typ = np.ctypeslib.as_array(d.efc_type)[:ne]
+    contact = typ >= 5
+    assert contact.any() and np.abs(f[contact]).max() > 1.0
+    expect = J[contact].T @ f[contact]
+    cf, cdof, on = orc.get("cfrc_ext"), orc.get("cdof"), _chain_masks(orc)
+    got = np.array([sum(cdof[j] @ cf[b] for b in range(1, orc.M["nbody"]) if on[b, j]) for j in range(nv)])
+    assert np.allclose(got, expect, rtol=1e-9, atol=1e-9 * np.abs(expect).max())
+
+
+def test_cfrc_ext_resultant_and_static_equilibrium(orc):
+    """Lying still on the floor: the floor's resultant force carries the weight and the com
+    velocity vanishes."""
+    q = orc.M["keyframes"]["prone"].copy()
+    orc.qpos[:] = q
+    for _ in range(2000):
+        orc.step(None, 1, full=True)
+    cf = orc.get("cfrc_ext")
+    total = cf[1:, 3:].sum(0)
+    mg = orc.M["body_subtreemass"][0] * 9.81
+    assert abs(total[2] - mg) < 0.02 * mg and np.abs(total[:2]).max() < 0.02 * mg
+    assert np.linalg.norm(orc.get("subtree_linvel")[0]) < 1e-2
+
+
+def test_subtree_linvel_is_momentum_over_mass():
+    """subtree_linvel[0] * M == sum_b (m_b lin_b - (m_b d_b) x ang_b) from cinert/cvel, and with no
+    gravity/contacts it stays constant (momentum conservation) over the Euler steps."""
+    from oracle.oracle import Oracle
+    o = Oracle(XML)
+    _strip_model(o, gravity=False)
+    q, v = _random_state(o, 9)
+    o.qpos[:] = q
+    o.qvel[:] = v
+    o.forward()
+    o.contact_forces()
+    p = np.zeros(3)
+    for b in range(1, o.M["nbody"]):
+        i, vel = o.get("cinert")[b], o.get("cvel")[b]
+        p += i[9] * vel[3:] - np.cross(i[6:9], vel[:3])
+    M = o.M["body_subtreemass"][0]
+    lv0 = o.get("subtree_linvel")[0].copy()
+    assert np.allclose(lv0 * M, p, rtol=1e-12, atol=1e-12)
+    for _ in range(20):
+        o.step(None, 1, full=True)
+    # conserved up to semi-implicit Euler's O(h) momentum error (pinned separately above)
+    assert np.allclose(o.get("subtree_linvel")[0], lv0, rtol=1e-2, atol=1e-2 * np.abs(lv0).max())
+
+
+def test_full_flag_off_keeps_reference_zeros(orc):
+    orc.qpos[:] = orc.M["keyframes"]["prone"]
+    for _ in range(50):
+        orc.step(None, 1)
+    assert not orc.get("cfrc_ext").any() and not orc.get("subtree_linvel").any()
