@@ -39,6 +39,12 @@ typedef struct hs_model hs_model;
 typedef struct hs_batch hs_batch;
 
 enum { HS_FP32 = 0, HS_FP64 = 1 };
+/* OR-ed into hs_batch_create's `precision` argument: the full-state option.  cfrc_ext (contact
+ * wrenches, mj_rnePostConstraint) and subtree_linvel (mj_subtreeVel) are computed every substep
+ * and the observation gains cfrc_ext[1:] -- the reference's commented-out obs component
+ * (custom_env.py:247,255) -- so obs_dim = 352 + 6 (nbody - 1) = 448 for humanoid.xml; rewards then
+ * read the real foot forces / com velocity.  Off (default) = the reference's zeros. */
+enum { HS_FULL_STATE = 0x100 };
 enum { HS_REWARD_NONE = -1, HS_REWARD_STAND = 0, HS_REWARD_KNEELING = 1, HS_REWARD_WALK = 2 };
 enum { HS_WARN_BADQPOS = 0, HS_WARN_BADQVEL = 1, HS_WARN_BADQACC = 2, HS_WARN_OVERFLOW = 3, HS_NWARN = 4 };
 #define HS_AUXDIM 40   /* per env aux row: qacc[32], com[3], ncon, nefc, newton iterations, pad */
@@ -77,6 +83,8 @@ typedef struct {
   uint8_t* terminated;     /* [N]      */
   uint8_t* truncated;      /* [N]      */
   void* aux;               /* [N][HS_AUXDIM] */
+  void* cfrc_ext;          /* [N][nbody][6]  (torque, force) at the root subtree com; HS_FULL_STATE only */
+  void* subtree_linvel;    /* [N][nbody][3]  HS_FULL_STATE only */
 } hs_buffers;
 
 typedef struct {
@@ -90,7 +98,7 @@ int hs_model_field(const hs_model* m, const char* name, double* out, int n);
 /* external == NULL: the library allocates (hipMalloc) and owns the buffers.
  * external != NULL: every pointer must be a device buffer of the documented size on `device`;
  * the caller keeps ownership (used by the Python layer to hand in torch-allocated tensors). */
-hs_batch* hs_batch_create(const hs_model* m, int n_envs, int device, uint64_t seed, int precision,
+hs_batch* hs_batch_create(const hs_model* m, int n_envs, int device, uint64_t seed, int precision /* | flags */,
                           const hs_buffers* external);
 void hs_batch_destroy(hs_batch* b);
 int hs_batch_get_info(const hs_batch* b, hs_batch_info* out);

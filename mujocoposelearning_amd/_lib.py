@@ -13,6 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HSIM_LIB", os.path.join(HERE, "libhsim.so"))   # HSIM_LIB: diagnostic builds
 
 HS_FP32, HS_FP64 = 0, 1
+HS_FULL_STATE = 0x100      # OR-ed into hs_batch_create's precision: cfrc_ext / subtree_linvel + 448-dim obs
 HS_REWARD_NONE, HS_REWARD_STAND, HS_REWARD_KNEELING, HS_REWARD_WALK = -1, 0, 1, 2
 HS_NWARN = 4
 HS_AUXDIM = 40
@@ -28,7 +29,7 @@ class hs_env_config(C.Structure):
 class hs_buffers(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ("qpos", "qvel", "qacc_warmstart", "ctrl", "time", "step_count", "episode",
                                           "total_reward", "warning", "obs", "terminal_obs", "reward", "terminated",
-                                          "truncated", "aux")]
+                                          "truncated", "aux", "cfrc_ext", "subtree_linvel")]
 
 
 class hs_batch_info(C.Structure):

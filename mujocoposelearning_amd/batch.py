@@ -25,7 +25,7 @@ def _torch():
 
 
 class HsBatch:
-    def __init__(self, model, n_envs, device=0, seed=0, precision="fp32"):
+    def __init__(self, model, n_envs, device=0, seed=0, precision="fp32", full_state=False):
         torch = _torch()
         if not torch.cuda.is_available():
             raise RuntimeError("HsBatch needs a ROCm GPU (torch.cuda.is_available() is False)")
@@ -36,16 +36,20 @@ class HsBatch:
         prec = _lib.HS_FP64 if precision == "fp64" else _lib.HS_FP32
         self.dtype = torch.float64 if prec == _lib.HS_FP64 else torch.float32
         nq, nv, nu, nb = model.nq, model.nv, model.nu, model.nbody
-        self.obs_dim = (nq - 2) + nv + 10 * nb + 6 * nb + nv
+        self.full_state = bool(full_state)
+        # custom_env.py:242-256 (352 for humanoid.xml); full_state adds cfrc_ext[1:] (their :247)
+        self.obs_dim = (nq - 2) + nv + 10 * nb + 6 * nb + nv + (6 * (nb - 1) if self.full_state else 0)
         N, f, i32, u8 = self.n, self.dtype, torch.int32, torch.uint8
         z = lambda *s, dt=f: torch.zeros(*s, dtype=dt, device=self.device)  # noqa: E731
         self.t = dict(qpos=z(N, nq), qvel=z(N, nv), qacc_warmstart=z(N, nv), ctrl=z(N, nu), time=z(N),
                       step_count=z(N, dt=i32), episode=z(N, dt=i32), total_reward=z(N),
                       warning=z(N, _lib.HS_NWARN, dt=i32), obs=z(N, self.obs_dim), terminal_obs=z(N, self.obs_dim),
-                      reward=z(N), terminated=z(N, dt=u8), truncated=z(N, dt=u8), aux=z(N, _lib.HS_AUXDIM))
+                      reward=z(N), terminated=z(N, dt=u8), truncated=z(N, dt=u8), aux=z(N, _lib.HS_AUXDIM),
+                      cfrc_ext=z(N, nb, 6), subtree_linvel=z(N, nb, 3))
         bufs = _lib.hs_buffers(**{k: v.data_ptr() for k, v in self.t.items()})
         torch.cuda.synchronize(self.device)
-        h = lib().hs_batch_create(model.handle, self.n, self.device.index, int(seed) & (2 ** 64 - 1), prec,
+        flags = prec | (_lib.HS_FULL_STATE if self.full_state else 0)
+        h = lib().hs_batch_create(model.handle, self.n, self.device.index, int(seed) & (2 ** 64 - 1), flags,
                                   C.byref(bufs))
         if not h:
             raise _lib.HsimError(lib().hs_last_error().decode())

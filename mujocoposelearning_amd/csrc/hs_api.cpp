@@ -16,6 +16,7 @@ struct hs_model {
 struct hs_batch {
   const hs_model* model = nullptr;
   int n = 0, device = 0, precision = HS_FP32, obs_dim = 0;
+  bool full_state = false;
   uint64_t seed = 0;
   void* dmodel = nullptr;
   hs_buffers buf{};
@@ -70,6 +71,8 @@ hs::EnvBuffers<T> env_buffers(const hs_batch* b) {
   e.terminated = b->buf.terminated;
   e.truncated = b->buf.truncated;
   e.aux = (T*)b->buf.aux;
+  e.cfrc_ext = (T*)b->buf.cfrc_ext;
+  e.subtree_linvel = (T*)b->buf.subtree_linvel;
   e.dbg = b->debug ? (T*)b->dbg : nullptr;
   return e;
 }
@@ -83,6 +86,7 @@ hs::StepParams params_of(const hs_batch* b, int mode, int nsub) {
   p.autoreset = b->cfg.autoreset;
   p.obs_dim = b->obs_dim;
   p.max_newton = b->cfg.max_newton;
+  p.full_state = b->full_state ? 1 : 0;
   p.duration = b->cfg.duration;
   p.init_height = b->cfg.init_height;
   p.noise_scale = b->cfg.noise_scale;
@@ -141,7 +145,9 @@ bool init_state(hs_batch* b) {
          hip_ok(hipMemset(b->buf.reward, 0, (size_t)N * es), "init") &&
          hip_ok(hipMemset(b->buf.terminated, 0, (size_t)N), "init") &&
          hip_ok(hipMemset(b->buf.truncated, 0, (size_t)N), "init") &&
-         hip_ok(hipMemset(b->buf.aux, 0, (size_t)N * hs::AUXDIM * es), "init");
+         hip_ok(hipMemset(b->buf.aux, 0, (size_t)N * hs::AUXDIM * es), "init") &&
+         (!b->buf.cfrc_ext || hip_ok(hipMemset(b->buf.cfrc_ext, 0, (size_t)N * m.nbody * 6 * es), "init")) &&
+         (!b->buf.subtree_linvel || hip_ok(hipMemset(b->buf.subtree_linvel, 0, (size_t)N * m.nbody * 3 * es), "init"));
 }
 
 template <typename T>
@@ -196,7 +202,14 @@ int hs_model_field(const hs_model* m, const char* name, double* out, int n) {
 hs_batch* hs_batch_create(const hs_model* m, int n_envs, int device, uint64_t seed, int precision,
                           const hs_buffers* external) {
   if (!m || n_envs <= 0) { fail("hs_batch_create: null model or n_envs <= 0"); return nullptr; }
-  if (precision != HS_FP32 && precision != HS_FP64) { fail("precision must be HS_FP32 or HS_FP64"); return nullptr; }
+  if ((precision & ~HS_FULL_STATE) != HS_FP32 && (precision & ~HS_FULL_STATE) != HS_FP64) {
+    fail("precision must be HS_FP32 or HS_FP64 (optionally | HS_FULL_STATE)");
+    return nullptr;
+  }
+  if ((precision & HS_FULL_STATE) && external && (!external->cfrc_ext || !external->subtree_linvel)) {
+    fail("HS_FULL_STATE needs external cfrc_ext and subtree_linvel buffers");
+    return nullptr;
+  }
   int ndev = 0;
   hipError_t de = hipGetDeviceCount(&ndev);
   if (de != hipSuccess || ndev == 0) {
@@ -211,8 +224,10 @@ hs_batch* hs_batch_create(const hs_model* m, int n_envs, int device, uint64_t se
   b->n = n_envs;
   b->device = device;
   b->seed = seed;
+  b->full_state = (precision & HS_FULL_STATE) != 0;
+  precision &= ~HS_FULL_STATE;
   b->precision = precision;
-  b->obs_dim = obs_dim_of(m->host);
+  b->obs_dim = obs_dim_of(m->host) + (b->full_state ? 6 * (m->host.nbody - 1) : 0);
   b->cfg.frame_skip = 5;
   b->cfg.max_steps = 750;
   b->cfg.reward_id = HS_REWARD_STAND;
@@ -240,7 +255,8 @@ hs_batch* hs_batch_create(const hs_model* m, int n_envs, int device, uint64_t se
          al(&b->buf.total_reward, N * es) && al((void**)&b->buf.warning, N * HS_NWARN * 4) &&
          al(&b->buf.obs, N * b->obs_dim * es) && al(&b->buf.terminal_obs, N * b->obs_dim * es) &&
          al(&b->buf.reward, N * es) && al((void**)&b->buf.terminated, N) && al((void**)&b->buf.truncated, N) &&
-         al(&b->buf.aux, N * hs::AUXDIM * es);
+         al(&b->buf.aux, N * hs::AUXDIM * es) && al(&b->buf.cfrc_ext, N * h.nbody * 6 * es) &&
+         al(&b->buf.subtree_linvel, N * h.nbody * 3 * es);
     if (!ok) { hs_batch_destroy(b); return nullptr; }
   }
   if (!hip_ok(hipMalloc(&b->dbg, hs::DBGDIM * 8), "hipMalloc(dbg)")) { hs_batch_destroy(b); return nullptr; }
@@ -255,7 +271,8 @@ void hs_batch_destroy(hs_batch* b) {
   if (b->owns) {
     void* ptrs[] = {b->buf.qpos, b->buf.qvel, b->buf.qacc_warmstart, b->buf.ctrl, b->buf.time, b->buf.step_count,
                     b->buf.episode, b->buf.total_reward, b->buf.warning, b->buf.obs, b->buf.terminal_obs,
-                    b->buf.reward, b->buf.terminated, b->buf.truncated, b->buf.aux};
+                    b->buf.reward, b->buf.terminated, b->buf.truncated, b->buf.aux, b->buf.cfrc_ext,
+                    b->buf.subtree_linvel};
     for (void* p : ptrs)
       if (p) (void)hipFree(p);
   }

@@ -32,6 +32,8 @@ struct EnvBuffers {
   uint8_t* terminated;   // [N]
   uint8_t* truncated;    // [N]
   T* aux;                // [N][AUXDIM]
+  T* cfrc_ext;           // [N][nbody][6]  (full_state)
+  T* subtree_linvel;     // [N][nbody][3]  (full_state)
   T* dbg;                // [DBGDIM] or nullptr
 };
 
@@ -43,7 +45,7 @@ struct StepParams {
   int autoreset;         // SB3 VecEnv auto-reset semantics
   int obs_dim;
   int max_newton;        // Newton iteration cap
-  int reserved;
+  int full_state;        // compute cfrc_ext / subtree_linvel; obs gains cfrc_ext[1:]
   double duration;       // custom_env.py:213 (10.0 in training)
   double init_height;    // custom_env.py:59 (1.282)
   double noise_scale;    // custom_env.py:109-110 (0.01)

@@ -324,7 +324,8 @@ struct Scratch {
              T xaxis[MAXJNT][3]; T gpos[MAXGEOM][3]; T gax[MAXGEOM][3]; } k;   // kinematics + collision
     struct { T crb[MAXBODY][10]; T buf[MAXDOF][6]; } c;          // composite rigid body
     struct { T cdofdot[MAXDOF][6]; T cfrc[MAXBODY][6]; T csub[MAXBODY][6]; } r;   // RNE
-    struct { T bvel[MAXBODY][6]; } n;                             // J x mapping (rows, Newton)
+    struct { T bvel[MAXBODY][6];                                  // J x mapping (rows, Newton)
+             T cfrc[MAXBODY][6], linv[MAXBODY][3], mv[MAXBODY][3]; } n;   // full_state (after solve)
   } u;
 };
 
@@ -1239,6 +1240,49 @@ struct Stepper {
     HS_STAMP(clk, 12);
   }
 
+  // full_state: contact part of mj_rnePostConstraint (cfrc_ext, at the root subtree com: body 2 of a
+  // contact gets +[(p - com) x F, F], body 1 the opposite, world skipped) and mj_subtreeVel's linear
+  // part (m v_com of every body = m lin + ang x (m d) from cvel / cinert, summed over subtrees).
+  // Results stay in the Newton union (free after the solve) until obs / reward / commit read them.
+  __device__ __forceinline__ void post_constraint() {
+    phase_begin();
+    const int b = sl;
+    T cf[6] = {0, 0, 0, 0, 0, 0}, mv[3] = {0, 0, 0};
+    if (b > 0 && b < nb) {
+      for (int c = 0; c < s.ncon; c++) {
+        int p = s.con_pair[c];
+        int b1 = m->pair_b1[p], b2 = m->pair_b2[p];
+        if (b != b1 && b != b2) continue;
+        const T sg = b == b2 ? T(1) : T(-1);
+        T r[3] = {s.con_pos[c][0] - s.com[0], s.con_pos[c][1] - s.com[1], s.con_pos[c][2] - s.com[2]}, t[3];
+        cross3(r, s.con_F[c], t);
+        for (int k = 0; k < 3; k++) { cf[k] += sg * t[k]; cf[3 + k] += sg * s.con_F[c][k]; }
+      }
+      const T* ci = s.cinert[b];
+      const T* cv = s.cvel[b];
+      T w[3];
+      cross3(cv, ci + 6, w);
+      for (int k = 0; k < 3; k++) mv[k] = ci[9] * cv[3 + k] + w[k];
+    }
+    if (b < nb) {
+      for (int k = 0; k < 6; k++) s.u.n.cfrc[b][k] = cf[k];
+      for (int k = 0; k < 3; k++) s.u.n.mv[b][k] = mv[k];
+    }
+    WSYNC();
+    if (b < nb) {
+      const uint32_t dm = b == 0 ? ((1u << nb) - 2u) : m->body_descmask[b];
+      T a[3] = {0, 0, 0}, ms = 0;
+      for (int c = 1; c < nb; c++)
+        if (bit(dm, c)) {
+          for (int k = 0; k < 3; k++) a[k] += s.u.n.mv[c][k];
+          ms += s.cinert[c][9];
+        }
+      const T inv = T(1) / (ms > T(1e-15) ? ms : T(1e-15));
+      for (int k = 0; k < 3; k++) s.u.n.linv[b][k] = a[k] * inv;
+    }
+    WSYNC();
+  }
+
   // mj_Euler with implicit damping, mj_integratePos
   __device__ __forceinline__ void euler(T& time) {
     phase_begin();
@@ -1333,9 +1377,19 @@ __device__ __forceinline__ void physics_step(Stepper<T, NV>& st, const StepParam
       reset_state(m, s, sl, time, xws);
     }
   }
+  if (p.full_state) st.post_constraint();   // pre-integration state, like cinert / cvel in the obs
   st.euler(time);
   HS_STAMP(st.clk, 13);
   xws = st.qacc;
+}
+
+// sum |cfrc_ext| of the last two bodies ("feet", reward_functions.py:121-122,176-177)
+template <typename T>
+__device__ __forceinline__ void foot_forces(MPtr<T> m, const Scratch<T>& s, T& lf, T& rf) {
+  const int nb = m->nbody;
+  lf = 0;
+  rf = 0;
+  for (int k = 0; k < 6; k++) { lf += fabs(s.u.n.cfrc[nb - 2][k]); rf += fabs(s.u.n.cfrc[nb - 1][k]); }
 }
 
 template <typename T>
@@ -1353,8 +1407,10 @@ __device__ __forceinline__ T compute_reward(MPtr<T> m, const Scratch<T>& s, cons
     T torque = exp(T(-0.05) * c2);
     T post = T(0.5) * exp(T(-2) * (h - T(1.282)) * (h - T(1.282))) + T(0.5) * exp(T(-3) * (roll * roll + pitch * pitch));
     if (p.reward_id == REWARD_STAND) {
-      // cfrc_ext is never computed by mj_step without sensors -> both "feet" forces are 0
+      // cfrc_ext is never computed by mj_step without sensors -> both "feet" forces are 0 (full_state:
+      // the real wrenches of the last two bodies, reward_functions.py:176-177)
       T lf = 0, rf = 0;
+      if (p.full_state) foot_forces(m, s, lf, rf);
       T foot = 1 - fmin(lf, rf) / (lf + rf + T(1e-8));
       T vr = exp(T(-2) * (s.qvel[0] - 1) * (s.qvel[0] - 1));
       T r = T(0.4) * vr + T(0.3) * post + T(0.2) * foot + T(0.1) * torque;
@@ -1370,9 +1426,15 @@ __device__ __forceinline__ T compute_reward(MPtr<T> m, const Scratch<T>& s, cons
     T posture = T(0.7) * exp(T(-5) * (roll * roll + pitch * pitch) / (mrp * mrp)) +
                 T(0.3) * exp(T(-5) * (h - T(k[0])) * (h - T(k[0])));
     T dist = sqrt(s.com[0] * s.com[0] + s.com[1] * s.com[1]);
-    T comv = T(0);   // subtree_linvel is lazy in MuJoCo -> 0
-    T com = T(0.7) * exp(T(-10) * (dist / T(k[3]))) + T(0.3) * exp(T(-0.1) * comv);
+    T comv = T(0);   // subtree_linvel is lazy in MuJoCo -> 0 (full_state: |subtree_linvel[0]|^2)
     T foot = T(0);   // min(0,0)/(0+0+1e-8)
+    if (p.full_state) {
+      for (int q = 0; q < 3; q++) comv += s.u.n.linv[0][q] * s.u.n.linv[0][q];
+      T lf, rf;
+      foot_forces(m, s, lf, rf);
+      foot = fmin(lf, rf) / (lf + rf + T(1e-8));
+    }
+    T com = T(0.7) * exp(T(-10) * (dist / T(k[3]))) + T(0.3) * exp(T(-0.1) * comv);
     T energy = exp(T(-0.01) * energy_sum);
     T alive = 1 - exp(T(-0.5) * time);
     return T(k[5]) * posture + T(k[6]) * com + T(k[7]) * foot + T(k[4]) * energy + T(k[8]) * alive;
@@ -1395,6 +1457,9 @@ __device__ __forceinline__ void write_obs(MPtr<T> m, const Scratch<T>& s, int sl
     out[k] = v;
   }
   if (sl < nv && o4 + sl < obs_dim) out[o4 + sl] = qfa;
+  const int o5 = o4 + nv, nf = 6 * (m->nbody - 1);
+  if (obs_dim >= o5 + nf)    // full_state: + cfrc_ext[1:] (custom_env.py:247,255, commented out there)
+    for (int k = sl; k < nf; k += HL) out[o5 + k] = s.u.n.cfrc[1 + k / 6][k % 6];
 }
 
 template <typename T, int NV>
@@ -1431,7 +1496,8 @@ __device__ __forceinline__ void dump_debug(const Stepper<T, NV>& st, T* dbg) {
 // per-env commit of state + aux (one half-wave)
 template <typename T, int NV>
 __device__ __forceinline__ void commit(MPtr<T> m, const EnvBuffers<T>& b, const Stepper<T, NV>& st,
-                       int env, T time, T xws, int step_count, uint32_t episode, T total, const int* warn) {
+                       int env, T time, T xws, int step_count, uint32_t episode, T total, const int* warn,
+                       bool full) {
   const Scratch<T>& s = st.s;
   const int sl = st.sl, nq = m->nq, nv = m->nv, nu = m->nu;
   if (sl < nq) b.qpos[(size_t)env * nq + sl] = s.qpos[sl];
@@ -1451,6 +1517,11 @@ __device__ __forceinline__ void commit(MPtr<T> m, const EnvBuffers<T>& b, const 
     a[MAXDOF + 0] = s.com[0]; a[MAXDOF + 1] = s.com[1]; a[MAXDOF + 2] = s.com[2];
     a[MAXDOF + 3] = (T)s.ncon; a[MAXDOF + 4] = (T)s.nefc; a[MAXDOF + 5] = (T)st.niter;
     for (int k = 0; k < NWARN; k++) b.warning[(size_t)env * NWARN + k] += warn[k];
+  }
+  if (full) {   // data.cfrc_ext / data.subtree_linvel of the last substep (pre-integration)
+    const int nb = m->nbody;
+    for (int k = sl; k < 6 * nb; k += HL) b.cfrc_ext[(size_t)env * 6 * nb + k] = s.u.n.cfrc[k / 6][k % 6];
+    for (int k = sl; k < 3 * nb; k += HL) b.subtree_linvel[(size_t)env * 3 * nb + k] = s.u.n.linv[k / 3][k % 3];
   }
 }
 
@@ -1529,7 +1600,7 @@ __global__ __launch_bounds__(64, 2) void step_kernel(MPtr<T> m, EnvBuffers<T> b,
           }
         }
         if (active && !do_reset) {
-          commit(st.m, b, st, env, time, xws, step_count, episode, total, warn);
+          commit(st.m, b, st, env, time, xws, step_count, episode, total, warn, p.full_state != 0);
           active = false;   // committed; a reset pass below is scratch work for this half
         }
       }
@@ -1559,7 +1630,7 @@ __global__ __launch_bounds__(64, 2) void step_kernel(MPtr<T> m, EnvBuffers<T> b,
       if (do_reset && active) {
         if (b.dbg && env == 0) dump_debug(st, b.dbg);
         write_obs(st.m, s, sl, st.qfa, obs_out, p.obs_dim);
-        commit(st.m, b, st, env, time, xws, 0, episode, T(0), warn);
+        commit(st.m, b, st, env, time, xws, 0, episode, T(0), warn, p.full_state != 0);
       }
       break;
     } else {

@@ -76,7 +76,7 @@ class HsData:
     @property
     def qfrc_actuator(self):
         o1, o2, o3, o4 = self._slices()
-        return self._obs()[o4:]
+        return self._obs()[o4:o4 + self._env.model.nv]
 
     @property
     def subtree_com(self):
@@ -91,11 +91,17 @@ class HsData:
 
     @property
     def subtree_linvel(self):
-        return np.zeros((self._env.model.nbody, 3))   # lazy in MuJoCo mj_step: never computed
+        """Zeros as in the reference (lazy in mj_step); computed with ``full_state_obs``."""
+        if not self._b().full_state:
+            return np.zeros((self._env.model.nbody, 3))
+        return self._b().subtree_linvel[self._env._idx].double().cpu().numpy()
 
     @property
     def cfrc_ext(self):
-        return np.zeros((self._env.model.nbody, 6))   # lazy in MuJoCo mj_step: never computed
+        """Zeros as in the reference (lazy in mj_step); computed with ``full_state_obs``."""
+        if not self._b().full_state:
+            return np.zeros((self._env.model.nbody, 6))
+        return self._b().cfrc_ext[self._env._idx].double().cpu().numpy()
 
     @property
     def warning(self):
@@ -122,6 +128,8 @@ class HumanoidEnv(Env):
             device = env_config.get('device', 0)
             precision = env_config.get('precision', 'fp64')
             max_newton = env_config.get('max_newton', 100)
+            # opt-in: cfrc_ext / subtree_linvel computed (reference: zeros) and obs += cfrc_ext[1:]
+            full_state = bool(env_config.get('full_state_obs', False))
         else:
             self.model_path = env_config
             self.duration = 15
@@ -132,9 +140,9 @@ class HumanoidEnv(Env):
             self.frame_skip = 5
             self.grace_period_steps = 0
             self.total_reward = 0.0
-            device, precision, max_newton = 0, 'fp64', 100
+            device, precision, max_newton, full_state = 0, 'fp64', 100, False
         self.model = HsModel(self.model_path)
-        self._batch = HsBatch(self.model, 1, device=device, precision=precision)
+        self._batch = HsBatch(self.model, 1, device=device, precision=precision, full_state=full_state)
         self._idx = 0
         self.data = HsData(self)
         self.frames = []

@@ -48,7 +48,8 @@ class HumanoidVecEnv(_Base):
         cfg = env_config if isinstance(env_config, dict) else {"model_path": env_config}
         self.env_config = dict(cfg)
         self.model = model if model is not None else HsModel(cfg["model_path"])
-        self.batch = HsBatch(self.model, n_envs, device=device, precision=precision, seed=seed)
+        self.batch = HsBatch(self.model, n_envs, device=device, precision=precision, seed=seed,
+                             full_state=bool(cfg.get("full_state_obs", False)))
         self.duration = float(cfg.get("duration", 15))
         self.frame_skip = int(cfg.get("frame_skip", 5))
         self.reward_config = cfg.get("reward_config", {"type": "default"})

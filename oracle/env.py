@@ -15,6 +15,7 @@ class OracleHumanoidEnv:
         self.duration = env_config.get('duration', 15)
         self.reward_config = env_config.get('reward_config', {'type': 'default'})
         self.frame_skip = env_config.get('frame_skip', 5)
+        self.full = bool(env_config.get('full_state_obs', False))   # hsim's opt-in full-state mode
         self.sim = Oracle(self.model_path, M=M)
         self.M = self.sim.M
         self.init_qpos = self.M["qpos0"].copy()
@@ -40,7 +41,7 @@ class OracleHumanoidEnv:
         pos_noise[3:7] = 0
         self.sim.qpos[:] += pos_noise
         self.sim.qvel[:] += vel_noise
-        self.sim.step(None, 1)
+        self.sim.step(None, 1, full=self.full)
         self.step_count = 0
         self.total_reward = 0.0
         return self.get_state(), {}
@@ -48,8 +49,11 @@ class OracleHumanoidEnv:
     def get_state(self):
         """custom_env.py:232-261: qpos[2:], qvel, cinert, cvel, qfrc_actuator."""
         nb = self.M["nbody"]
-        return np.concatenate([self.sim.qpos[2:], self.sim.qvel, self.sim.get("cinert").reshape(nb * 10),
-                               self.sim.get("cvel").reshape(nb * 6), self.sim.get("qfrc_actuator")])
+        parts = [self.sim.qpos[2:], self.sim.qvel, self.sim.get("cinert").reshape(nb * 10),
+                 self.sim.get("cvel").reshape(nb * 6), self.sim.get("qfrc_actuator")]
+        if self.full:   # + cfrc_ext[1:] (custom_env.py:247, commented out in the reference)
+            parts.append(self.sim.get("cfrc_ext")[1:].reshape(-1))
+        return np.concatenate(parts)
 
     def compute_reward(self):
         t = self.reward_config.get('type', 'default')
@@ -62,7 +66,7 @@ class OracleHumanoidEnv:
     def step(self, action):
         self.step_count += 1
         a = np.asarray(action, dtype=np.float32).astype(np.float64)
-        self.sim.step(a, self.frame_skip)
+        self.sim.step(a, self.frame_skip, full=self.full)
         state = self.get_state()
         truncated = self.step_count >= 750
         reward = 0.0 if truncated else self.compute_reward()

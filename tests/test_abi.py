@@ -59,6 +59,14 @@ def test_batch_create_without_gpu_fails_loudly():
 
 
 def test_config_struct_layout():
+    """The ctypes mirrors follow include/hsim.h field by field (names, order, pointer size)."""
+    import os
+    import re
     from mujocoposelearning_amd import _lib
     assert C.sizeof(_lib.hs_env_config) == 6 * 4 + 3 * 8 + 9 * 8
-    assert C.sizeof(_lib.hs_buffers) == 15 * 8
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "hsim.h")).read()
+    body = re.search(r"typedef struct \{(.*?)\} hs_buffers;", hdr, re.S).group(1)
+    names = re.findall(r"\*\s*(\w+);", body)
+    assert [n for n, _ in _lib.hs_buffers._fields_] == names
+    assert C.sizeof(_lib.hs_buffers) == len(names) * 8
+    assert _lib.HS_FULL_STATE == int(re.search(r"HS_FULL_STATE = (0x[0-9a-fA-F]+)", hdr).group(1), 16)
