@@ -809,6 +809,7 @@ int model_field(const HostModel& m, const std::string& name, double* out, int n)
   else if (name == "ngeom") v = {(double)m.ngeom};
   else if (name == "ntendon") v = {(double)m.ntendon};
   else if (name == "opt_timestep") v = {m.timestep};
+  else if (name == "opt_gravity") v = {m.gravity[0], m.gravity[1], m.gravity[2]};
   else if (name == "stat_meaninertia") v = {m.meaninertia};
   else if (name == "body_parentid") I(m.body_parentid);
   else if (name == "body_rootid") I(m.body_rootid);

@@ -51,6 +51,12 @@ class HsModel:
             out = out.reshape((-1,) + (shp if isinstance(shp, tuple) else (shp,)))
         return out
 
+    @property
+    def opt(self):
+        """MjModel.opt subset (generate_trajectories.py:46 reads opt.timestep)."""
+        from types import SimpleNamespace
+        return SimpleNamespace(timestep=float(self.field("opt_timestep")[0]), gravity=self.field("opt_gravity"))
+
     def keyframe(self, name):
         return self.field("key_" + name)
 

@@ -213,3 +213,21 @@ def test_train_humanoid_short_run(tmp_path):
     assert m.num_timesteps == 64 * 16 * 2
     assert np.isfinite(m.logger["policy_loss"]) and np.isfinite(m.logger["value_loss"])
     assert (tmp_path / "final_model.zip").exists()
+
+
+def test_generate_trajectory_xml_with_saved_policy(tmp_path):
+    """generate_trajectories.py mirror end to end on the GPU engine: a PPO checkpoint saved in the
+    SB3 layout is reloaded and rolled out; the keyframes follow the reference file's layout."""
+    import xml.etree.ElementTree as ET
+    from mujocoposelearning_amd.ppo import ActorCritic
+    from mujocoposelearning_amd.sb3_format import save_sb3_zip
+    from mujocoposelearning_amd.trajectories import generate_trajectory_xml
+    pol = ActorCritic(352, 21, [64, 64], [64, 64])
+    zp = save_sb3_zip(tmp_path / "final_model", pol, None, {"policy_kwargs": {"net_arch": [64, 64],
+                                                                              "activation_fn": "Tanh"}})
+    out = generate_trajectory_xml(zp, XML, tmp_path / "traj.xml", num_steps=40, step_interval=5)
+    keys = ET.parse(out).getroot().find("keyframe").findall("key")
+    assert keys[4].get("name") == "initial_pose" and len(keys) == 4 + 1 + 8
+    assert [k.get("time") for k in keys[5:]] == [f"{s * 0.005:.3f}" for s in range(0, 40, 5)]
+    q = np.array(keys[4].get("qpos").split(), float)
+    assert abs(q[2] - 1.282) < 0.002 and np.isfinite(q).all()
