@@ -232,7 +232,7 @@ hs_batch* hs_batch_create(const hs_model* m, int n_envs, int device, uint64_t se
   b->cfg.max_steps = 750;
   b->cfg.reward_id = HS_REWARD_STAND;
   b->cfg.autoreset = 1;
-  b->cfg.max_newton = 100;
+  b->cfg.max_newton = m->host.iterations;     // <option iterations>
   b->cfg.duration = 15.0;
   b->cfg.init_height = 1.282;
   b->cfg.noise_scale = 0.01;

@@ -384,16 +384,40 @@ struct Compiler {
     return true;
   }
 
+  // <option>: timestep, gravity, iterations, tolerance are honoured; anything that changes the
+  // dynamics in a way the engine does not implement is rejected (never silently ignored).
+  bool parse_option(const XNode* k) {
+    if (k->get("timestep")) m.timestep = nums(k->get("timestep"))[0];
+    if (k->get("gravity")) {
+      auto g = nums(k->get("gravity"));
+      if (g.size() != 3) { err = "<option gravity> needs 3 numbers"; return false; }
+      for (int j = 0; j < 3; j++) m.gravity[j] = g[j];
+    }
+    if (k->get("iterations")) m.iterations = (int)nums(k->get("iterations"))[0];
+    if (k->get("tolerance")) m.tolerance = nums(k->get("tolerance"))[0];
+    auto is = [&](const char* a, const char* dflt) { return !k->get(a) || std::string(k->get(a)) == dflt; };
+    auto zero = [&](const char* a) {
+      if (!k->get(a)) return true;
+      for (double x : nums(k->get(a))) if (x != 0) return false;
+      return true;
+    };
+    if (!is("integrator", "Euler")) { err = "only integrator=\"Euler\" is supported (reference: MuJoCo default)"; return false; }
+    if (!is("cone", "pyramidal")) { err = "only cone=\"pyramidal\" is supported"; return false; }
+    if (!zero("noslip_iterations")) { err = "noslip solver not supported"; return false; }
+    if (!zero("density") || !zero("viscosity")) { err = "fluid forces (density/viscosity) not supported"; return false; }
+    for (auto& f : k->kids)
+      if (f->tag == "flag")
+        for (auto& a : f->attrs)
+          if (a.first != "energy") { err = "<option><flag " + a.first + "> not supported"; return false; }
+    return true;
+  }
+
   bool run(const XNode* root) {
     if (root->tag != "mujoco") { err = "root element must be <mujoco>"; return false; }
     classes["main"] = DefClass();
     for (auto& k : root->kids) {
       if (k->tag == "default") parse_defaults(k.get(), nullptr);
-      if (k->tag == "option" && k->get("timestep")) m.timestep = nums(k->get("timestep"))[0];
-      if (k->tag == "option" && k->get("gravity")) {
-        auto g = nums(k->get("gravity"));
-        for (int j = 0; j < 3; j++) m.gravity[j] = g[j];
-      }
+      if (k->tag == "option" && !parse_option(k.get())) return false;
       if (k->tag == "compiler" && k->get("angle") && std::string(k->get("angle")) != "degree") {
         err = "compiler angle other than degree not supported";
         return false;
@@ -810,6 +834,8 @@ int model_field(const HostModel& m, const std::string& name, double* out, int n)
   else if (name == "ntendon") v = {(double)m.ntendon};
   else if (name == "opt_timestep") v = {m.timestep};
   else if (name == "opt_gravity") v = {m.gravity[0], m.gravity[1], m.gravity[2]};
+  else if (name == "opt_iterations") v = {(double)m.iterations};
+  else if (name == "opt_tolerance") v = {m.tolerance};
   else if (name == "stat_meaninertia") v = {m.meaninertia};
   else if (name == "body_parentid") I(m.body_parentid);
   else if (name == "body_rootid") I(m.body_rootid);

@@ -167,7 +167,25 @@ def compile_mjcf(path):
         return out
 
     opt = root.find("option")
-    timestep = float(opt.get("timestep", 0.002)) if opt is not None else 0.002
+    o = opt.attrib if opt is not None else {}
+    timestep = float(o.get("timestep", 0.002))
+    gravity = np.array([float(x) for x in o.get("gravity", "0 0 -9.81").split()])
+    iterations = int(float(o.get("iterations", 100)))
+    tolerance = float(o.get("tolerance", 1e-8))
+    # options that change the dynamics beyond what the restatement covers are rejected, not ignored
+    if o.get("integrator", "Euler") != "Euler":
+        raise ValueError("only integrator='Euler' is supported")
+    if o.get("cone", "pyramidal") != "pyramidal":
+        raise ValueError("only cone='pyramidal' is supported")
+    if float(o.get("noslip_iterations", 0)) != 0:
+        raise ValueError("noslip solver not supported")
+    if float(o.get("density", 0)) != 0 or float(o.get("viscosity", 0)) != 0:
+        raise ValueError("fluid forces not supported")
+    if opt is not None:
+        for f in opt.findall("flag"):
+            for a in f.attrib:
+                if a != "energy":
+                    raise ValueError(f"<option><flag {a}> not supported")
 
     bodies = [dict(name="world", parent=-1, pos=np.zeros(3), quat=np.array([1.0, 0, 0, 0]))]
     joints, geoms = [], []
@@ -254,10 +272,10 @@ def compile_mjcf(path):
     nbody, njnt, ngeom = len(bodies), len(joints), len(geoms)
     M = {}
     M["opt_timestep"] = timestep
-    M["opt_gravity"] = np.array([0.0, 0.0, -9.81])
+    M["opt_gravity"] = gravity
     M["opt_impratio"] = 1.0
-    M["opt_tolerance"] = 1e-8
-    M["opt_iterations"] = 100
+    M["opt_tolerance"] = tolerance
+    M["opt_iterations"] = iterations
     M["opt_ls_iterations"] = 50
     M["nbody"], M["njnt"], M["ngeom"] = nbody, njnt, ngeom
     M["body_name"] = [b["name"] for b in bodies]

@@ -135,3 +135,40 @@ def test_product_compiler_errors(tmp_path):
     broken.write_text("<mujoco><worldbody>")
     with pytest.raises(HsimError, match="XML parse error"):
         HsModel(str(broken))
+
+
+def _variant(tmp_path, option):
+    src = open(XML).read()
+    assert '<option timestep="0.005"/>' in src or "<option" in src
+    import re
+    out = re.sub(r"<option[^>]*/>", option, src, count=1)
+    p = tmp_path / "variant.xml"
+    p.write_text(out)
+    return str(p)
+
+
+def test_option_overrides_agree_between_compilers(tmp_path):
+    """<option> timestep / gravity / iterations / tolerance are honoured by the product compiler
+    and the oracle compiler alike (compiler generality)."""
+    from mujocoposelearning_amd.model import HsModel
+    from oracle.model import compile_mjcf
+    p = _variant(tmp_path, '<option timestep="0.002" gravity="0.5 0 -5" iterations="20" tolerance="1e-10"/>')
+    m, M = HsModel(p), compile_mjcf(p)
+    assert m.opt.timestep == 0.002 == M["opt_timestep"]
+    assert np.array_equal(m.opt.gravity, [0.5, 0, -5]) and np.array_equal(M["opt_gravity"], [0.5, 0, -5])
+    assert m.field("opt_iterations")[0] == 20 == M["opt_iterations"]
+    assert m.field("opt_tolerance")[0] == 1e-10 == M["opt_tolerance"]
+
+
+@pytest.mark.parametrize("option", ['<option integrator="RK4"/>', '<option cone="elliptic"/>',
+                                    '<option noslip_iterations="3"/>', '<option density="1.2"/>',
+                                    '<option><flag contact="disable"/></option>'])
+def test_unsupported_options_fail_loudly_in_both_compilers(tmp_path, option):
+    from mujocoposelearning_amd._lib import HsimError
+    from mujocoposelearning_amd.model import HsModel
+    from oracle.model import compile_mjcf
+    p = _variant(tmp_path, option)
+    with pytest.raises(HsimError):
+        HsModel(p)
+    with pytest.raises(ValueError):
+        compile_mjcf(p)
