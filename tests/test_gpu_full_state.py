@@ -85,8 +85,9 @@ def test_default_keeps_reference_zeros(model):
 
 
 def test_full_state_fp32_batch_is_finite_and_carries_the_weight(model):
-    """configs[4]-style batch (full-state obs) in fp32: finite outputs, and for envs lying still
-    the summed contact force is about the weight."""
+    """configs[4]-style batch (full-state obs) in fp32: finite outputs, and once the passive
+    humanoids lie on the floor, the time-averaged vertical contact force equals the weight
+    (impulse balance: the average vertical acceleration of a lying body is ~0)."""
     import torch
     from mujocoposelearning_amd.batch import HsBatch
     n = 1024
@@ -96,10 +97,12 @@ def test_full_state_fp32_batch_is_finite_and_carries_the_weight(model):
     z = torch.zeros(n, 21, device=b.device)
     for _ in range(600):          # 9 s of passive collapse: everyone ends up lying on the floor
         obs, rew, *_ = b.step(z)
+    acc = torch.zeros(n, device=b.device, dtype=torch.float64)
+    for _ in range(200):
+        obs, rew, *_ = b.step(z)
+        acc += b.cfrc_ext[:, 1:, 5].sum(1).double()               # vertical force on all bodies
     torch.cuda.synchronize()
     assert torch.isfinite(obs).all() and torch.isfinite(rew).all()
-    fz = b.cfrc_ext[:, 1:, 5].sum(1)                                   # vertical force, all bodies
-    still = b.qvel.abs().max(1).values < 1e-2
-    assert still.sum() > n // 2
     mg = 40.84402122162132 * 9.81
-    assert ((fz[still] - mg).abs() < 0.05 * mg).float().mean() > 0.95
+    fz = acc / 200
+    assert ((fz - mg).abs() < 0.05 * mg).float().mean() > 0.9
