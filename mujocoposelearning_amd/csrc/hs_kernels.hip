@@ -807,11 +807,13 @@ struct Stepper {
   __device__ __forceinline__ void mass_matrix() {
     phase_begin();
     if (sl > 0 && sl < nb) {
-      uint32_t dm = m->body_descmask[sl];
+      const uint32_t dm = m->body_descmask[sl];
       T a[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-      for (int c = 1; c < nb; c++)
-        if ((dm >> c) & 1u)
-          for (int k = 0; k < 10; k++) a[k] += s.cinert[c][k];
+#pragma unroll 4
+      for (int c = 1; c < nb; c++) {   // predicated (no divergent branch), partially unrolled
+        const bool in = (dm >> c) & 1u;
+        for (int k = 0; k < 10; k++) a[k] += in ? s.cinert[c][k] : T(0);
+      }
       for (int k = 0; k < 10; k++) s.u.c.crb[sl][k] = a[k];
     }
     WSYNC();
@@ -845,35 +847,35 @@ struct Stepper {
     if (sl < nb) {
       T v[6] = {0, 0, 0, 0, 0, 0};
       if (sl > 0) {
-        uint32_t ch = m->body_chainmask[sl];
-        for (int j = 0; j < nv; j++)
-          if ((ch >> j) & 1u) {
-            T q = s.qvel[j];
-            for (int k = 0; k < 6; k++) v[k] += s.cdof[j][k] * q;
-          }
+        const uint32_t ch = m->body_chainmask[sl];
+#pragma unroll 4
+        for (int j = 0; j < nv; j++) {
+          const T q = ((ch >> j) & 1u) ? s.qvel[j] : T(0);
+          for (int k = 0; k < 6; k++) v[k] = fma(s.cdof[j][k], q, v[k]);
+        }
       }
       for (int k = 0; k < 6; k++) s.cvel[sl][k] = v[k];
     }
     if (sl < NV) {
-      uint32_t dm = m->dof_dotmask[sl];
+      const uint32_t dm = m->dof_dotmask[sl];
       T v[6] = {0, 0, 0, 0, 0, 0}, cdd[6];
-      for (int j = 0; j < nv; j++)
-        if ((dm >> j) & 1u) {
-          T q = s.qvel[j];
-          for (int k = 0; k < 6; k++) v[k] += s.cdof[j][k] * q;
-        }
+#pragma unroll 4
+      for (int j = 0; j < nv; j++) {
+        const T q = ((dm >> j) & 1u) ? s.qvel[j] : T(0);
+        for (int k = 0; k < 6; k++) v[k] = fma(s.cdof[j][k], q, v[k]);
+      }
       cross_motion(v, cd, cdd);
       for (int k = 0; k < 6; k++) s.u.r.cdofdot[sl][k] = cdd[k];
     }
     WSYNC();
     if (sl > 0 && sl < nb) {   // RNE: cacc, cfrc_body
-      uint32_t ch = m->body_chainmask[sl];
+      const uint32_t ch = m->body_chainmask[sl];
       T a[6] = {0, 0, 0, -m->gravity[0], -m->gravity[1], -m->gravity[2]};
-      for (int j = 0; j < nv; j++)
-        if ((ch >> j) & 1u) {
-          T q = s.qvel[j];
-          for (int k = 0; k < 6; k++) a[k] += s.u.r.cdofdot[j][k] * q;
-        }
+#pragma unroll 4
+      for (int j = 0; j < nv; j++) {
+        const T q = ((ch >> j) & 1u) ? s.qvel[j] : T(0);
+        for (int k = 0; k < 6; k++) a[k] = fma(s.u.r.cdofdot[j][k], q, a[k]);
+      }
       T f[6], t[6], t2[6];
       mul_inert(s.cinert[sl], a, f);
       mul_inert(s.cinert[sl], s.cvel[sl], t);
@@ -882,11 +884,13 @@ struct Stepper {
     }
     WSYNC();
     if (sl > 0 && sl < nb) {   // subtree sums of cfrc_body
-      uint32_t dm = m->body_descmask[sl];
+      const uint32_t dm = m->body_descmask[sl];
       T a[6] = {0, 0, 0, 0, 0, 0};
-      for (int c = 1; c < nb; c++)
-        if ((dm >> c) & 1u)
-          for (int k = 0; k < 6; k++) a[k] += s.u.r.cfrc[c][k];
+#pragma unroll 4
+      for (int c = 1; c < nb; c++) {
+        const bool in = (dm >> c) & 1u;
+        for (int k = 0; k < 6; k++) a[k] += in ? s.u.r.cfrc[c][k] : T(0);
+      }
       for (int k = 0; k < 6; k++) s.u.r.csub[sl][k] = a[k];
     }
     WSYNC();
