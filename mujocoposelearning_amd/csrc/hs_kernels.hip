@@ -371,13 +371,14 @@ __device__ __forceinline__ void make_frame(Con<T>& c) {
 
 // number of contacts (0..2) for static pair p (mjc_* primitives)
 template <typename T>
-__device__ __forceinline__ int collide_pair(MPtr<T> m, const Scratch<T>& s, int p, Con<T>& c0, Con<T>& c1) {
-  int g1 = m->pair_g1[p], g2 = m->pair_g2[p], fn = m->pair_fn[p];
+__device__ __forceinline__ int collide_pair(const Scratch<T>& s, const int4 info, const T (&sz)[4], Con<T>& c0,
+                                           Con<T>& c1) {
+  const int g1 = info.x, g2 = info.y, fn = info.z;
   const T* p1 = s.u.k.gpos[g1];
   const T* p2 = s.u.k.gpos[g2];
   const T* a1 = s.u.k.gax[g1];
   const T* a2 = s.u.k.gax[g2];
-  T r1 = m->geom_size[g1][0], r2 = m->geom_size[g2][0], h1 = m->geom_size[g1][1], h2 = m->geom_size[g2][1];
+  const T r1 = sz[0], h1 = sz[1], r2 = sz[2], h2 = sz[3];
   int n = 0;
   if (fn == PAIR_PLANE_SPHERE) {
     n = plane_sphere(p1, a1, p2, r2, c0) ? 1 : 0;
@@ -785,11 +786,17 @@ struct Stepper {
   __device__ __forceinline__ int collision() {
     phase_begin();
     int ncon = 0;
-    for (int base = 0; base < m->npair; base += HL) {
+    const int npair = m->npair;
+    for (int base = 0; base < npair; base += HL) {
       int p = base + sl;
       Con<T> c0, c1;
       int n = 0;
-      if (p < m->npair) n = collide_pair(m, s, p, c0, c1);
+      if (p < npair) {
+        const int4 info = make_int4(m->pair_info[p][0], m->pair_info[p][1], m->pair_info[p][2], m->pair_info[p][3]);
+        T sz[4];
+        for (int k = 0; k < 4; k++) sz[k] = m->pair_size[p][k];
+        n = collide_pair(s, info, sz, c0, c1);
+      }
       uint32_t m1 = hballot(n >= 1, up), m2 = hballot(n >= 2, up);
       int pre = below(m1, sl) + below(m2, sl);
       if (n >= 1) store_contact(m, s, ncon + pre, c0, p);

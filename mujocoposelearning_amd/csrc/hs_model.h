@@ -62,6 +62,10 @@ struct DevModel {
   int pair_g1[MAXPAIR], pair_g2[MAXPAIR], pair_b1[MAXPAIR], pair_b2[MAXPAIR];
   int pair_fn[MAXPAIR], pair_dim[MAXPAIR];
   T pair_mu[MAXPAIR], pair_margin[MAXPAIR], pair_solref[MAXPAIR][2], pair_solimp[MAXPAIR][5];
+  // what the narrow phase of one pair needs, packed into two 16-byte records per pair (one
+  // dwordx4 load each, no dependent geom-table lookup): {g1, g2, fn, dim}, {r1, h1, r2, h2}
+  alignas(16) int pair_info[MAXPAIR][4];
+  alignas(16) T pair_size[MAXPAIR][4];
   int ten_nwrap[MAXTEN], ten_wrapdof[MAXTEN][MAXWRAP], ten_wrapqadr[MAXTEN][MAXWRAP], ten_limited[MAXTEN];
   T ten_wrapcoef[MAXTEN][MAXWRAP], ten_range[MAXTEN][2], ten_solref[MAXTEN][2], ten_solimp[MAXTEN][5];
   T ten_margin[MAXTEN], ten_invweight0[MAXTEN];

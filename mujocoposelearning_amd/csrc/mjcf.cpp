@@ -1059,6 +1059,9 @@ bool build_dev_model(const HostModel& m, DevModel<T>& d, std::string& err) {
     }
     if (dim != 1 && dim != 3) { err = "only condim 1 and 3 supported"; return false; }
     d.pair_dim[p] = dim;
+    d.pair_info[p][0] = g1; d.pair_info[p][1] = g2; d.pair_info[p][2] = fn; d.pair_info[p][3] = dim;
+    d.pair_size[p][0] = (T)m.geom_size[3 * g1]; d.pair_size[p][1] = (T)m.geom_size[3 * g1 + 1];
+    d.pair_size[p][2] = (T)m.geom_size[3 * g2]; d.pair_size[p][3] = (T)m.geom_size[3 * g2 + 1];
     d.pair_mu[p] = (T)mu;
     d.pair_margin[p] = (T)(std::max(m.geom_margin[g1], m.geom_margin[g2]) - std::max(m.geom_gap[g1], m.geom_gap[g2]));
     if (std::max(m.geom_margin[g1], m.geom_margin[g2]) != 0) { err = "nonzero geom margin not supported"; return false; }
