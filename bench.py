@@ -103,6 +103,9 @@ def main():
     ap.add_argument("--no-rollout", action="store_true")
     ap.add_argument("--no-gae", action="store_true")
     ap.add_argument("--train-iters", type=int, default=2, help="PPO iterations of the train mode (0: skip)")
+    ap.add_argument("--groups", default="1", help="stream groups for the headline run (1 = one launch per step)")
+    ap.add_argument("--free-groups", type=int, default=4, help="extra sim-only leg: this many free-running stream "
+                                                                "groups (0: skip)")
     ap.add_argument("--dist-backend", default=os.environ.get("HSIM_BENCH_BACKEND", "nccl"),
                     help="nccl (= RCCL over xGMI; the real multi-GPU run) or gloo (multi-rank rehearsal on one GPU)")
     ap.add_argument("--cpu-steps", type=int, default=60000, help="vec steps of the CPU baseline (~13 s)")
@@ -135,8 +138,10 @@ def main():
     cfg = {"model_path": XML, "duration": DURATION, "reward_config": {"type": "stand"}, "frame_skip": FRAME_SKIP}
     model = HsModel(XML)
     n = args.envs
+    groups = args.groups if args.groups == "auto" else int(args.groups)
     env = HumanoidVecEnv(cfg, n_envs=n, device=dev_index, precision=args.precision, seed=1000 + rank,
-                         model=model)
+                         model=model, groups=groups)
+    n_groups = len(env.batch._groups)
     env.reset_tensors()
     g = torch.Generator(device=dev).manual_seed(rank)
     tape_len = min(args.steps + args.warmup, 256)
@@ -160,7 +165,7 @@ def main():
     ev1.record(stream)
     barrier()
     elapsed = time.perf_counter() - t0
-    kernel_ms = ev0.elapsed_time(ev1) / args.steps          # only the step kernel runs in this region
+    step_ms = ev0.elapsed_time(ev1) / args.steps
     t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -195,6 +200,51 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         rollout = dict(value=n * rs * world / float(t.item()), unit="env_steps/s",
                        note="policy MLP[256,256] (pi+vf) forward + diag-Gaussian sample + clip + env step")
+
+    # extra sim-only leg: the same n envs as free-running stream groups (no per-step join; the
+    # action tape is open-loop, so every env still takes exactly the same steps)
+    grouped = None
+    if args.free_groups > 1:
+        envg = HumanoidVecEnv(cfg, n_envs=n, device=dev_index, precision=args.precision, seed=3000 + rank,
+                              model=model, groups=args.free_groups)
+        envg.reset_tensors()
+        for k in range(args.warmup):
+            envg.batch.step(tape[k % tape_len], join=False)
+        envg.batch.join()
+        barrier()
+        tg = time.perf_counter()
+        for k in range(args.steps):
+            envg.batch.step(tape[(args.warmup + k) % tape_len], join=False)
+        envg.batch.join()
+        barrier()
+        t = torch.tensor([time.perf_counter() - tg], dtype=torch.float64, device=red_dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        grouped = dict(value=n * args.steps * world / float(t.item()), unit="env_steps/s", groups=args.free_groups,
+                       note="same workload as value, envs split into free-running stream groups (HsBatch "
+                            "join=False): one group's Newton tail overlaps the others' launches")
+        envg.close()
+
+    # roofline pass: the step kernel with all n envs in ONE launch per step (groups=1), HIP events on
+    # the stream it is launched on -- the per-launch figure rocprofv3 reports for profiles/collect.sh
+    if n_groups == 1:
+        kernel_ms = step_ms
+    else:
+        env1 = HumanoidVecEnv(cfg, n_envs=n, device=dev_index, precision=args.precision, seed=2000 + rank,
+                              model=model, groups=1)
+        env1.reset_tensors()
+        for k in range(args.warmup):
+            env1.step_tensors(tape[k % tape_len])
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        rsteps = min(args.steps, 50)
+        for k in range(rsteps):
+            env1.step_tensors(tape[(args.warmup + k) % tape_len])
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        kernel_ms = e0.elapsed_time(e1) / rsteps
+        env1.close()
 
     # train mode (SURVEY 8d iii): end-to-end on-device PPO iterations (rollout with the
     # MLP[256,256] policy + GAE + clipped-surrogate updates with the per-step gradient all-reduce)
@@ -271,16 +321,20 @@ def main():
             "config": {"workload": "configs[1]: humanoid.xml x 4096 envs per GPU, 'stand' reward, frame_skip 3, "
                                    "duration 10 (sim-only env steps)",
                        "n_envs_per_gpu": n, "n_envs_total": n * world, "frame_skip": FRAME_SKIP,
-                       "reward": "stand", "parallelism": f"dp{world} (env shards, no collective)"},
+                       "reward": "stand", "parallelism": f"dp{world} (env shards, no collective)",
+                       "stream_groups": n_groups},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "step_kernel<float,27>" if args.precision == "fp32" else "step_kernel<double,27>",
-                         "kernel_ms_per_launch": kernel_ms,
+                         "kernel_ms_per_launch": kernel_ms, "envs_per_launch": n,
                          "algo_bytes_per_env_step": ALGO_BYTES_PER_ENV_STEP,
-                         "note": "latency/VALU-bound kernel; HBM fraction reported per BASELINE.json"},
+                         "note": "latency/VALU-bound kernel; HBM fraction reported per BASELINE.json; measured "
+                                 "with all envs in one launch per step (the headline value uses "
+                                 f"{n_groups} stream groups; step time {step_ms:.3f} ms)"},
             "cpu_baseline": cpu_res,
             "rollout": rollout,
             "gae": gae_res,
+            "sim_only_stream_groups": grouped,
             "train": train_res,
             "sim_stats": stats,
         }

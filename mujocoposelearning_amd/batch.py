@@ -25,7 +25,13 @@ def _torch():
 
 
 class HsBatch:
-    def __init__(self, model, n_envs, device=0, seed=0, precision="fp32", full_state=False):
+    def __init__(self, model, n_envs, device=0, seed=0, precision="fp32", full_state=False, groups=1):
+        """``groups`` > 1 splits the envs into that many native sub-batches (contiguous env ranges
+        bound to slices of the same tensors), each launched on its own HIP stream: a group's
+        Newton-iteration tail can overlap the other groups' next launches.  That needs the groups
+        to run free (``step(..., join=False)`` then ``join()``): a per-step join (the default, what
+        a policy that reads every env's obs needs) makes each step as long as its slowest group.
+        Results per env are identical; reset-noise streams differ (per-group seeds)."""
         torch = _torch()
         if not torch.cuda.is_available():
             raise RuntimeError("HsBatch needs a ROCm GPU (torch.cuda.is_available() is False)")
@@ -46,16 +52,28 @@ class HsBatch:
                       warning=z(N, _lib.HS_NWARN, dt=i32), obs=z(N, self.obs_dim), terminal_obs=z(N, self.obs_dim),
                       reward=z(N), terminated=z(N, dt=u8), truncated=z(N, dt=u8), aux=z(N, _lib.HS_AUXDIM),
                       cfrc_ext=z(N, nb, 6), subtree_linvel=z(N, nb, 3))
-        bufs = _lib.hs_buffers(**{k: v.data_ptr() for k, v in self.t.items()})
         torch.cuda.synchronize(self.device)
         flags = prec | (_lib.HS_FULL_STATE if self.full_state else 0)
-        h = lib().hs_batch_create(model.handle, self.n, self.device.index, int(seed) & (2 ** 64 - 1), flags,
-                                  C.byref(bufs))
-        if not h:
-            raise _lib.HsimError(lib().hs_last_error().decode())
-        self._h = h
+        G = max(1, min(int(groups), self.n))
+        bounds = [self.n * g // G for g in range(G + 1)]
+        self._groups = []                       # (handle, lo, hi)
+        for g in range(G):
+            lo, hi = bounds[g], bounds[g + 1]
+            bufs = _lib.hs_buffers(**{k: v.data_ptr() + lo * v.stride(0) * v.element_size() for k, v in self.t.items()})
+            gseed = (int(seed) + 0x9E3779B97F4A7C15 * g) & (2 ** 64 - 1)
+            h = lib().hs_batch_create(model.handle, hi - lo, self.device.index, gseed, flags, C.byref(bufs))
+            if not h:
+                self.close()
+                raise _lib.HsimError(lib().hs_last_error().decode())
+            self._groups.append((h, lo, hi))
+        self._h = self._groups[0][0]
+        # group 0 runs on the caller's current stream, groups 1.. on their own: G groups use exactly G
+        # streams (a process has GPU_MAX_HW_QUEUES = 4 hardware queues; two streams sharing one serialise)
+        self._streams = [None] + [torch.cuda.Stream(self.device) for _ in range(G - 1)] if G > 1 else None
+        self._events = [torch.cuda.Event()] if G > 1 else None
+        self._free = False
         self.cfg = _lib.hs_env_config()
-        check(lib().hs_get_config(h, C.byref(self.cfg)))
+        check(lib().hs_get_config(self._h, C.byref(self.cfg)))
 
     # -- tensors (device views, valid until the next call) ---------------------------------
     def __getattr__(self, name):
@@ -92,52 +110,99 @@ class HsBatch:
             p = {**dict(zip(KNEEL_KEYS, KNEEL_DEFAULTS)), **kneel_params}
             for k, key in enumerate(KNEEL_KEYS):
                 c.kneel_params[k] = float(p[key])
-        check(lib().hs_set_config(self._h, C.byref(c)))
+        for h, _, _ in self._groups:
+            check(lib().hs_set_config(h, C.byref(c)))
 
     def set_seed(self, seed):
-        check(lib().hs_set_seed(self._h, int(seed) & (2 ** 64 - 1)))
+        for g, (h, _, _) in enumerate(self._groups):
+            check(lib().hs_set_seed(h, (int(seed) + 0x9E3779B97F4A7C15 * g) & (2 ** 64 - 1)))
+
+    def _launch(self, fn, *tensors, join=True):
+        """fn(handle, lo, hi, stream) per group; multi-group launches fan out to the group streams
+        and (join=True) join back into the caller's current stream.  A free-running session
+        (join=False) waits on the caller's stream once, at its first launch (inputs produced before
+        it); later free launches add no cross-stream waits (5 streams share the 4 hardware queues
+        of a process, GPU_MAX_HW_QUEUES=4, and per-step waits would serialise them again)."""
+        if self._streams is None:
+            h, lo, hi = self._groups[0]
+            fn(h, lo, hi, self.stream)
+            return
+        torch = _torch()
+        cur = torch.cuda.current_stream(self.device)
+        if join or not self._free:
+            self._events[0].record(cur)
+            for st in self._streams[1:]:
+                st.wait_event(self._events[0])
+        self._free = not join
+        for (h, lo, hi), st in zip(self._groups, self._streams):
+            if st is not None:
+                for t in tensors:
+                    if t is not None:
+                        t.record_stream(st)
+            fn(h, lo, hi, (cur if st is None else st).cuda_stream)
+        if join:
+            self.join()
+
+    def join(self):
+        """Make the caller's current stream wait for every group's last launch."""
+        if self._streams is None:
+            return
+        cur = _torch().cuda.current_stream(self.device)
+        for st in self._streams[1:]:
+            cur.wait_stream(st)
+        self._free = False
 
     # -- stepping --------------------------------------------------------------------------
     def reset(self, mask=None, qpos_noise=None, qvel_noise=None):
         """custom_env.py:97-150 for the envs selected by ``mask`` (None = all)."""
         torch = _torch()
         keep = []
-        def ptr(x, dt):
+        def dev(x, dt):
             if x is None:
                 return None
             x = torch.as_tensor(x, device=self.device).to(dt).contiguous()
             keep.append(x)
-            return x.data_ptr()
-        check(lib().hs_reset(self._h, ptr(mask, torch.uint8), ptr(qpos_noise, self.dtype), ptr(qvel_noise, self.dtype),
-                             self.stream))
+            return x
+        mk, qn, vn = dev(mask, torch.uint8), dev(qpos_noise, self.dtype), dev(qvel_noise, self.dtype)
+
+        def off(x, lo):
+            return None if x is None else x.data_ptr() + lo * x.stride(0) * x.element_size()
+        self._launch(lambda h, lo, hi, st: check(lib().hs_reset(h, off(mk, lo), off(qn, lo), off(vn, lo), st)),
+                     mk, qn, vn)
         return self.t["obs"]
 
-    def step(self, actions):
-        """custom_env.py:152-230 batched; ``actions`` [N, nu] float32 on device."""
+    def step(self, actions, join=True):
+        """custom_env.py:152-230 batched; ``actions`` [N, nu] float32 on device.  With stream
+        groups and join=False the groups run free; call ``join()`` before reading outputs."""
         torch = _torch()
         a = torch.as_tensor(actions, device=self.device).to(torch.float32).contiguous()
         assert a.shape == (self.n, self.model.nu), a.shape
-        check(lib().hs_step(self._h, a.data_ptr(), self.stream))
+        row = a.stride(0) * a.element_size()
+        self._launch(lambda h, lo, hi, st: check(lib().hs_step(h, a.data_ptr() + lo * row, st)), a, join=join)
         return self.t["obs"], self.t["reward"], self.t["terminated"], self.t["truncated"]
 
     def physics_step(self, ctrl=None, nsub=1):
         """nsub raw mj_step's with the given ctrl [N, nu] (None keeps the current ctrl)."""
         torch = _torch()
-        p = None
+        c = None
         if ctrl is not None:
             c = torch.as_tensor(ctrl, device=self.device).to(torch.float32).contiguous()
             assert c.shape == (self.n, self.model.nu), c.shape
-            p = c.data_ptr()
             self._keep = c
-        check(lib().hs_physics_step(self._h, p, int(nsub), self.stream))
+
+        def go(h, lo, hi, st):
+            p = None if c is None else c.data_ptr() + lo * c.stride(0) * c.element_size()
+            check(lib().hs_physics_step(h, p, int(nsub), st))
+        self._launch(go, c)
 
     # -- host state access (through the C ABI, synchronous, fp64) ---------------------------
     def get_state(self):
         N, m = self.n, self.model
         out = dict(qpos=np.zeros((N, m.nq)), qvel=np.zeros((N, m.nv)), qacc_warmstart=np.zeros((N, m.nv)),
                    time=np.zeros(N), ctrl=np.zeros((N, m.nu)))
-        check(lib().hs_state_io(self._h, 0, out["qpos"].ctypes.data, out["qvel"].ctypes.data,
-                                out["qacc_warmstart"].ctypes.data, out["time"].ctypes.data, out["ctrl"].ctypes.data))
+        keys = ("qpos", "qvel", "qacc_warmstart", "time", "ctrl")
+        for h, lo, hi in self._groups:
+            check(lib().hs_state_io(h, 0, *[out[k][lo:hi].ctypes.data for k in keys]))
         return out
 
     def set_state(self, qpos=None, qvel=None, qacc_warmstart=None, time=None, ctrl=None):
@@ -148,7 +213,8 @@ class HsBatch:
             return a, a.ctypes.data
         N, m = self.n, self.model
         keep = [p(qpos, (N, m.nq)), p(qvel, (N, m.nv)), p(qacc_warmstart, (N, m.nv)), p(time, (N,)), p(ctrl, (N, m.nu))]
-        check(lib().hs_state_io(self._h, 1, *[k[1] for k in keep]))
+        for h, lo, hi in self._groups:
+            check(lib().hs_state_io(h, 1, *[None if a is None else a[lo:hi].ctypes.data for a, _ in keep]))
 
     def set_debug(self, on=True):
         check(lib().hs_set_debug(self._h, int(bool(on))))
@@ -159,13 +225,15 @@ class HsBatch:
         return out
 
     def synchronize(self):
-        check(lib().hs_synchronize(self._h))
+        for h, _, _ in self._groups:
+            check(lib().hs_synchronize(h))
 
     def close(self):
-        h = self.__dict__.get("_h")
-        if h:
-            lib().hs_batch_destroy(h)
-            self._h = None
+        for h, _, _ in self.__dict__.get("_groups", []):
+            if h:
+                lib().hs_batch_destroy(h)
+        self._groups = []
+        self._h = None
 
     def __del__(self):
         try:

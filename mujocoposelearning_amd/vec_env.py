@@ -42,14 +42,17 @@ except ImportError:
 
 
 class HumanoidVecEnv(_Base):
-    def __init__(self, env_config, n_envs=8, device=0, precision="fp32", seed=0, model=None, max_newton=100):
+    def __init__(self, env_config, n_envs=8, device=0, precision="fp32", seed=0, model=None, max_newton=None,
+                 groups="auto"):
         if callable(env_config):            # SB3 style list of env_fns is not meaningful on device
             raise TypeError("pass the env_config dict (train_sb3.py:183-200), not env factories")
         cfg = env_config if isinstance(env_config, dict) else {"model_path": env_config}
         self.env_config = dict(cfg)
         self.model = model if model is not None else HsModel(cfg["model_path"])
+        if groups == "auto":      # one launch per step (stream groups only pay off when run free, see HsBatch)
+            groups = 1
         self.batch = HsBatch(self.model, n_envs, device=device, precision=precision, seed=seed,
-                             full_state=bool(cfg.get("full_state_obs", False)))
+                             full_state=bool(cfg.get("full_state_obs", False)), groups=groups)
         self.duration = float(cfg.get("duration", 15))
         self.frame_skip = int(cfg.get("frame_skip", 5))
         self.reward_config = cfg.get("reward_config", {"type": "default"})

@@ -94,6 +94,28 @@ def streams(n=4096, steps=100):
               f"{n * steps / dt:,.0f} env-steps/s")
 
 
+def groups_api(n=4096, steps=100):
+    """HsBatch(groups=G).step(join=False) vs separate batches stepped inside torch.cuda.stream()."""
+    model = HsModel(XML)
+    g = torch.Generator(device="cuda").manual_seed(0)
+    tape = torch.rand(steps + 5, n, model.nu, device="cuda", generator=g) * 2 - 1
+    for G in (1, 2, 4):
+        b = HsBatch(model, n, precision="fp32", seed=1, groups=G)
+        b.configure(frame_skip=3, duration=10.0, reward_id=0)
+        b.reset()
+        for k in range(5):
+            b.step(tape[k], join=False)
+        b.join()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for k in range(steps):
+            b.step(tape[5 + k], join=False)
+        b.join()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t
+        print(f"HsBatch(groups={G}) join=False: {dt / steps * 1e3:.3f} ms/step -> {n * steps / dt:,.0f} env-steps/s")
+
+
 def tail(n=4096, steps=300, prec="fp32"):
     """Distribution of per-env Newton iterations / contacts over an episode, and the launch-time
     sensitivity to the Newton iteration cap (the launch ends with its slowest wave)."""
@@ -131,6 +153,7 @@ def tail(n=4096, steps=300, prec="fp32"):
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "streams":
         streams()
+        groups_api()
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "tail":
         tail()

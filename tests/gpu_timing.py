@@ -57,5 +57,37 @@ def main(n=4096, steps=20, prec="fp32"):
                   f"max {life[sel].max():,.0f}")
 
 
+def predict(n=4096, steps=60, prec="fp32"):
+    """Is per-env Newton work predictable from the previous env step?  (timing build: dbg[11100+env]
+    = Newton iterations of env summed over the launch's substeps)"""
+    model = HsModel(os.path.join(ROOT, "tests", "golden", "humanoid.xml"))
+    b = HsBatch(model, n, precision=prec, seed=1)
+    b.configure(frame_skip=3, duration=10.0, reward_id=0)
+    b.reset()
+    b.set_debug(True)
+    g = torch.Generator(device="cuda").manual_seed(0)
+    hist = []
+    for k in range(steps):
+        b.step(torch.rand(n, 21, device="cuda", generator=g) * 2 - 1)
+        hist.append(b.get_debug()[11100:11100 + n].copy())
+    h = np.array(hist[10:])
+    c1 = np.mean([np.corrcoef(h[i], h[i + 1])[0, 1] for i in range(len(h) - 1)])
+    c5 = np.mean([np.corrcoef(h[i], h[i + 5])[0, 1] for i in range(len(h) - 5)])
+    # wave cost model: max over the env pair; compare random pairing vs pairing sorted by the
+    # previous step's count (what a predictor-driven permutation would achieve)
+    rnd, srt = [], []
+    for i in range(len(h) - 1):
+        cur, prev = h[i + 1], h[i]
+        rnd.append(np.maximum(cur[0::2], cur[1::2]).sum())
+        o = np.argsort(prev)
+        srt.append(np.maximum(cur[o][0::2], cur[o][1::2]).sum())
+    print(f"[{prec}] N={n}: corr(iters_t, iters_t+1) {c1:.2f}, corr(t, t+5) {c5:.2f}; "
+          f"sum over waves of max(pair): random pairing {np.mean(rnd):,.0f} vs sorted by previous step "
+          f"{np.mean(srt):,.0f} ({np.mean(srt) / np.mean(rnd):.3f}); ideal {h[1:].sum(1).mean() / 2:,.0f}")
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[2] == "predict":
+        predict(prec=sys.argv[1])
+        sys.exit(0)
     main(prec=sys.argv[1] if len(sys.argv) > 1 else "fp32")

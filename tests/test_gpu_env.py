@@ -231,3 +231,50 @@ def test_generate_trajectory_xml_with_saved_policy(tmp_path):
     assert [k.get("time") for k in keys[5:]] == [f"{s * 0.005:.3f}" for s in range(0, 40, 5)]
     q = np.array(keys[4].get("qpos").split(), float)
     assert abs(q[2] - 1.282) < 0.002 and np.isfinite(q).all()
+
+
+def test_stream_groups_are_bitwise_identical_to_one_batch(model):
+    """HsBatch(groups=4) (4 native sub-batches on 4 HIP streams over slices of the same tensors)
+    steps every env exactly like one batch."""
+    import torch
+    from mujocoposelearning_amd.batch import HsBatch
+    n = 1000                                   # ragged: 250 per group
+    rng = np.random.default_rng(0)
+    q0 = np.tile(model.qpos0, (n, 1))
+    q0[:, 2] = 1.282
+    q0[:, 3:7] = [1, 0, 0, 0]
+    q0 += rng.uniform(-0.01, 0.01, q0.shape) * np.r_[1, 1, 0.1, 0, 0, 0, 0, np.ones(21)]
+    v0 = rng.uniform(-0.01, 0.01, (n, 27))
+    tape = torch.tensor(rng.uniform(-1, 1, (30, n, 21)), dtype=torch.float32, device="cuda")
+    outs = []
+    for G in (1, 4):
+        b = HsBatch(model, n, precision="fp32", groups=G)
+        assert len(b._groups) == G
+        b.configure(frame_skip=3, duration=10.0, reward_id=0)
+        b.set_state(qpos=q0, qvel=v0, time=0.005, qacc_warmstart=0.0)
+        for k in range(30):
+            obs, rew, term, trunc = b.step(tape[k], join=(k % 2 == 0))   # free-running half the time
+        b.join()
+        torch.cuda.synchronize()
+        outs.append((obs.clone(), rew.clone(), b.get_state()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    for k in ("qpos", "qvel", "qacc_warmstart", "time"):
+        assert np.array_equal(outs[0][2][k], outs[1][2][k]), k
+
+
+def test_grouped_vecenv_episode_semantics():
+    """2048 envs in 4 stream groups: every env terminates at step 667 and auto-resets."""
+    import torch
+    from mujocoposelearning_amd.vec_env import HumanoidVecEnv
+    env = HumanoidVecEnv(CFG, n_envs=2048, groups=4)
+    assert len(env.batch._groups) == 4
+    env.reset_tensors()
+    a = torch.zeros(2048, 21, device=env.device)
+    for k in range(667):
+        obs, rew, term, trunc = env.step_tensors(a)
+        if k < 666:
+            assert not term.any()
+    torch.cuda.synchronize()
+    assert term.all() and not trunc.any()
+    assert (env.batch.step_count == 0).all() and torch.isfinite(obs).all()
+    assert (env.batch.terminal_obs[:, 0] != obs[:, 0]).any()
