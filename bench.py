@@ -104,6 +104,7 @@ def main():
     ap.add_argument("--no-gae", action="store_true")
     ap.add_argument("--train-iters", type=int, default=2, help="PPO iterations of the train mode (0: skip)")
     ap.add_argument("--groups", default="1", help="stream groups for the headline run (1 = one launch per step)")
+    ap.add_argument("--no-configs", action="store_true", help="skip the configs[3]/[4] legs")
     ap.add_argument("--free-groups", type=int, default=4, help="extra sim-only leg: this many free-running stream "
                                                                 "groups (0: skip)")
     ap.add_argument("--dist-backend", default=os.environ.get("HSIM_BENCH_BACKEND", "nccl"),
@@ -225,6 +226,38 @@ def main():
                             "join=False): one group's Newton tail overlaps the others' launches")
         envg.close()
 
+    # BASELINE.json configs[3] (kneeling reward, 4096 envs) and configs[4] (full-state obs, 8192
+    # envs over 8 GPUs = 1024 per GPU): same sim-only protocol, one launch per step
+    config_legs = None
+    if not args.no_configs:
+        def leg(cfg_x, n_x, label):
+            e = HumanoidVecEnv(cfg_x, n_envs=n_x, device=dev_index, precision=args.precision, seed=4000 + rank,
+                               model=model)
+            e.reset_tensors()
+            tp = tape[:, :n_x] if n_x <= n else (torch.rand(tape_len, n_x, model.nu, device=dev) * 2 - 1)
+            for k in range(args.warmup):
+                e.step_tensors(tp[k % tape_len])
+            barrier()
+            tl = time.perf_counter()
+            ks = min(args.steps, 50)
+            for k in range(ks):
+                e.step_tensors(tp[(args.warmup + k) % tape_len])
+            barrier()
+            tt = torch.tensor([time.perf_counter() - tl], dtype=torch.float64, device=red_dev)
+            if world > 1:
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            r = dict(value=n_x * ks * world / float(tt.item()), unit="env_steps/s", n_envs_per_gpu=n_x,
+                     obs_dim=e.obs_dim, workload=label)
+            e.close()
+            return r
+        config_legs = {
+            "configs[3]": leg({**cfg, "reward_config": {"type": "kneeling"}}, n,
+                              "kneeling (robust_kneeling_reward) device reward, humanoid.xml x 4096 envs per GPU"),
+            "configs[4]": leg({**cfg, "full_state_obs": True}, 1024,
+                              "full-state obs (+cfrc_ext[1:], 448 floats; subtree_linvel), 1024 envs per GPU "
+                              "(8192 over 8 GPUs)"),
+        }
+
     # roofline pass: the step kernel with all n envs in ONE launch per step (groups=1), HIP events on
     # the stream it is launched on -- the per-launch figure rocprofv3 reports for profiles/collect.sh
     if n_groups == 1:
@@ -335,6 +368,7 @@ def main():
             "rollout": rollout,
             "gae": gae_res,
             "sim_only_stream_groups": grouped,
+            "other_configs": config_legs,
             "train": train_res,
             "sim_stats": stats,
         }

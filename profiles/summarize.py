@@ -41,7 +41,7 @@ def main(tag="r01", n_envs=4096, precision="fp32", src=None):
                grid=int(row["Grid_Size"]), workgroup=int(row["Workgroup_Size"]))
     json.dump(out, open(os.path.join(ROOT, "profiles", "traffic_step_kernel.json"), "w"), indent=1)
     lines = [f"# rocprofv3 summary `{tag}` -- step kernel, {n_envs} envs, {precision}", "",
-             "Command: `bash profiles/collect.sh` (bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-rollout --no-gae --train-iters 0 --groups 1 --free-groups 0)", "",
+             "Command: `bash profiles/collect.sh` (bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-rollout --no-gae --train-iters 0 --groups 1 --free-groups 0 --no-configs)", "",
              "## Kernel stats (rocprofv3 --kernel-trace --stats)", "",
              "| kernel | calls | avg us | min us | max us | % |", "|---|---|---|---|---|---|"]
     for r in stats[:6]:
