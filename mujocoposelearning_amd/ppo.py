@@ -150,7 +150,9 @@ class PPO:
         f, dev = torch.float32, self.device
         self.buf = dict(obs=torch.zeros(T, N, D, dtype=f, device=dev), act=torch.zeros(T, N, A, dtype=f, device=dev),
                         rew=torch.zeros(T, N, dtype=f, device=dev), start=torch.zeros(T, N, dtype=f, device=dev),
-                        val=torch.zeros(T, N, dtype=f, device=dev), logp=torch.zeros(T, N, dtype=f, device=dev))
+                        val=torch.zeros(T, N, dtype=f, device=dev), logp=torch.zeros(T, N, dtype=f, device=dev),
+                        done=torch.zeros(T, N, dtype=torch.bool, device=dev),
+                        epret=torch.zeros(T, N, dtype=torch.float64, device=dev))
         self.obs = env.reset_tensors().float().clone()
         self.episode_start = torch.ones(N, dtype=f, device=dev)
         self.num_timesteps = 0
@@ -160,6 +162,9 @@ class PPO:
         self.logger = {}
 
     def collect_rollouts(self):
+        """SB3 PPO.collect_rollouts on device.  No host synchronisation inside the loop: the
+        timeout bootstrap r += gamma V(terminal_obs) is evaluated for every env and masked, and
+        finished-episode returns are recorded in device buffers and read back once at the end."""
         b, env, pol = self.buf, self.env, self.policy
         for t in range(self.n_steps):
             a, logp, v = pol.act(self.obs)
@@ -169,19 +174,18 @@ class PPO:
             b["logp"][t] = logp
             b["start"][t] = self.episode_start
             obs, rew, term, trunc = env.step_tensors(a.clamp(-1.0, 1.0))
-            r = rew.float()
-            done = (term | trunc).float()
-            if bool(trunc.any()):   # SB3 timeout bootstrap: r += gamma * V(terminal_obs)
-                tv = pol.value(env.terminal_obs.float())
-                r = r + self.gamma * tv * (trunc.float() * (1 - term.float()))
-            b["rew"][t] = r
+            term, trunc = term.bool(), trunc.bool()
+            boot = (trunc & ~term).float()          # TimeLimit.truncated: bootstrap from V(terminal obs)
+            tv = pol.value(env.terminal_obs.float())
+            b["rew"][t] = rew.float() + self.gamma * torch.where(boot > 0, tv, torch.zeros_like(tv))
+            done = term | trunc
             self.ep_acc += rew.double()
-            if bool(done.any()):
-                idx = done.bool()
-                self.ep_returns += self.ep_acc[idx].tolist()
-                self.ep_acc[idx] = 0
+            b["done"][t] = done
+            b["epret"][t] = self.ep_acc
+            self.ep_acc.masked_fill_(done, 0.0)
             self.obs = obs.float().clone()
-            self.episode_start = done
+            self.episode_start = done.float()
+        self.ep_returns += b["epret"][b["done"]].tolist()      # one device -> host transfer per rollout
         self.num_timesteps += self.n_steps * env.num_envs * self.world_size
         last_v = pol.value(self.obs)
         return gae(b["rew"], b["val"], b["start"], last_v, self.episode_start, self.gamma, self.gae_lambda)
