@@ -1059,8 +1059,7 @@ struct Stepper {
   __device__ __forceinline__ void solve(T xws, int maxit, T tol, const T (&D)[RPL], const T (&ar)[RPL],
                                         const int (&rd)[RPL], const T (&rc)[RPL]) {
     phase_begin();
-    const int nv = m->nv;
-    const int nefc = s.nefc, nlim = s.nlim, ncon = s.ncon;
+    const int nefc = s.nefc, ncon = s.ncon;
     T x = sl < NV ? xws : T(0);
     bool vr[RPL];
 #pragma unroll
@@ -1538,7 +1537,9 @@ __device__ __forceinline__ void commit(MPtr<T> m, const EnvBuffers<T>& b, const 
 
 // ------------------------------------------------------------------ the kernel
 template <typename T, int NV>
-__global__ __launch_bounds__(64, 2) void step_kernel(MPtr<T> m, EnvBuffers<T> b,
+// 2 waves/SIMD (the VGPR budget of 256) for the fp32 engine; the fp64 parity engine needs more
+// registers and runs at 1
+__global__ __launch_bounds__(64, sizeof(T) == 4 ? 2 : 1) void step_kernel(MPtr<T> m, EnvBuffers<T> b,
                                                   const float* __restrict__ actions,
                                                   const uint8_t* __restrict__ reset_mask,
                                                   const T* __restrict__ nz_q, const T* __restrict__ nz_v,
