@@ -246,3 +246,21 @@ def test_option_override_model_fp64_trajectory(tmp_path):
     assert np.abs(st["qpos"][0] - o.qpos).max() < 1e-8
     assert np.abs(st["qvel"][0] - o.qvel).max() < 1e-6
     assert abs(st["time"][0] - 0.2) < 1e-12
+
+
+@pytest.mark.parametrize("tape", ["zeros", "uniform"])
+def test_fp64_1000_substeps_within_chaos_envelope(tape):
+    """SURVEY 8d parity run: 1000 substeps.  The fp64 GPU engine may differ from the oracle only as
+    much as the oracle differs from itself under a 1e-15 relative perturbation (the chaos
+    envelope of this contact-rich system), with an absolute floor of 1e-9.  Full table:
+    profiles/parity_report.md (tests/parity_report.py)."""
+    import parity_report as pr
+    from mujocoposelearning_amd.model import HsModel
+    from oracle.oracle import Oracle
+    q, v, rng = pr.initial(Oracle(XML), 0)
+    tp = (np.zeros((pr.NSUB, 21)) if tape == "zeros" else rng.uniform(-1, 1, (pr.NSUB, 21))).astype(np.float32)
+    ref, env = pr.run_oracle(q, v, tp), pr.run_oracle(q, v, tp, perturb=1e-15)
+    gpu = pr.run_gpu(HsModel(XML), "fp64", q, v, tp)
+    for k in range(len(ref)):
+        bound = max(1e-9, 20 * np.abs(env[k][0] - ref[k][0]).max())
+        assert np.abs(gpu[k][0] - ref[k][0]).max() <= bound, (k, bound)
