@@ -234,24 +234,48 @@ template <>
 __device__ __forceinline__ float rsqrt_t<float>(float x) { return __builtin_amdgcn_rsqf(x); }
 
 template <int NV, typename T>
-__device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T* col) {
-  static_for<0, NV>([&](auto kc) {
-    constexpr int k = decltype(kc)::value;
+__device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb)[2]) {
+  // two columns per LDS round trip: every lane publishes (a_ik, a_i,k+1) as one ds_write and reads
+  // the 2x2 pivot block and (a_jk, a_j,k+1) back as broadcasts.  With L_P the pivot block's
+  // Cholesky factor (1/L_kk = r1, L_k+1,k = l10, 1/L_k+1,k+1 = r2), row i gets
+  //   z = L_P^-1 (a_ik, a_i,k+1)   (its L entries)    f = L_P^-T z   (its Schur coefficients)
+  //   A_ij -= f0 a_jk + f1 a_j,k+1   (j >= k+2)
+  // and the pivot rows' own z are their L entries (L_kk, and l10, L_k+1,k+1).
+  static_for<0, NV / 2>([&](auto bc) {
+    constexpr int k = 2 * decltype(bc)::value;
     const int sl_k = opaque_v(sl);     // fresh compare per step (no 64-bit mask kept live)
-    col[sl_k] = A[k];
-    T akk = col[k];
-    akk = akk > T(1e-30) ? akk : T(1e-30);
-    T r = rsqrt_t(akk);                // 1 / L_kk
-    T lik = (sl_k == k) ? akk * r : A[k] * r;
-    dinv = (sl_k == k) ? r : dinv;
-    T f = A[k] * (r * r);              // a_ik / a_kk
-    A[k] = lik;
-    static_for<k + 1, NV>([&](auto jc) {
+    cb[sl_k][0] = A[k];
+    cb[sl_k][1] = A[k + 1];
+    T p = cb[k][0], q = cb[k + 1][0], t = cb[k + 1][1];
+    p = p > T(1e-30) ? p : T(1e-30);
+    T r1 = rsqrt_t(p);
+    T l10 = q * r1;
+    T s11 = t - l10 * l10;
+    s11 = s11 > T(1e-30) ? s11 : T(1e-30);
+    T r2 = rsqrt_t(s11);
+    T z0 = A[k] * r1;
+    T z1 = (sl_k == k + 1) ? s11 * r2 : (A[k + 1] - l10 * z0) * r2;
+    T f1 = z1 * r2;
+    T f0 = (z0 - l10 * f1) * r1;
+    A[k] = (sl_k == k) ? p * r1 : z0;
+    A[k + 1] = z1;
+    dinv = (sl_k == k) ? r1 : ((sl_k == k + 1) ? r2 : dinv);
+    static_for<k + 2, NV>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
-      A[j] = fma(-f, col[j], A[j]);
+      A[j] = fma(-f0, cb[j][0], fma(-f1, cb[j][1], A[j]));
     });
     SCHED_FENCE();
   });
+  if constexpr (NV % 2 == 1) {         // trailing single column
+    constexpr int k = NV - 1;
+    const int sl_k = opaque_v(sl);
+    cb[sl_k][0] = A[k];
+    T akk = cb[k][0];
+    akk = akk > T(1e-30) ? akk : T(1e-30);
+    T r = rsqrt_t(akk);
+    A[k] = (sl_k == k) ? akk * r : A[k] * r;
+    dinv = (sl_k == k) ? r : dinv;
+  }
 }
 // solve (L L') x = b; sub-lane i holds b_i; returns x_i.  Sub-lane k finishes y_k / x_k itself
 // (times its own 1/L_kk) and one broadcast hands it to the half.
@@ -325,7 +349,8 @@ struct Scratch {
     struct { T crb[MAXBODY][10]; T buf[MAXDOF][6]; } c;          // composite rigid body
     struct { T cdofdot[MAXDOF][6]; T cfrc[MAXBODY][6]; T csub[MAXBODY][6]; } r;   // RNE
     struct { T bvel[MAXBODY][6];                                  // J x mapping (rows, Newton)
-             T cfrc[MAXBODY][6], linv[MAXBODY][3], mv[MAXBODY][3]; } n;   // full_state (after solve)
+             T cfrc[MAXBODY][6], linv[MAXBODY][3], mv[MAXBODY][3];    // full_state (after solve)
+             alignas(16) T cb[MAXDOF][2]; } n;                       // Cholesky column pairs
   } u;
 };
 
@@ -1171,7 +1196,7 @@ struct Stepper {
       }
       HS_STAMP(clk, 9);
       T hdinv = 0;
-      chol_rows<NV>(H, hdinv, sl, s.vx);
+      chol_rows<NV>(H, hdinv, sl, s.u.n.cb);
       T sdir = -chol_solve<NV>(H, hdinv, g, sl);
       if (sl >= NV) sdir = 0;
       HS_STAMP(clk, 10);
@@ -1302,7 +1327,7 @@ struct Stepper {
 #pragma unroll
     for (int j = 0; j < NV; j++) He[j] = Mr[j] + ((j == sl) ? h * damp : T(0));
     T edinv = 0;
-    chol_rows<NV>(He, edinv, sl, s.vx);
+    chol_rows<NV>(He, edinv, sl, s.u.n.cb);
     T a = chol_solve<NV>(He, edinv, fsmooth + fcon, sl);
     if (sl < NV) s.qvel[sl] += h * a;
     WSYNC();
