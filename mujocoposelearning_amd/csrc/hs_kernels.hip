@@ -40,9 +40,10 @@ static_assert(MAXDOF == HL, "one dof per sub-lane (lim_row slots, dof masks)");
 // unrolled loops (which otherwise inflates VGPR pressure far past the occupancy target)
 #define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 
-// single-wave workgroup: LDS ops of a wave execute in order; this fence only stops the compiler
-// from reordering LDS accesses across phase boundaries (no s_barrier needed for one wave).
-#define WSYNC() __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup")
+// single-wave workgroup: LDS ops of a wave execute in order, so a compiler-only barrier suffices to
+// keep LDS accesses from moving across phase boundaries (no s_barrier, and no s_waitcnt that a
+// workgroup-scope fence would add).
+#define WSYNC() asm volatile("" ::: "memory")
 
 // ------------------------------------------------------------------ cross-lane helpers
 // compile-time loop: f(std::integral_constant<int, i>) for i in [B, E)
