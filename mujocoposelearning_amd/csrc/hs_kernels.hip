@@ -468,18 +468,25 @@ __device__ __forceinline__ void store_contact(MPtr<T> m, Scratch<T>& s, int slot
   s.con_mu[slot] = m->pair_mu[p];
 }
 
-// impedance (mj_makeImpedance getimpedance), MuJoCo clamps d0/dmax to [1e-4, 0.9999]
+// impedance (mj_makeImpedance getimpedance), MuJoCo clamps d0/dmax to [1e-4, 0.9999].  The sigmoid
+// y = x^p / mid^(p-1) (x <= mid) or 1 - (1-x)^p / (1-mid)^(p-1) takes its constant denominators from
+// the model (si[5..7], fill_solimp) and one pow, skipped for the default power 2.
 template <typename T>
 __device__ __forceinline__ T impedance(CPtr<T> si, T pos, T margin) {
   T s0 = fmin(T(0.9999), fmax(T(0.0001), si[0])), s1 = fmin(T(0.9999), fmax(T(0.0001), si[1]));
   if (s0 == s1 || si[2] <= T(1e-15)) return T(0.5) * (s0 + s1);
-  T x = (pos - margin) / si[2];
+  T x = (pos - margin) * si[5];
   if (x < 0) x = -x;
   if (x >= 1 || x <= 0) return x >= 1 ? s1 : s0;
-  T y;
-  if (si[4] == 1) y = x;
-  else if (x <= si[3]) y = pow(x, si[4]) / pow(si[3], si[4] - 1);
-  else y = 1 - pow(1 - x, si[4]) / pow(1 - si[3], si[4] - 1);
+  const T p = si[4];
+  T y = x;
+  if (p != T(1)) {
+    const bool lo = x <= si[3];
+    const T base = lo ? x : 1 - x;
+    T pw = base * base;
+    if (p != T(2)) pw = pow(base, p);
+    y = lo ? pw * si[6] : 1 - pw * si[7];
+  }
   return s0 + y * (s1 - s0);
 }
 

@@ -25,6 +25,9 @@ constexpr int MAXCON = 32;    // contacts per env (one half-wave lane each; over
 constexpr int MAXEFC = 128;   // constraint rows per env (4 per half-wave lane)
 constexpr int MAXLEVEL = 16;
 constexpr int MAXJPB = 3;     // hinge joints per body (kinematics keeps their rotations in registers)
+// solimp on the device: MuJoCo's (d0, dwidth, width, midpoint, power) followed by derived constants
+// (1/width, 1/mid^(power-1), 1/(1-mid)^(power-1)) so the impedance sigmoid takes one pow at most
+constexpr int SOLIMP = 8;
 
 enum GeomType { GEOM_PLANE = 0, GEOM_SPHERE = 2, GEOM_CAPSULE = 3 };
 enum JointType { JNT_FREE = 0, JNT_HINGE = 3 };
@@ -47,7 +50,7 @@ struct DevModel {
   T body_mass[MAXBODY], body_invweight_tran[MAXBODY];
   int jnt_type[MAXJNT], jnt_qposadr[MAXJNT], jnt_dofadr[MAXJNT], jnt_bodyid[MAXJNT], jnt_limited[MAXJNT];
   T jnt_pos[MAXJNT][3], jnt_axis[MAXJNT][3], jnt_range[MAXJNT][2];
-  T jnt_solref[MAXJNT][2], jnt_solimp[MAXJNT][5], jnt_margin[MAXJNT];
+  T jnt_solref[MAXJNT][2], jnt_solimp[MAXJNT][SOLIMP], jnt_margin[MAXJNT];
   int dof_bodyid[MAXDOF], dof_jntid[MAXDOF], dof_qposadr[MAXDOF];   // qposadr: hinge dofs, else -1
   uint32_t dof_ancmask[MAXDOF];       // dof ancestors incl. self (dof_parentid chain)
   uint32_t dof_dotmask[MAXDOF];       // dofs whose motion precedes this dof in mj_comVel
@@ -61,13 +64,13 @@ struct DevModel {
   // static candidate pairs, canonical (MuJoCo) processing order; g1 has the lower geom type
   int pair_g1[MAXPAIR], pair_g2[MAXPAIR], pair_b1[MAXPAIR], pair_b2[MAXPAIR];
   int pair_fn[MAXPAIR], pair_dim[MAXPAIR];
-  T pair_mu[MAXPAIR], pair_margin[MAXPAIR], pair_solref[MAXPAIR][2], pair_solimp[MAXPAIR][5];
+  T pair_mu[MAXPAIR], pair_margin[MAXPAIR], pair_solref[MAXPAIR][2], pair_solimp[MAXPAIR][SOLIMP];
   // what the narrow phase of one pair needs, packed into two 16-byte records per pair (one
   // dwordx4 load each, no dependent geom-table lookup): {g1, g2, fn, dim}, {r1, h1, r2, h2}
   alignas(16) int pair_info[MAXPAIR][4];
   alignas(16) T pair_size[MAXPAIR][4];
   int ten_nwrap[MAXTEN], ten_wrapdof[MAXTEN][MAXWRAP], ten_wrapqadr[MAXTEN][MAXWRAP], ten_limited[MAXTEN];
-  T ten_wrapcoef[MAXTEN][MAXWRAP], ten_range[MAXTEN][2], ten_solref[MAXTEN][2], ten_solimp[MAXTEN][5];
+  T ten_wrapcoef[MAXTEN][MAXWRAP], ten_range[MAXTEN][2], ten_solref[MAXTEN][2], ten_solimp[MAXTEN][SOLIMP];
   T ten_margin[MAXTEN], ten_invweight0[MAXTEN];
   T qpos0[MAXQ];
 };

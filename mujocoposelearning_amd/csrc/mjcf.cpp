@@ -903,6 +903,16 @@ int model_field(const HostModel& m, const std::string& name, double* out, int n)
   return cnt;
 }
 
+// device solimp: the 5 MuJoCo values + 1/width, 1/mid^(p-1), 1/(1-mid)^(p-1) (getimpedance's
+// constant denominators, mj_makeImpedance)
+template <typename T>
+void fill_solimp(T (&dst)[SOLIMP], const double* si) {
+  for (int k = 0; k < 5; k++) dst[k] = (T)si[k];
+  dst[5] = (T)(si[2] > 0 ? 1.0 / si[2] : 0.0);
+  dst[6] = (T)(1.0 / std::pow(si[3], si[4] - 1));
+  dst[7] = (T)(1.0 / std::pow(1 - si[3], si[4] - 1));
+}
+
 template <typename T>
 bool build_dev_model(const HostModel& m, DevModel<T>& d, std::string& err) {
   std::memset(&d, 0, sizeof d);
@@ -974,7 +984,7 @@ bool build_dev_model(const HostModel& m, DevModel<T>& d, std::string& err) {
     d.jnt_limited[j] = m.jnt_limited[j] && m.jnt_type[j] == JNT_HINGE;
     for (int k = 0; k < 3; k++) { d.jnt_pos[j][k] = (T)m.jnt_pos[3 * j + k]; d.jnt_axis[j][k] = (T)m.jnt_axis[3 * j + k]; }
     for (int k = 0; k < 2; k++) { d.jnt_range[j][k] = (T)m.jnt_range[2 * j + k]; d.jnt_solref[j][k] = (T)m.jnt_solref[2 * j + k]; }
-    for (int k = 0; k < 5; k++) d.jnt_solimp[j][k] = (T)m.jnt_solimp[5 * j + k];
+    fill_solimp(d.jnt_solimp[j], &m.jnt_solimp[5 * j]);
     d.jnt_margin[j] = (T)m.jnt_margin[j];
   }
   for (int i = 0; i < m.nv; i++) {
@@ -1066,7 +1076,7 @@ bool build_dev_model(const HostModel& m, DevModel<T>& d, std::string& err) {
     d.pair_margin[p] = (T)(std::max(m.geom_margin[g1], m.geom_margin[g2]) - std::max(m.geom_gap[g1], m.geom_gap[g2]));
     if (std::max(m.geom_margin[g1], m.geom_margin[g2]) != 0) { err = "nonzero geom margin not supported"; return false; }
     for (int k = 0; k < 2; k++) d.pair_solref[p][k] = (T)sr[k];
-    for (int k = 0; k < 5; k++) d.pair_solimp[p][k] = (T)si[k];
+    fill_solimp(d.pair_solimp[p], si);
   }
   for (int t = 0; t < m.ntendon; t++) {
     if (m.tendon_num[t] > MAXWRAP) { err = "tendon has too many joints"; return false; }
@@ -1079,7 +1089,7 @@ bool build_dev_model(const HostModel& m, DevModel<T>& d, std::string& err) {
     }
     d.ten_limited[t] = m.tendon_limited[t];
     for (int k = 0; k < 2; k++) { d.ten_range[t][k] = (T)m.tendon_range[2 * t + k]; d.ten_solref[t][k] = (T)m.tendon_solref[2 * t + k]; }
-    for (int k = 0; k < 5; k++) d.ten_solimp[t][k] = (T)m.tendon_solimp[5 * t + k];
+    fill_solimp(d.ten_solimp[t], &m.tendon_solimp[5 * t]);
     d.ten_margin[t] = (T)m.tendon_margin[t];
     d.ten_invweight0[t] = (T)m.tendon_invweight0[t];
   }
