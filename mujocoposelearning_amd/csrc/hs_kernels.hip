@@ -54,9 +54,11 @@ __device__ __forceinline__ void static_for(F&& f) {
     static_for<B + 1, E>(f);
   }
 }
+// bound_ctrl set: every pattern used here reads in-bounds lanes only, and with it the DPP combiner
+// folds the move into its consumer (hsum's adds become single v_add_f32_dpp instructions)
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp32(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
 }
 // v_permlane16_swap(v, v): .first = rows {0,0,2,2}, .second = rows {1,1,3,3} (row = 16 lanes),
 // i.e. every lane of a 32-lane half sees the half's low row in .first and its high row in .second.
@@ -614,8 +616,9 @@ __device__ __forceinline__ T jtf_lane(MPtr<T> m, const Scratch<T>& s, int sl, co
 // Built only with -DHS_TIMING (libhsim_timing.so): s_memtime stamps accumulated per phase,
 // summed over waves into dbg[8000 + slot].  The product build compiles them out.
 #ifdef HS_TIMING
+constexpr int NSLOT = 18;
 struct PhaseClock {
-  uint64_t acc[16] = {0};
+  uint64_t acc[NSLOT] = {0};
   uint64_t prev = 0, t0 = 0;
   __device__ __forceinline__ void start() { prev = t0 = __builtin_amdgcn_s_memtime(); }
   __device__ __forceinline__ void stamp(int slot) {
@@ -1205,6 +1208,7 @@ struct Stepper {
       HS_STAMP(clk, 9);
       T hdinv = 0;
       chol_rows<NV>(H, hdinv, sl, s.u.n.cb);
+      HS_STAMP(clk, 15);
       T sdir = -chol_solve<NV>(H, hdinv, g, sl);
       if (sl >= NV) sdir = 0;
       HS_STAMP(clk, 10);
@@ -1217,6 +1221,7 @@ struct Stepper {
       map_vx<NV>(m, s, sl, nb);
 #pragma unroll
       for (int q = 0; q < RPL; q++) Js[q] = vr[q] ? row_Jx(m, s, rd[q], rc[q]) : T(0);
+      HS_STAMP(clk, 16);
       // alpha = 1 is exact when no row changes state on [0, 1] (jar is linear in alpha)
       bool same1 = true;
 #pragma unroll
@@ -1337,6 +1342,7 @@ struct Stepper {
     T edinv = 0;
     chol_rows<NV>(He, edinv, sl, s.u.n.cb);
     T a = chol_solve<NV>(He, edinv, fsmooth + fcon, sl);
+    HS_STAMP(clk, 17);
     if (sl < NV) s.qvel[sl] += h * a;
     WSYNC();
     if (sl < m->njnt) {
@@ -1692,8 +1698,8 @@ __global__ __launch_bounds__(64, sizeof(T) == 4 ? 2 : 1) void step_kernel(MPtr<T
 #ifdef HS_TIMING
   HS_STAMP(st.clk, 14);
   if (sl == 0 && b.dbg) {
-    for (int k = 0; k < 15; k++) atomicAdd(&b.dbg[8000 + k], (T)st.clk.acc[k]);
-    atomicAdd(&b.dbg[8015], (T)st.niter);
+    for (int k = 0; k < NSLOT; k++) atomicAdd(&b.dbg[8000 + k], (T)st.clk.acc[k]);
+    atomicAdd(&b.dbg[8020], (T)st.niter);
   }
   // per-wave lifetime of this launch (shader cycles) -> dbg[9000 + wave] (waves < 7000)
   if (lane == 0 && b.dbg && blockIdx.x < 2048) b.dbg[9000 + blockIdx.x] = (T)(st.clk.prev - st.clk.t0);
