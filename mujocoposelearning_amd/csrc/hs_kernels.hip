@@ -337,6 +337,7 @@ struct Scratch {
   T con_F[MAXCON][3];
   int con_pair[MAXCON];
   int con_adr[MAXCON];
+  uint32_t con_bb[MAXCON];    // b1 | b2 << 8 | condim << 16 of the contact's pair (no model lookups per use)
   uint32_t con_m1[MAXCON];    // dof chain masks of the contact's bodies (m1 = 0: world)
   uint32_t con_m2[MAXCON];
   T con_mu[MAXCON];
@@ -464,9 +465,10 @@ __device__ __forceinline__ void store_contact(MPtr<T> m, Scratch<T>& s, int slot
   for (int k = 0; k < 3; k++) { s.con_pos[slot][k] = c.pos[k]; s.con_n[slot][k] = c.n[k]; s.con_t1[slot][k] = c.t1[k]; }
   s.con_dist[slot] = c.dist;
   s.con_pair[slot] = p;
-  int b1 = m->pair_b1[p];
+  const int b1 = m->pair_b1[p], b2 = m->pair_b2[p];
+  s.con_bb[slot] = (uint32_t)b1 | (uint32_t)b2 << 8 | (uint32_t)m->pair_dim[p] << 16;
   s.con_m1[slot] = b1 ? m->body_chainmask[b1] : 0u;
-  s.con_m2[slot] = m->body_chainmask[m->pair_b2[p]];
+  s.con_m2[slot] = m->body_chainmask[b2];
   s.con_mu[slot] = m->pair_mu[p];
 }
 
@@ -494,11 +496,15 @@ __device__ __forceinline__ T impedance(CPtr<T> si, T pos, T margin) {
 
 // ------------------------------------------------------------------ J x for all rows
 // s.vx (generalized vector) -> body spatial velocities -> contact frame velocities
+// ch: this body lane's dof chain mask (body_chainmask, 0 for the world), loaded by the caller
+template <typename T>
+__device__ __forceinline__ uint32_t chain_mask(MPtr<T> m, int sl, int nb) {
+  return (sl > 0 && sl < nb) ? m->body_chainmask[sl] : 0u;
+}
 template <int NV, typename T>
-__device__ __forceinline__ void map_vx(MPtr<T> m, Scratch<T>& s, int sl, int nb) {
+__device__ __forceinline__ void map_vx(Scratch<T>& s, int sl, int nb, uint32_t ch) {
   if (sl < nb) {   // body spatial velocity = sum over the body's dof chain of cdof_j x_j
     T v[6] = {0, 0, 0, 0, 0, 0};
-    const uint32_t ch = sl > 0 ? m->body_chainmask[sl] : 0u;
     static_for<0, NV>([&](auto jc) {      // unrolled + predicated: no per-dof branch, loads pipelined
       constexpr int j = decltype(jc)::value;
       T xj = bit(ch, j) ? s.vx[j] : T(0);
@@ -509,8 +515,8 @@ __device__ __forceinline__ void map_vx(MPtr<T> m, Scratch<T>& s, int sl, int nb)
   }
   WSYNC();
   if (sl < s.ncon) {
-    int p = s.con_pair[sl];
-    int b1 = m->pair_b1[p], b2 = m->pair_b2[p];
+    const uint32_t bb = s.con_bb[sl];
+    const int b1 = bb & 0xff, b2 = (bb >> 8) & 0xff;
     T r[3] = {s.con_pos[sl][0] - s.com[0], s.con_pos[sl][1] - s.com[1], s.con_pos[sl][2] - s.com[2]};
     T w[3], v1[3], v2[3];
     cross3(s.u.n.bvel[b2], r, w);
@@ -561,7 +567,7 @@ template <typename T>
 __device__ __forceinline__ void contact_aggregates(MPtr<T> m, Scratch<T>& s, int sl) {
   if (sl < s.ncon) {
     int adr = s.con_adr[sl];
-    int nr = m->pair_dim[s.con_pair[sl]] == 1 ? 1 : 4;
+    int nr = (s.con_bb[sl] >> 16) == 1 ? 1 : 4;
     T U[6] = {0, 0, 0, 0, 0, 0}, F[3] = {0, 0, 0};
     for (int q = 0; q < nr; q++) {
       int r = adr + q;
@@ -616,7 +622,7 @@ __device__ __forceinline__ T jtf_lane(MPtr<T> m, const Scratch<T>& s, int sl, co
 // Built only with -DHS_TIMING (libhsim_timing.so): s_memtime stamps accumulated per phase,
 // summed over waves into dbg[8000 + slot].  The product build compiles them out.
 #ifdef HS_TIMING
-constexpr int NSLOT = 18;
+constexpr int NSLOT = 20;
 struct PhaseClock {
   uint64_t acc[NSLOT] = {0};
   uint64_t prev = 0, t0 = 0;
@@ -995,7 +1001,7 @@ struct Stepper {
     int nlim = nrow;
     {   // contacts: 1 row (condim 1) or 4 pyramid rows (condim 3)
       bool isc = sl < ncon;
-      bool pyr = isc && m->pair_dim[s.con_pair[sl]] == 3;
+      bool pyr = isc && (s.con_bb[sl] >> 16) == 3;
       uint32_t mc = hballot(isc, up), mp = hballot(pyr, up);
       int pre = nrow + below(mc, sl) + 3 * below(mp, sl);
       int tot = __popc(mc) + 3 * __popc(mp);
@@ -1003,7 +1009,7 @@ struct Stepper {
         overflow = 1;
         int fit = 0, nr = nrow;
         for (int c = 0; c < ncon; c++) {
-          int need = (m->pair_dim[s.con_pair[c]] == 3) ? 4 : 1;
+          int need = (s.con_bb[c] >> 16) == 3 ? 4 : 1;
           if (nr + need > MAXEFC) break;
           nr += need;
           fit++;
@@ -1022,7 +1028,7 @@ struct Stepper {
     if (sl == 0) { s.ncon = ncon; s.nefc = nrow; s.nlim = nlim; s.njl = njl; }
     if (sl < NV) s.vx[sl] = s.qvel[sl];
     WSYNC();
-    map_vx<NV>(m, s, sl, nb);     // row velocities J qvel for aref
+    map_vx<NV>(s, sl, nb, chain_mask(m, sl, nb));     // row velocities J qvel for aref
 #pragma unroll
     for (int q = 0; q < RPL; q++) {
       int r = sl + HL * q;
@@ -1061,7 +1067,8 @@ struct Stepper {
           pos = s.con_dist[id];
           margin = m->pair_margin[p];
           sr = m->pair_solref[p]; si = m->pair_solimp[p];
-          T tran = m->body_invweight_tran[m->pair_b1[p]] + m->body_invweight_tran[m->pair_b2[p]];
+          const uint32_t bb = s.con_bb[id];
+          T tran = m->body_invweight_tran[bb & 0xff] + m->body_invweight_tran[(bb >> 8) & 0xff];
           T mu = s.con_mu[id];
           dA = kind == RK_CN ? tran : tran + mu * mu * tran;
           rd[q] = kid;
@@ -1101,11 +1108,12 @@ struct Stepper {
 #pragma unroll
     for (int q = 0; q < RPL; q++) vr[q] = sl + HL * q < nefc;
     const uint32_t anci = sl < NV ? m->dof_ancmask[sl] : 0u;
+    const uint32_t bch = chain_mask(m, sl, nb);     // loaded once per solve (map_vx per iteration)
     const T scale = m->newton_scale;
     if (sl < NV) s.vx[sl] = x;
     WSYNC();
     T Mx = matvec_lds(Mr, s.vx);     // kept current below (Mx += alpha M s)
-    map_vx<NV>(m, s, sl, nb);
+    map_vx<NV>(s, sl, nb, bch);
     T jar[RPL], Js[RPL];
 #pragma unroll
     for (int q = 0; q < RPL; q++) jar[q] = vr[q] ? row_Jx(m, s, rd[q], rc[q]) - ar[q] : T(0);
@@ -1218,7 +1226,9 @@ struct Stepper {
       T Ms = matvec_lds(Mr, s.vx);
       T A0 = hsum(sl < NV ? sdir * Ms : T(0));
       T B0 = hsum(sl < NV ? sdir * (Mx - fsmooth) : T(0));
-      map_vx<NV>(m, s, sl, nb);
+      HS_STAMP(clk, 18);
+      map_vx<NV>(s, sl, nb, bch);
+      HS_STAMP(clk, 19);
 #pragma unroll
       for (int q = 0; q < RPL; q++) Js[q] = vr[q] ? row_Jx(m, s, rd[q], rc[q]) : T(0);
       HS_STAMP(clk, 16);
@@ -1298,8 +1308,8 @@ struct Stepper {
     T cf[6] = {0, 0, 0, 0, 0, 0}, mv[3] = {0, 0, 0};
     if (b > 0 && b < nb) {
       for (int c = 0; c < s.ncon; c++) {
-        int p = s.con_pair[c];
-        int b1 = m->pair_b1[p], b2 = m->pair_b2[p];
+        const uint32_t bb = s.con_bb[c];
+        const int b1 = bb & 0xff, b2 = (bb >> 8) & 0xff;
         if (b != b1 && b != b2) continue;
         const T sg = b == b2 ? T(1) : T(-1);
         T r[3] = {s.con_pos[c][0] - s.com[0], s.con_pos[c][1] - s.com[1], s.con_pos[c][2] - s.com[2]}, t[3];

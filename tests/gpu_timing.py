@@ -13,8 +13,8 @@ from mujocoposelearning_amd.model import HsModel  # noqa: E402
 
 NAMES = ["load", "kinematics", "mass_matrix", "vel+rne", "collision", "rows+aref", "newton:init Jx",
          "newton:rowf+aggr", "newton:gradient", "newton:hessian", "newton:solve", "newton:ls loop",
-         "newton:final frc", "euler:integrate", "obs+writeback", "newton:chol", "newton:ls setup (M s, J s)",
-         "euler:chol+solve"]
+         "newton:final frc", "euler:integrate", "obs+writeback", "newton:chol", "newton:ls J s rows",
+         "euler:chol+solve", "newton:ls M s", "newton:ls map_vx"]
 NS = len(NAMES)
 
 
