@@ -1575,7 +1575,8 @@ __device__ __forceinline__ void commit(MPtr<T> m, const EnvBuffers<T>& b, const 
     T* a = b.aux + (size_t)env * AUXDIM;
     a[MAXDOF + 0] = s.com[0]; a[MAXDOF + 1] = s.com[1]; a[MAXDOF + 2] = s.com[2];
     a[MAXDOF + 3] = (T)s.ncon; a[MAXDOF + 4] = (T)s.nefc; a[MAXDOF + 5] = (T)st.niter;
-    for (int k = 0; k < NWARN; k++) b.warning[(size_t)env * NWARN + k] += warn[k];
+    for (int k = 0; k < NWARN; k++)   // read-modify-write only when set (a load here would wait for
+      if (warn[k]) b.warning[(size_t)env * NWARN + k] += warn[k];   // every store issued above)
   }
   if (full) {   // data.cfrc_ext / data.subtree_linvel of the last substep (pre-integration)
     const int nb = m->nbody;
@@ -1626,6 +1627,8 @@ __global__ __launch_bounds__(64, sizeof(T) == 4 ? 2 : 1) void step_kernel(MPtr<T
   int step_count = b.step_count[env];
   uint32_t episode = b.episode[env];
   T total = b.total_reward[env];
+  // the action is the same for all substeps: one load, issued with the state loads
+  const T act = (actions && sl < nu) ? (T)actions[(size_t)env * nu + sl] : T(0);
   T* obs_out = b.obs + (size_t)env * p.obs_dim;
   const int nsub = (p.mode == MODE_RESET) ? 0 : p.nsub;
   bool in_reset = false;
@@ -1696,7 +1699,7 @@ __global__ __launch_bounds__(64, sizeof(T) == 4 ? 2 : 1) void step_kernel(MPtr<T
       break;
     } else {
       // data.ctrl[:] = action each substep (custom_env.py:159); mj_resetData may have zeroed it
-      if (sl < nu && actions) s.ctrl[sl] = (T)actions[(size_t)env * nu + sl];
+      if (sl < nu && actions) s.ctrl[sl] = act;
       WSYNC();
     }
     physics_step(st, p, time, xws, warn);
