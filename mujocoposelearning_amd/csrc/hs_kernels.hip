@@ -132,6 +132,24 @@ template <typename T>
 using MPtr = const __attribute__((address_space(4))) DevModel<T>*;
 template <typename T>
 using CPtr = const __attribute__((address_space(4))) T*;      // pointer into the model
+// All launch arguments travel as ONE by-value struct, so it sits at offset 0 of the kernarg
+// segment.  The kernel reads it through an opaque()-laundered constant-address-space pointer to
+// that segment: every use is a fresh scalar load (scalar cache) instead of ~80 SGPRs kept live
+// for the whole kernel (which spill to VGPR lanes, and the per-lane buffer addresses derived
+// from them to scratch -- 150 B/lane of spill traffic written back to HBM every launch).
+template <typename T>
+struct KArgs {
+  MPtr<T> m;
+  EnvBuffers<T> b;
+  const float* actions;       // [N][nu] f32 (null in MODE_RESET)
+  const uint8_t* reset_mask;  // [N] or null
+  const T* nz_q;              // [N][nq] host reset noise or null (device RNG)
+  const T* nz_v;              // [N][nv] or null
+  StepParams p;
+  int nenv;
+};
+template <typename T>
+using KPtr = const __attribute__((address_space(4))) KArgs<T>*;
 // Same for a per-lane value: stops lane-invariant compare masks (j <= sl, bit(mask, sl), ...)
 // being hoisted out of the loops as dozens of 64-bit SGPR masks (which then spill).
 __device__ __forceinline__ int opaque_v(int x) {
@@ -1403,7 +1421,7 @@ __device__ __forceinline__ void reset_state(MPtr<T> m, Scratch<T>& s, int sl, T&
 }
 
 template <typename T, int NV>
-__device__ __forceinline__ void physics_step(Stepper<T, NV>& st, const StepParams& p, T& time, T& xws, int* warn) {
+__device__ __forceinline__ void physics_step(Stepper<T, NV>& st, KPtr<T> k, T& time, T& xws, int* warn) {
   MPtr<T> m = st.m;
   Scratch<T>& s = st.s;
   const int sl = st.sl;
@@ -1427,7 +1445,7 @@ __device__ __forceinline__ void physics_step(Stepper<T, NV>& st, const StepParam
     HS_STAMP(st.clk, 3);
     if (st.rows(D, ar, rd, rc)) warn[WARN_OVERFLOW]++;
     HS_STAMP(st.clk, 5);
-    st.solve(xws, p.max_newton, sizeof(T) == 8 ? T(1e-13) : T(1e-7), D, ar, rd, rc);
+    st.solve(xws, opaque(k)->p.max_newton, sizeof(T) == 8 ? T(1e-13) : T(1e-7), D, ar, rd, rc);
     bool ba = sl < m->nv && isbad(st.qacc);
     bool redo = hballot(ba, up) != 0 && attempt == 0;
     if (__ballot(redo) == 0) break;          // wave-uniform loop control
@@ -1436,7 +1454,7 @@ __device__ __forceinline__ void physics_step(Stepper<T, NV>& st, const StepParam
       reset_state(m, s, sl, time, xws);
     }
   }
-  if (p.full_state) st.post_constraint();   // pre-integration state, like cinert / cvel in the obs
+  if (opaque(k)->p.full_state) st.post_constraint();   // pre-integration state, like cinert / cvel in the obs
   st.euler(time);
   HS_STAMP(st.clk, 13);
   xws = st.qacc;
@@ -1452,7 +1470,7 @@ __device__ __forceinline__ void foot_forces(MPtr<T> m, const Scratch<T>& s, T& l
 }
 
 template <typename T>
-__device__ __forceinline__ T compute_reward(MPtr<T> m, const Scratch<T>& s, const StepParams& p, T time,
+__device__ __forceinline__ T compute_reward(MPtr<T> m, const Scratch<T>& s, KPtr<T> k, T time,
                             T energy_sum) {
   // quaternion_to_euler (utils.py:3-21): pitch = arcsin(2(wy - zx)), not clamped
   T w = s.qpos[3], x = s.qpos[4], y = s.qpos[5], z = s.qpos[6];
@@ -1460,16 +1478,16 @@ __device__ __forceinline__ T compute_reward(MPtr<T> m, const Scratch<T>& s, cons
   T pitch = asin(2 * (w * y - z * x));
   T h = s.qpos[2];
   int nu = m->nu;
-  if (p.reward_id == REWARD_STAND || p.reward_id == REWARD_WALK) {
+  if (k->p.reward_id == REWARD_STAND || k->p.reward_id == REWARD_WALK) {
     T c2 = 0;
     for (int u = 0; u < nu; u++) c2 += s.ctrl[u] * s.ctrl[u];
     T torque = exp(T(-0.05) * c2);
     T post = T(0.5) * exp(T(-2) * (h - T(1.282)) * (h - T(1.282))) + T(0.5) * exp(T(-3) * (roll * roll + pitch * pitch));
-    if (p.reward_id == REWARD_STAND) {
+    if (k->p.reward_id == REWARD_STAND) {
       // cfrc_ext is never computed by mj_step without sensors -> both "feet" forces are 0 (full_state:
       // the real wrenches of the last two bodies, reward_functions.py:176-177)
       T lf = 0, rf = 0;
-      if (p.full_state) foot_forces(m, s, lf, rf);
+      if (k->p.full_state) foot_forces(m, s, lf, rf);
       T foot = 1 - fmin(lf, rf) / (lf + rf + T(1e-8));
       T vr = exp(T(-2) * (s.qvel[0] - 1) * (s.qvel[0] - 1));
       T r = T(0.4) * vr + T(0.3) * post + T(0.2) * foot + T(0.1) * torque;
@@ -1478,25 +1496,25 @@ __device__ __forceinline__ T compute_reward(MPtr<T> m, const Scratch<T>& s, cons
     T vr = exp(T(-0.5) * (s.qvel[0] - 10) * (s.qvel[0] - 10));
     return h < T(0.8) ? T(0.1) * h / T(0.8) : vr + post * torque;
   }
-  if (p.reward_id == REWARD_KNEELING) {
-    const double* k = p.kneel;   // target_height, min_height, max_roll_pitch, com_radius, energy_w, posture_w, com_w, foot_w, alive_w
-    if (h < T(k[1])) return h * h;
-    T mrp = T(k[2]);
+  if (k->p.reward_id == REWARD_KNEELING) {
+    CPtr<double> kn = k->p.kneel;   // target_height, min_height, max_roll_pitch, com_radius, energy_w, posture_w, com_w, foot_w, alive_w
+    if (h < T(kn[1])) return h * h;
+    T mrp = T(kn[2]);
     T posture = T(0.7) * exp(T(-5) * (roll * roll + pitch * pitch) / (mrp * mrp)) +
-                T(0.3) * exp(T(-5) * (h - T(k[0])) * (h - T(k[0])));
+                T(0.3) * exp(T(-5) * (h - T(kn[0])) * (h - T(kn[0])));
     T dist = sqrt(s.com[0] * s.com[0] + s.com[1] * s.com[1]);
     T comv = T(0);   // subtree_linvel is lazy in MuJoCo -> 0 (full_state: |subtree_linvel[0]|^2)
     T foot = T(0);   // min(0,0)/(0+0+1e-8)
-    if (p.full_state) {
+    if (k->p.full_state) {
       for (int q = 0; q < 3; q++) comv += s.u.n.linv[0][q] * s.u.n.linv[0][q];
       T lf, rf;
       foot_forces(m, s, lf, rf);
       foot = fmin(lf, rf) / (lf + rf + T(1e-8));
     }
-    T com = T(0.7) * exp(T(-10) * (dist / T(k[3]))) + T(0.3) * exp(T(-0.1) * comv);
+    T com = T(0.7) * exp(T(-10) * (dist / T(kn[3]))) + T(0.3) * exp(T(-0.1) * comv);
     T energy = exp(T(-0.01) * energy_sum);
     T alive = 1 - exp(T(-0.5) * time);
-    return T(k[5]) * posture + T(k[6]) * com + T(k[7]) * foot + T(k[4]) * energy + T(k[8]) * alive;
+    return T(kn[5]) * posture + T(kn[6]) * com + T(kn[7]) * foot + T(kn[4]) * energy + T(kn[8]) * alive;
   }
   return T(0);
 }
@@ -1554,34 +1572,34 @@ __device__ __forceinline__ void dump_debug(const Stepper<T, NV>& st, T* dbg) {
 
 // per-env commit of state + aux (one half-wave)
 template <typename T, int NV>
-__device__ __forceinline__ void commit(MPtr<T> m, const EnvBuffers<T>& b, const Stepper<T, NV>& st,
+__device__ __forceinline__ void commit(MPtr<T> m, KPtr<T> k, const Stepper<T, NV>& st,
                        int env, T time, T xws, int step_count, uint32_t episode, T total, const int* warn,
                        bool full) {
   const Scratch<T>& s = st.s;
   const int sl = st.sl, nq = m->nq, nv = m->nv, nu = m->nu;
-  if (sl < nq) b.qpos[(size_t)env * nq + sl] = s.qpos[sl];
-  if (sl + HL < nq) b.qpos[(size_t)env * nq + sl + HL] = s.qpos[sl + HL];
+  if (sl < nq) k->b.qpos[(size_t)env * nq + sl] = s.qpos[sl];
+  if (sl + HL < nq) k->b.qpos[(size_t)env * nq + sl + HL] = s.qpos[sl + HL];
   if (sl < nv) {
-    b.qvel[(size_t)env * nv + sl] = s.qvel[sl];
-    b.qacc_ws[(size_t)env * nv + sl] = xws;
-    b.aux[(size_t)env * AUXDIM + sl] = st.qacc;
+    k->b.qvel[(size_t)env * nv + sl] = s.qvel[sl];
+    k->b.qacc_ws[(size_t)env * nv + sl] = xws;
+    k->b.aux[(size_t)env * AUXDIM + sl] = st.qacc;
   }
-  if (sl < nu) b.ctrl[(size_t)env * nu + sl] = s.ctrl[sl];
+  if (sl < nu) k->b.ctrl[(size_t)env * nu + sl] = s.ctrl[sl];
   if (sl == 0) {
-    b.time[env] = time;
-    b.step_count[env] = step_count;
-    b.episode[env] = episode;
-    b.total_reward[env] = total;
-    T* a = b.aux + (size_t)env * AUXDIM;
+    k->b.time[env] = time;
+    k->b.step_count[env] = step_count;
+    k->b.episode[env] = episode;
+    k->b.total_reward[env] = total;
+    T* a = k->b.aux + (size_t)env * AUXDIM;
     a[MAXDOF + 0] = s.com[0]; a[MAXDOF + 1] = s.com[1]; a[MAXDOF + 2] = s.com[2];
     a[MAXDOF + 3] = (T)s.ncon; a[MAXDOF + 4] = (T)s.nefc; a[MAXDOF + 5] = (T)st.niter;
-    for (int k = 0; k < NWARN; k++)   // read-modify-write only when set (a load here would wait for
-      if (warn[k]) b.warning[(size_t)env * NWARN + k] += warn[k];   // every store issued above)
+    for (int w = 0; w < NWARN; w++)   // read-modify-write only when set (a load here would wait for
+      if (warn[w]) k->b.warning[(size_t)env * NWARN + w] += warn[w];   // every store issued above)
   }
   if (full) {   // data.cfrc_ext / data.subtree_linvel of the last substep (pre-integration)
     const int nb = m->nbody;
-    for (int k = sl; k < 6 * nb; k += HL) b.cfrc_ext[(size_t)env * 6 * nb + k] = s.u.n.cfrc[k / 6][k % 6];
-    for (int k = sl; k < 3 * nb; k += HL) b.subtree_linvel[(size_t)env * 3 * nb + k] = s.u.n.linv[k / 3][k % 3];
+    for (int q = sl; q < 6 * nb; q += HL) k->b.cfrc_ext[(size_t)env * 6 * nb + q] = s.u.n.cfrc[q / 6][q % 6];
+    for (int q = sl; q < 3 * nb; q += HL) k->b.subtree_linvel[(size_t)env * 3 * nb + q] = s.u.n.linv[q / 3][q % 3];
   }
 }
 
@@ -1589,31 +1607,43 @@ __device__ __forceinline__ void commit(MPtr<T> m, const EnvBuffers<T>& b, const 
 template <typename T, int NV>
 // 2 waves/SIMD (the VGPR budget of 256) for the fp32 engine; the fp64 parity engine needs more
 // registers and runs at 1
-__global__ __launch_bounds__(64, sizeof(T) == 4 ? 2 : 1) void step_kernel(MPtr<T> m, EnvBuffers<T> b,
-                                                  const float* __restrict__ actions,
-                                                  const uint8_t* __restrict__ reset_mask,
-                                                  const T* __restrict__ nz_q, const T* __restrict__ nz_v,
-                                                  StepParams p, int nenv) {
+__global__ __launch_bounds__(64, sizeof(T) == 4 ? 2 : 1) void step_kernel(KArgs<T> /* read via kernarg ptr */) {
   __shared__ Scratch<T> smem[2];
+  const KPtr<T> ka = (KPtr<T>)__builtin_amdgcn_kernarg_segment_ptr();
   const int lane = threadIdx.x;
   const bool up = lane >= HL;
   const int sl = lane & (HL - 1);
+  const int nenv = ka->nenv;
   const int env_raw = 2 * blockIdx.x + (up ? 1 : 0);
   bool active = env_raw < nenv;                       // ghost half for odd N
   const int env = active ? env_raw : nenv - 1;
-  if (p.mode == MODE_RESET && reset_mask && !reset_mask[env]) active = false;
+  const int mode = ka->p.mode;
+  if (mode == MODE_RESET && ka->reset_mask && !ka->reset_mask[env]) active = false;
   if (__ballot(active) == 0) return;                  // wave-uniform exit
   Scratch<T>& s = smem[up ? 1 : 0];
+  MPtr<T> m = ka->m;
   const int nq = m->nq, nv = m->nv, nu = m->nu;
   Stepper<T, NV> st(m, s, lane);
-  if (b.dbg && env == 0 && active) st.dbg = b.dbg;
+  if (ka->b.dbg && env == 0 && active) st.dbg = ka->b.dbg;
   int warn[NWARN] = {0, 0, 0, 0};
-  T time = b.time[env];
-  T xws = (sl < nv) ? b.qacc_ws[(size_t)env * nv + sl] : T(0);
-  if (sl < nq) s.qpos[sl] = b.qpos[(size_t)env * nq + sl];
-  if (sl + HL < nq) s.qpos[sl + HL] = b.qpos[(size_t)env * nq + sl + HL];
-  if (sl < nv) s.qvel[sl] = b.qvel[(size_t)env * nv + sl];
-  if (sl < nu) s.ctrl[sl] = b.ctrl[(size_t)env * nu + sl];
+  T time, xws;
+  int step_count;
+  uint32_t episode;
+  T total, act;
+  {
+    time = ka->b.time[env];
+    xws = (sl < nv) ? ka->b.qacc_ws[(size_t)env * nv + sl] : T(0);
+    if (sl < nq) s.qpos[sl] = ka->b.qpos[(size_t)env * nq + sl];
+    if (sl + HL < nq) s.qpos[sl + HL] = ka->b.qpos[(size_t)env * nq + sl + HL];
+    if (sl < nv) s.qvel[sl] = ka->b.qvel[(size_t)env * nv + sl];
+    if (sl < nu) s.ctrl[sl] = ka->b.ctrl[(size_t)env * nu + sl];
+    step_count = ka->b.step_count[env];
+    episode = ka->b.episode[env];
+    total = ka->b.total_reward[env];
+    // the action is the same for all substeps: one load, issued with the state loads
+    const float* actions = ka->actions;
+    act = (actions && sl < nu) ? (T)actions[(size_t)env * nu + sl] : T(0);
+  }
   WSYNC();
   st.clk.start();
   st.qfa = 0;
@@ -1623,14 +1653,8 @@ __global__ __launch_bounds__(64, sizeof(T) == 4 ? 2 : 1) void step_kernel(MPtr<T
   // Both halves always run the same instruction stream; a half that is inactive (ghost env,
   // masked reset) or not resetting while its partner resets computes on scratch but commits
   // nothing (its real state was committed before the shared reset pass).
-  bool do_reset = p.mode == MODE_RESET && active;
-  int step_count = b.step_count[env];
-  uint32_t episode = b.episode[env];
-  T total = b.total_reward[env];
-  // the action is the same for all substeps: one load, issued with the state loads
-  const T act = (actions && sl < nu) ? (T)actions[(size_t)env * nu + sl] : T(0);
-  T* obs_out = b.obs + (size_t)env * p.obs_dim;
-  const int nsub = (p.mode == MODE_RESET) ? 0 : p.nsub;
+  bool do_reset = mode == MODE_RESET && active;
+  const int nsub = (mode == MODE_RESET) ? 0 : ka->p.nsub;
   bool in_reset = false;
 #ifdef HS_TIMING
   int tot_iter = 0;
@@ -1638,53 +1662,59 @@ __global__ __launch_bounds__(64, sizeof(T) == 4 ? 2 : 1) void step_kernel(MPtr<T
   // One loop, ONE inlined physics_step call site: substeps 0..nsub-1 apply the action; after the
   // last one the env bookkeeping runs; if any half of the wave must reset, one more substep
   // runs with the reset state (a half that is not resetting has already committed and computes
-  // on scratch only).
+  // on scratch only).  Launch arguments are re-read through k = opaque(ka) at each use.
   for (int sub = 0;; sub++) {
     st.m = opaque(st.m);
     st.sl = opaque_v(st.sl);
     if (sub == nsub && !in_reset) {
       if (nsub > 0) {
-        if (active) write_obs(st.m, s, sl, st.qfa, obs_out, p.obs_dim);
-        if (p.mode == MODE_ENV_STEP) {
+        KPtr<T> k = opaque(ka);
+        const int obs_dim = k->p.obs_dim;
+        if (active) write_obs(st.m, s, sl, st.qfa, k->b.obs + (size_t)env * obs_dim, obs_dim);
+        if (k->p.mode == MODE_ENV_STEP) {
           step_count += 1;
-          bool trunc = step_count >= p.max_steps;
+          bool trunc = step_count >= k->p.max_steps;
           T e = (sl >= 6 && sl < nv) ? st.qfa * s.qvel[sl] : T(0);
           T esum = hsum(e * e);
-          T r = trunc ? T(0) : compute_reward(st.m, s, p, time, esum);
+          T r = trunc ? T(0) : compute_reward(st.m, s, k, time, esum);
           total += r;
-          bool term = (double)time >= p.duration;
+          bool term = (double)time >= k->p.duration;
           if (sl == 0 && active) {
-            b.reward[env] = r;
-            b.terminated[env] = term;
-            b.truncated[env] = trunc;
+            k->b.reward[env] = r;
+            k->b.terminated[env] = term;
+            k->b.truncated[env] = trunc;
           }
-          if ((term || trunc) && p.autoreset && active) {
-            write_obs(st.m, s, sl, st.qfa, b.terminal_obs + (size_t)env * p.obs_dim, p.obs_dim);
+          if ((term || trunc) && k->p.autoreset && active) {
+            write_obs(st.m, s, sl, st.qfa, k->b.terminal_obs + (size_t)env * obs_dim, obs_dim);
             do_reset = true;
           }
         }
         if (active && !do_reset) {
-          commit(st.m, b, st, env, time, xws, step_count, episode, total, warn, p.full_state != 0);
+          commit(st.m, k, st, env, time, xws, step_count, episode, total, warn, k->p.full_state != 0);
           active = false;   // committed; a reset pass below is scratch work for this half
         }
       }
       if (__ballot(do_reset) == 0) break;
       // custom_env.py:97-130: mj_resetData; qpos = init (z=1.282, upright); += U(+-0.01) noise
       // with z noise x0.1 and no quaternion noise; qvel = U(+-0.01); one mj_step with ctrl = 0.
+      KPtr<T> k = opaque(ka);
       in_reset = true;
       st.dbg = nullptr;
-      T sc = (T)p.noise_scale;
+      T sc = (T)k->p.noise_scale;
+      const uint64_t seed = k->p.seed;
+      const T* nz_q = k->nz_q;
+      const T* nz_v = k->nz_v;
       uint32_t ep = episode + 1;
-      for (int k = sl; k < nq; k += HL) {
-        T q = m->qpos0[k];
-        T nzq = nz_q ? nz_q[(size_t)env * nq + k] : uniform_pm<T>(p.seed, env, ep, k, sc);
+      for (int q = sl; q < nq; q += HL) {
+        T v = m->qpos0[q];
+        T nzq = nz_q ? nz_q[(size_t)env * nq + q] : uniform_pm<T>(seed, env, ep, q, sc);
         if (m->jnt_type[0] == JNT_FREE) {
-          if (k == 2) { q = (T)p.init_height; nzq *= T(0.1); }
-          if (k >= 3 && k < 7) { q = k == 3 ? T(1) : T(0); nzq = 0; }
+          if (q == 2) { v = (T)k->p.init_height; nzq *= T(0.1); }
+          if (q >= 3 && q < 7) { v = q == 3 ? T(1) : T(0); nzq = 0; }
         }
-        s.qpos[k] = q + nzq;
+        s.qpos[q] = v + nzq;
       }
-      if (sl < nv) s.qvel[sl] = nz_v ? nz_v[(size_t)env * nv + sl] : uniform_pm<T>(p.seed, env, ep, 64 + sl, sc);
+      if (sl < nv) s.qvel[sl] = nz_v ? nz_v[(size_t)env * nv + sl] : uniform_pm<T>(seed, env, ep, 64 + sl, sc);
       if (sl < nu) s.ctrl[sl] = 0;
       xws = 0;
       time = 0;
@@ -1692,32 +1722,35 @@ __global__ __launch_bounds__(64, sizeof(T) == 4 ? 2 : 1) void step_kernel(MPtr<T
       WSYNC();
     } else if (sub > nsub) {
       if (do_reset && active) {
-        if (b.dbg && env == 0) dump_debug(st, b.dbg);
-        write_obs(st.m, s, sl, st.qfa, obs_out, p.obs_dim);
-        commit(st.m, b, st, env, time, xws, 0, episode, T(0), warn, p.full_state != 0);
+        KPtr<T> k = opaque(ka);
+        if (k->b.dbg && env == 0) dump_debug(st, k->b.dbg);
+        const int obs_dim = k->p.obs_dim;
+        write_obs(st.m, s, sl, st.qfa, k->b.obs + (size_t)env * obs_dim, obs_dim);
+        commit(st.m, k, st, env, time, xws, 0, episode, T(0), warn, k->p.full_state != 0);
       }
       break;
     } else {
       // data.ctrl[:] = action each substep (custom_env.py:159); mj_resetData may have zeroed it
-      if (sl < nu && actions) s.ctrl[sl] = act;
+      if (sl < nu && opaque(ka)->actions) s.ctrl[sl] = act;
       WSYNC();
     }
-    physics_step(st, p, time, xws, warn);
+    physics_step(st, ka, time, xws, warn);
 #ifdef HS_TIMING
     tot_iter += st.niter;
 #endif
-    if (b.dbg && env == 0 && active && !in_reset) dump_debug(st, b.dbg);
+    if (st.dbg && active && !in_reset) dump_debug(st, st.dbg);
   }
 #ifdef HS_TIMING
   HS_STAMP(st.clk, 14);
-  if (sl == 0 && b.dbg) {
-    for (int k = 0; k < NSLOT; k++) atomicAdd(&b.dbg[8000 + k], (T)st.clk.acc[k]);
-    atomicAdd(&b.dbg[8020], (T)st.niter);
+  T* dbg = ka->b.dbg;
+  if (sl == 0 && dbg) {
+    for (int q = 0; q < NSLOT; q++) atomicAdd(&dbg[8000 + q], (T)st.clk.acc[q]);
+    atomicAdd(&dbg[8020], (T)st.niter);
   }
   // per-wave lifetime of this launch (shader cycles) -> dbg[9000 + wave] (waves < 7000)
-  if (lane == 0 && b.dbg && blockIdx.x < 2048) b.dbg[9000 + blockIdx.x] = (T)(st.clk.prev - st.clk.t0);
+  if (lane == 0 && dbg && blockIdx.x < 2048) dbg[9000 + blockIdx.x] = (T)(st.clk.prev - st.clk.t0);
   // per-env Newton iterations summed over this launch's substeps -> dbg[11100 + env]
-  if (sl == 0 && b.dbg && blockIdx.x < 2048) b.dbg[11100 + 2 * blockIdx.x + (up ? 1 : 0)] = (T)tot_iter;
+  if (sl == 0 && dbg && blockIdx.x < 2048) dbg[11100 + 2 * blockIdx.x + (up ? 1 : 0)] = (T)tot_iter;
 #endif
 }
 
@@ -1731,8 +1764,8 @@ hipError_t launch_step(const DevModel<T>* dmodel, int nv, const EnvBuffers<T>& b
   dim3 grid((nenv + 1) / 2), block(WAVE);
   switch (nv) {
     case 27:
-      hipLaunchKernelGGL((step_kernel<T, 27>), grid, block, 0, stream, (MPtr<T>)dmodel, b, actions, reset_mask, noise_qpos,
-                         noise_qvel, p, nenv);
+      hipLaunchKernelGGL((step_kernel<T, 27>), grid, block, 0, stream,
+                         KArgs<T>{(MPtr<T>)dmodel, b, actions, reset_mask, noise_qpos, noise_qvel, p, nenv});
       break;
     default:
       return hipErrorInvalidValue;
