@@ -694,15 +694,19 @@ struct Stepper {
       s.u.k.xquat[0][0] = 1; s.u.k.xquat[0][1] = s.u.k.xquat[0][2] = s.u.k.xquat[0][3] = 0;
       for (int k = 0; k < 9; k++) s.u.k.xmat[0][k] = (k % 4 == 0) ? T(1) : T(0);
     }
-    // Everything a body needs that does not depend on its parent is loaded / computed before the
-    // level loop (one model-load latency instead of one dependent chain per level; the joint
-    // half-angle rotations are computed by all bodies at once).
+    // mj_kinematics, split so the serial level loop carries one frame composition per level:
+    // (1) in parallel over bodies, the body's transform RELATIVE TO ITS PARENT (body_pos/quat
+    //     followed by its hinges, each rotating about jnt_pos: p' = a - R(q qloc) jpos with the
+    //     anchor a = p + R(q) jpos) and each hinge's anchor/axis in the parent frame;
+    // (2) level by level: xquat = normalize(xquat_par * q_loc), xpos = xpos_par + xmat_par p_loc;
+    // (3) in parallel again: xanchor = xpos_par + xmat_par a_loc, xaxis = xmat_par ax_loc.
+    // Mathematically identical to MuJoCo's per-joint world-frame recursion (rounding differs).
     const int b = sl;
     const bool isb = b > 0 && b < nb;
     int depth = -1, par = 0, ja = 0, jn = 0, fqa = 0;
     bool isfree = false;
-    T bp[3] = {0, 0, 0}, bq[4] = {1, 0, 0, 0};
-    T jpos[MAXJPB][3], jax[MAXJPB][3], jrot[MAXJPB][4];
+    T pl[3] = {0, 0, 0}, ql[4] = {1, 0, 0, 0};
+    T anl[MAXJPB][3], axl[MAXJPB][3];
     if (isb) {
       depth = m->body_depth[b];
       par = m->body_parentid[b];
@@ -710,53 +714,51 @@ struct Stepper {
       jn = m->body_jntnum[b];
       isfree = jn == 1 && m->jnt_type[ja] == JNT_FREE;
       fqa = m->jnt_qposadr[ja];
-      for (int k = 0; k < 3; k++) bp[k] = m->body_pos[b][k];
-      for (int k = 0; k < 4; k++) bq[k] = m->body_quat[b][k];
+      for (int k = 0; k < 3; k++) pl[k] = m->body_pos[b][k];
+      for (int k = 0; k < 4; k++) ql[k] = m->body_quat[b][k];
+    }
+    if (isfree) {
+      for (int k = 0; k < 3; k++) pl[k] = s.qpos[fqa + k];
+      for (int k = 0; k < 4; k++) ql[k] = s.qpos[fqa + 3 + k];
     }
 #pragma unroll
     for (int jj = 0; jj < MAXJPB; jj++) {
       const bool use = isb && !isfree && jj < jn;
       const int j = use ? ja + jj : 0;
-      T ang = 0;
-      for (int k = 0; k < 3; k++) { jpos[jj][k] = use ? m->jnt_pos[j][k] : T(0); jax[jj][k] = use ? m->jnt_axis[j][k] : T(0); }
+      T jp[3], jx[3], ang = 0;
+      for (int k = 0; k < 3; k++) { jp[k] = use ? m->jnt_pos[j][k] : T(0); jx[k] = use ? m->jnt_axis[j][k] : T(0); }
       if (use) {
         int qa = m->jnt_qposadr[j];
         ang = s.qpos[qa] - m->qpos0[qa];
       }
       T sn, cs;
       sincos_t(T(0.5) * ang, sn, cs);
-      jrot[jj][0] = cs; jrot[jj][1] = jax[jj][0] * sn; jrot[jj][2] = jax[jj][1] * sn; jrot[jj][3] = jax[jj][2] * sn;
+      const T jr[4] = {cs, jx[0] * sn, jx[1] * sn, jx[2] * sn};
+      T R[9];
+      quat2mat(ql, R);
+      mv3(R, jx, axl[jj]);
+      mv3(R, jp, anl[jj]);
+      for (int k = 0; k < 3; k++) anl[jj][k] += pl[k];
+      if (use) {
+        mulq(ql, jr, ql);
+        quat2mat(ql, R);
+        T v[3];
+        mv3(R, jp, v);
+        for (int k = 0; k < 3; k++) pl[k] = anl[jj][k] - v[k];
+      }
     }
     WSYNC();
     for (int L = 1; L <= m->nlevel; L++) {
       if (depth == L) {
         T pos[3], q[4];
-        if (isfree) {
-          for (int k = 0; k < 3; k++) pos[k] = s.qpos[fqa + k];
-          for (int k = 0; k < 4; k++) q[k] = s.qpos[fqa + 3 + k];
-          normalize4(q);
-          for (int k = 0; k < 3; k++) { s.u.k.xanchor[ja][k] = pos[k]; s.u.k.xaxis[ja][k] = m->jnt_axis[ja][k]; }
+        if (isfree) {   // parent is the world: the free joint's qpos is the world frame
+          for (int k = 0; k < 3; k++) pos[k] = pl[k];
+          for (int k = 0; k < 4; k++) q[k] = ql[k];
         } else {
-          mv3(s.u.k.xmat[par], bp, pos);
+          mv3(s.u.k.xmat[par], pl, pos);
           for (int k = 0; k < 3; k++) pos[k] += s.u.k.xpos[par][k];
           T pq[4] = {s.u.k.xquat[par][0], s.u.k.xquat[par][1], s.u.k.xquat[par][2], s.u.k.xquat[par][3]};
-          mulq(pq, bq, q);
-#pragma unroll
-          for (int jj = 0; jj < MAXJPB; jj++) {
-            if (jj < jn) {
-              T R[9], ax[3], an[3];
-              quat2mat(q, R);
-              mv3(R, jax[jj], ax);
-              mv3(R, jpos[jj], an);
-              for (int k = 0; k < 3; k++) an[k] += pos[k];
-              mulq(q, jrot[jj], q);
-              quat2mat(q, R);
-              T v[3];
-              mv3(R, jpos[jj], v);
-              for (int k = 0; k < 3; k++) pos[k] = an[k] - v[k];
-              for (int k = 0; k < 3; k++) { s.u.k.xanchor[ja + jj][k] = an[k]; s.u.k.xaxis[ja + jj][k] = ax[k]; }
-            }
-          }
+          mulq(pq, ql, q);
         }
         normalize4(q);
         for (int k = 0; k < 4; k++) s.u.k.xquat[b][k] = q[k];
@@ -764,6 +766,23 @@ struct Stepper {
         quat2mat(q, s.u.k.xmat[b]);
       }
       WSYNC();
+    }
+    if (isb) {
+      if (isfree) {
+        for (int k = 0; k < 3; k++) { s.u.k.xanchor[ja][k] = s.u.k.xpos[b][k]; s.u.k.xaxis[ja][k] = m->jnt_axis[ja][k]; }
+      } else {
+        const T* Rp = s.u.k.xmat[par];
+        const T* xp = s.u.k.xpos[par];
+#pragma unroll
+        for (int jj = 0; jj < MAXJPB; jj++) {
+          if (jj < jn) {
+            T an[3], ax[3];
+            mv3(Rp, anl[jj], an);
+            mv3(Rp, axl[jj], ax);
+            for (int k = 0; k < 3; k++) { s.u.k.xanchor[ja + jj][k] = xp[k] + an[k]; s.u.k.xaxis[ja + jj][k] = ax[k]; }
+          }
+        }
+      }
     }
     if (sl < m->ngeom) {
       int g = sl, gb = m->geom_bodyid[g];
