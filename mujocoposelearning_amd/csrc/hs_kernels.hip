@@ -640,7 +640,7 @@ __device__ __forceinline__ T jtf_lane(MPtr<T> m, const Scratch<T>& s, int sl, co
 // Built only with -DHS_TIMING (libhsim_timing.so): s_memtime stamps accumulated per phase,
 // summed over waves into dbg[8000 + slot].  The product build compiles them out.
 #ifdef HS_TIMING
-constexpr int NSLOT = 20;
+constexpr int NSLOT = 24;
 struct PhaseClock {
   uint64_t acc[NSLOT] = {0};
   uint64_t prev = 0, t0 = 0;
@@ -674,6 +674,7 @@ struct Stepper {
   T fcon;         // qfrc_constraint_i
   T qacc;         // solver output qacc_i
   T qfa;          // qfrc_actuator_i (obs / kneeling reward)
+  T damp;         // dof_damping_i, loaded with the constraint rows (Euler reads it)
   int niter;
   T* dbg = nullptr;   // stage-dump target (env 0 in debug mode only)
 
@@ -1001,6 +1002,7 @@ struct Stepper {
   // mj_makeConstraint + mj_makeImpedance + reference (aref); row q of this lane: r = sl + 32 q
   __device__ __forceinline__ int rows(T (&D)[RPL], T (&ar)[RPL], int (&rd)[RPL], T (&rc)[RPL]) {
     phase_begin();
+    damp = sl < NV ? m->dof_damping[sl] : T(0);
     int overflow = 0;
     int ncon = s.ncon;
     int nrow = 0;
@@ -1383,11 +1385,12 @@ struct Stepper {
     phase_begin();
     T h = m->timestep;
     T He[NV];
-    T damp = sl < NV ? m->dof_damping[sl] : T(0);
 #pragma unroll
     for (int j = 0; j < NV; j++) He[j] = Mr[j] + ((j == sl) ? h * damp : T(0));
+    HS_STAMP(clk, 20);
     T edinv = 0;
     chol_rows<NV>(He, edinv, sl, s.u.n.cb);
+    HS_STAMP(clk, 21);
     T a = chol_solve<NV>(He, edinv, fsmooth + fcon, sl);
     HS_STAMP(clk, 17);
     if (sl < NV) s.qvel[sl] += h * a;
@@ -1764,7 +1767,7 @@ __global__ __launch_bounds__(64, sizeof(T) == 4 ? 2 : 1) void step_kernel(KArgs<
   T* dbg = ka->b.dbg;
   if (sl == 0 && dbg) {
     for (int q = 0; q < NSLOT; q++) atomicAdd(&dbg[8000 + q], (T)st.clk.acc[q]);
-    atomicAdd(&dbg[8020], (T)st.niter);
+    atomicAdd(&dbg[8030], (T)st.niter);
   }
   // per-wave lifetime of this launch (shader cycles) -> dbg[9000 + wave] (waves < 7000)
   if (lane == 0 && dbg && blockIdx.x < 2048) dbg[9000 + blockIdx.x] = (T)(st.clk.prev - st.clk.t0);

@@ -14,7 +14,7 @@ from mujocoposelearning_amd.model import HsModel  # noqa: E402
 NAMES = ["load", "kinematics", "mass_matrix", "vel+rne", "collision", "rows+aref", "newton:init Jx",
          "newton:rowf+aggr", "newton:gradient", "newton:hessian", "newton:solve", "newton:ls loop",
          "newton:final frc", "euler:integrate", "obs+writeback", "newton:chol", "newton:ls J s rows",
-         "euler:chol+solve", "newton:ls M s", "newton:ls map_vx"]
+         "euler:solve", "newton:ls M s", "newton:ls map_vx", "euler:pre", "euler:chol", "-", "-"]
 NS = len(NAMES)
 
 
@@ -29,7 +29,7 @@ def main(n=4096, steps=20, prec="fp32"):
     b.set_debug(True)
     b.t["aux"].zero_()
     torch.cuda.synchronize()
-    dbg0 = b.get_debug()[8000:8021].copy()
+    dbg0 = b.get_debug()[8000:8031].copy()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
     for k in range(steps):
@@ -37,11 +37,11 @@ def main(n=4096, steps=20, prec="fp32"):
     ev1.record()
     torch.cuda.synchronize()
     ms = ev0.elapsed_time(ev1) / steps
-    d = b.get_debug()[8000:8021] - dbg0
+    d = b.get_debug()[8000:8031] - dbg0
     tot = d[:NS].sum()
     per = d[:NS] / (n * steps * 3)
     print(f"[{prec}] N={n}: {ms:.3f} ms/launch; cycles per env-substep (wave lifetime) {tot / (n * steps * 3):,.0f}; "
-          f"newton iters/substep {d[20] / (n * steps):.2f}")
+          f"newton iters/substep {d[30] / (n * steps):.2f}")
     for name, c, f in zip(NAMES, per, d[:NS] / tot):
         print(f"  {name:20s} {c:10,.0f} cyc  {100 * f:5.1f}%")
     life = b.get_debug()[9000:9000 + (n + 1) // 2]        # last launch, one value per wave
