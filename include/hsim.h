@@ -120,6 +120,13 @@ int hs_physics_step(hs_batch* b, const float* ctrl, int nsub, void* stream);
  * Any pointer may be NULL.  Arrays are [N][nq], [N][nv], [N][nv], [N], [N][nu]. */
 int hs_state_io(hs_batch* b, int dir, double* qpos, double* qvel, double* qacc_warmstart, double* time,
                 double* ctrl);
+/* mj_kinematics + mj_comPos of env `env` (visualisation; the pose data mujoco.Renderer.update_scene
+ * reads from mjData at custom_env.py:284-288).  qpos: nq fp64 values to pose instead of the env's
+ * current state (NULL = current).  Outputs, each nullable: xpos [nbody][3], xmat [nbody][9],
+ * geom_xpos [ngeom][3], geom_zaxis [ngeom][3] (capsule axis), com [3] (subtree_com of the root).
+ * Synchronous; not on the step path. */
+int hs_kinematics(hs_batch* b, int env, const double* qpos, double* xpos, double* xmat, double* geom_xpos,
+                  double* geom_zaxis, double* com);
 /* Stage dump of env 0 after its last substep (parity debugging); n >= 16384 doubles. */
 int hs_set_debug(hs_batch* b, int enable);
 int hs_get_debug(hs_batch* b, double* out, int n);

@@ -70,6 +70,7 @@ def lib():
         "hs_step": (i, [vp, vp, vp]),
         "hs_physics_step": (i, [vp, vp, i, vp]),
         "hs_state_io": (i, [vp, i, vp, vp, vp, vp, vp]),
+        "hs_kinematics": (i, [vp, i, vp, vp, vp, vp, vp, vp]),
         "hs_set_debug": (i, [vp, i]),
         "hs_get_debug": (i, [vp, vp, i]),
         "hs_synchronize": (i, [vp]),
@@ -87,7 +88,7 @@ def lib():
 
 EXPORTED = ("hs_model_load", "hs_model_free", "hs_model_field", "hs_batch_create", "hs_batch_destroy",
             "hs_batch_get_info", "hs_get_buffers", "hs_set_config", "hs_set_seed", "hs_get_config", "hs_reset", "hs_step",
-            "hs_physics_step", "hs_state_io", "hs_set_debug", "hs_get_debug", "hs_synchronize", "hs_gae",
+            "hs_physics_step", "hs_state_io", "hs_kinematics", "hs_set_debug", "hs_get_debug", "hs_synchronize", "hs_gae",
             "hs_last_error", "hs_version")
 
 

@@ -216,6 +216,26 @@ class HsBatch:
         for h, lo, hi in self._groups:
             check(lib().hs_state_io(h, 1, *[None if a is None else a[lo:hi].ctypes.data for a, _ in keep]))
 
+    def kinematics(self, env=0, qpos=None):
+        """mj_kinematics + mj_comPos of one env on the GPU (hs_kinematics): body xpos / xmat,
+        geom_xpos / geom_zaxis and the root subtree COM, fp64 on the host.  ``qpos`` poses that
+        configuration instead of the env's current one.  Visualisation only (one sync launch)."""
+        env = int(env)
+        for h, lo, hi in self._groups:
+            if lo <= env < hi:
+                break
+        else:
+            raise IndexError(f"env {env} out of range [0, {self.n})")
+        m = self.model
+        out = {"xpos": np.zeros((m.nbody, 3)), "xmat": np.zeros((m.nbody, 9)), "geom_xpos": np.zeros((m.ngeom, 3)),
+               "geom_zaxis": np.zeros((m.ngeom, 3)), "com": np.zeros(3)}
+        q = None if qpos is None else np.ascontiguousarray(qpos, np.float64)
+        if q is not None and q.shape != (m.nq,):
+            raise ValueError(f"qpos must have shape ({m.nq},)")
+        check(lib().hs_kinematics(h, env - lo, None if q is None else q.ctypes.data,
+                                  *[out[k].ctypes.data for k in ("xpos", "xmat", "geom_xpos", "geom_zaxis", "com")]))
+        return out
+
     def set_debug(self, on=True):
         check(lib().hs_set_debug(self._h, int(bool(on))))
 

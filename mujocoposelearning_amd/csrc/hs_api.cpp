@@ -170,6 +170,41 @@ int state_io(hs_batch* b, int dir, double* qpos, double* qvel, double* warm, dou
   }
   return 0;
 }
+template <typename T>
+int kinematics_io(hs_batch* b, int env, const double* qpos, double* xpos, double* xmat, double* gxpos,
+                  double* gzaxis, double* com) {
+  const auto& m = b->model->host;
+  T* dq = nullptr;
+  T* dout = nullptr;
+  int rc = -1;
+  std::vector<T> out(hs::KINDIM);
+  if (!hip_ok(hipMalloc(&dq, m.nq * sizeof(T)), "kinematics alloc") ||
+      !hip_ok(hipMalloc(&dout, hs::KINDIM * sizeof(T)), "kinematics alloc"))
+    goto done;
+  if (qpos) {
+    std::vector<T> q(qpos, qpos + m.nq);
+    if (!hip_ok(hipMemcpy(dq, q.data(), m.nq * sizeof(T), hipMemcpyHostToDevice), "kinematics qpos")) goto done;
+  } else if (!hip_ok(hipMemcpy(dq, (const T*)b->buf.qpos + (size_t)env * m.nq, m.nq * sizeof(T),
+                               hipMemcpyDeviceToDevice), "kinematics qpos")) {
+    goto done;
+  }
+  if (!hip_ok(hs::launch_kinematics<T>((const hs::DevModel<T>*)b->dmodel, m.nv, dq, dout, nullptr), "kinematics launch") ||
+      !hip_ok(hipMemcpy(out.data(), dout, hs::KINDIM * sizeof(T), hipMemcpyDeviceToHost), "kinematics out"))
+    goto done;
+  {
+    struct Part { double* dst; int off, n; } parts[] = {
+        {xpos, 0, m.nbody * 3}, {xmat, hs::MAXBODY * 3, m.nbody * 9}, {gxpos, hs::MAXBODY * 12, m.ngeom * 3},
+        {gzaxis, hs::MAXBODY * 12 + hs::MAXGEOM * 3, m.ngeom * 3}, {com, hs::MAXBODY * 12 + hs::MAXGEOM * 6, 3}};
+    for (auto& p : parts)
+      if (p.dst)
+        for (int k = 0; k < p.n; k++) p.dst[k] = (double)out[p.off + k];
+  }
+  rc = 0;
+done:
+  if (dq) (void)hipFree(dq);
+  if (dout) (void)hipFree(dout);
+  return rc;
+}
 }  // namespace
 
 extern "C" {
@@ -340,6 +375,16 @@ int hs_state_io(hs_batch* b, int dir, double* qpos, double* qvel, double* qacc_w
   if (!hip_ok(hipDeviceSynchronize(), "sync")) return -1;
   return b->precision == HS_FP64 ? state_io<double>(b, dir, qpos, qvel, qacc_warmstart, time, ctrl)
                                  : state_io<float>(b, dir, qpos, qvel, qacc_warmstart, time, ctrl);
+}
+
+int hs_kinematics(hs_batch* b, int env, const double* qpos, double* xpos, double* xmat, double* geom_xpos,
+                  double* geom_zaxis, double* com) {
+  if (!b) return fail("null batch");
+  if (env < 0 || env >= b->n) return fail("env index out of range");
+  DeviceGuard g(b->device);
+  if (!hip_ok(hipDeviceSynchronize(), "sync")) return -1;
+  return b->precision == HS_FP64 ? kinematics_io<double>(b, env, qpos, xpos, xmat, geom_xpos, geom_zaxis, com)
+                                 : kinematics_io<float>(b, env, qpos, xpos, xmat, geom_xpos, geom_zaxis, com);
 }
 
 int hs_set_debug(hs_batch* b, int enable) {

@@ -61,6 +61,11 @@ hipError_t launch_step(const DevModel<T>* dmodel, int nv, const EnvBuffers<T>& b
                        const uint8_t* reset_mask, const T* noise_qpos, const T* noise_qvel,
                        const StepParams& p, int nenv, hipStream_t stream);
 
+// mj_kinematics/mj_comPos of one state (device qpos[nq]) -> out[KINDIM] (see kin_kernel)
+constexpr int KINDIM = MAXBODY * 12 + MAXGEOM * 6 + 3;
+template <typename T>
+hipError_t launch_kinematics(const DevModel<T>* dmodel, int nv, const T* qpos, T* out, hipStream_t stream);
+
 // GAE reverse scan over [T][N] float32 rollout arrays (gae.hip)
 hipError_t launch_gae(const float* rew, const float* val, const float* start, const float* last_val,
                       const float* last_done, float* adv, float* ret, int T, int N, float gamma, float lam,

@@ -1776,6 +1776,33 @@ __global__ __launch_bounds__(64, sizeof(T) == 4 ? 2 : 1) void step_kernel(KArgs<
 #endif
 }
 
+// mj_kinematics + mj_comPos of ONE state (visualisation / data view, never the step path): one
+// wave, the lower half-wave computes, the upper half duplicates it.  out = [xpos MAXBODY*3]
+// [xmat MAXBODY*9][geom_xpos MAXGEOM*3][geom z-axis MAXGEOM*3][subtree_com[0] 3].
+template <typename T, int NV>
+__global__ __launch_bounds__(64) void kin_kernel(MPtr<T> m, const T* __restrict__ qpos, T* __restrict__ out) {
+  __shared__ Scratch<T> smem[2];
+  const int lane = threadIdx.x;
+  const bool up = lane >= HL;
+  const int sl = lane & (HL - 1);
+  Scratch<T>& s = smem[up ? 1 : 0];
+  for (int k = sl; k < m->nq; k += HL) s.qpos[k] = qpos[k];
+  WSYNC();
+  Stepper<T, NV> st(m, s, lane);
+  st.kinematics();
+  if (up) return;
+  const int nb = m->nbody, ng = m->ngeom;
+  for (int k = sl; k < nb * 3; k += HL) out[k] = s.u.k.xpos[k / 3][k % 3];
+  out += MAXBODY * 3;
+  for (int k = sl; k < nb * 9; k += HL) out[k] = s.u.k.xmat[k / 9][k % 9];
+  out += MAXBODY * 9;
+  for (int k = sl; k < ng * 3; k += HL) out[k] = s.u.k.gpos[k / 3][k % 3];
+  out += MAXGEOM * 3;
+  for (int k = sl; k < ng * 3; k += HL) out[k] = s.u.k.gax[k / 3][k % 3];
+  out += MAXGEOM * 3;
+  if (sl < 3) out[sl] = s.com[sl];
+}
+
 }  // namespace
 
 template <typename T>
@@ -1801,5 +1828,14 @@ template hipError_t launch_step<float>(const DevModel<float>*, int, const EnvBuf
 template hipError_t launch_step<double>(const DevModel<double>*, int, const EnvBuffers<double>&, const float*,
                                         const uint8_t*, const double*, const double*, const StepParams&, int,
                                         hipStream_t);
+
+template <typename T>
+hipError_t launch_kinematics(const DevModel<T>* dmodel, int nv, const T* qpos, T* out, hipStream_t stream) {
+  if (nv != 27) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((kin_kernel<T, 27>), dim3(1), dim3(WAVE), 0, stream, (MPtr<T>)dmodel, qpos, out);
+  return hipGetLastError();
+}
+template hipError_t launch_kinematics<float>(const DevModel<float>*, int, const float*, float*, hipStream_t);
+template hipError_t launch_kinematics<double>(const DevModel<double>*, int, const double*, double*, hipStream_t);
 
 }  // namespace hs

@@ -12,11 +12,14 @@ for this single-env surface, 'fp32'), ``max_newton``.
 """
 from __future__ import annotations
 
+from pathlib import Path
+
 import numpy as np
 
 from . import reward_functions as _rf
 from .batch import HsBatch
 from .model import HsModel
+from .render import Renderer, write_video
 from .spaces import Box, Env
 
 CLIP_OBSERVATION_VALUE = np.inf   # custom_env.py:9
@@ -158,8 +161,8 @@ class HumanoidEnv(Env):
                                      dtype=np.float64)
         self.action_space = Box(low=-ACTION_CLIP_VALUE, high=ACTION_CLIP_VALUE, shape=(self.model.nu,),
                                 dtype=np.float32)
-        if self.render_mode == "rgb_array":
-            raise NotImplementedError("rendering (mujoco.Renderer) is out of scope for this engine")
+        if self.render_mode == "rgb_array":   # custom_env.py:63-66
+            self.renderer = Renderer(self.model)
         self.reset()
 
     def _configure(self, max_newton):
@@ -180,7 +183,10 @@ class HumanoidEnv(Env):
         vel_noise = np.random.uniform(low=-0.01, high=0.01, size=self.model.nv)
         # the kernel applies pos_noise[2] *= 0.1, pos_noise[3:7] = 0 and the init pose (custom_env.py:105-117)
         self._batch.reset(qpos_noise=pos_noise[None], qvel_noise=vel_noise[None])
-        self.frames = []
+        self.frames = []          # custom_env.py:123-127
+        if self.renderer:
+            self.renderer.close()
+            self.renderer = None
         state = self._get_state()
         info = {
             'reward_components': {'forward': 0.0, 'standing': 0.0, 'healthy_pose': 0.0, 'alive': 0.0, 'total': 0.0},
@@ -222,6 +228,8 @@ class HumanoidEnv(Env):
             'terminated': terminated,
             'total_reward': self.total_reward,
         }
+        if self.render_mode == "rgb_array":   # custom_env.py:227-228
+            self.render()
         return state, reward, terminated, truncated, info
 
     def _get_state(self):
@@ -235,12 +243,40 @@ class HumanoidEnv(Env):
         return _rf.REWARD_FUNCTIONS[reward_type](self.data, reward_params)
 
     def render(self):
+        """custom_env.py:273-289: one 480x640 frame from the 'side' camera while the frame count is
+        below time x framerate (render.Renderer: host ray casting over GPU-computed poses)."""
         if self.render_mode != "rgb_array":
-            return None
-        raise NotImplementedError("rendering (mujoco.Renderer) is out of scope for this engine")
+            return
+        if self.renderer is None:
+            self.renderer = Renderer(self.model, height=480, width=640)
+        if len(self.frames) < self.data.time * self.framerate:
+            camera_id = self.model.camera('side').id
+            self.renderer.update_scene(self.data, camera=camera_id)
+            self.frames.append(self.renderer.render())
 
     def save_video(self, episode_num):
-        raise NotImplementedError("video recording (mediapy) is out of scope for this engine")
+        """custom_env.py:291-321, written as recordings/[run_name/]episode_<n>.gif: mediapy's h264
+        mp4 encoder (ffmpeg) is not in this image.  Returns the path (None without frames)."""
+        recordings_dir = Path("recordings")
+        if getattr(self, 'run_name', None):
+            recordings_dir = recordings_dir / self.run_name
+        recordings_dir.mkdir(parents=True, exist_ok=True)
+        video_path = recordings_dir / f"episode_{episode_num}.gif"
+        if video_path.exists():
+            video_path.unlink()
+        out = None
+        if len(self.frames) > 0:
+            out = str(write_video(str(video_path), self.frames, fps=self.framerate))
+        else:
+            print("No frames to save!")
+        self.frames = []
+        if self.renderer:
+            self.renderer.close()
+            self.renderer = None
+        return out
 
     def close(self):
+        if self.renderer:
+            self.renderer.close()
+            self.renderer = None
         self._batch.close()

@@ -60,6 +60,14 @@ class HsModel:
     def keyframe(self, name):
         return self.field("key_" + name)
 
+    def camera(self, name):
+        """MjModel.camera(name) subset (custom_env.py:286 reads ``.id``): MJCF cameras in id order."""
+        from .render import parse_cameras
+        for c in parse_cameras(self.path):
+            if c.name == name:
+                return c
+        raise KeyError(f"Invalid name '{name}'. Valid names: {[c.name for c in parse_cameras(self.path)]}")
+
     @property
     def qpos0(self):
         return self.field("qpos0")
