@@ -331,11 +331,21 @@ def main():
     if rank == 0:
         achieved = ALGO_BYTES_PER_ENV_STEP * n / (kernel_ms * 1e-3) / 1e9
         traffic = None
+        issue = None
         if os.path.exists(PROFILE_TRAFFIC):
             try:
                 tr = json.load(open(PROFILE_TRAFFIC))
                 if tr.get("n_envs") == n and tr.get("precision") == args.precision:
                     traffic = tr.get("hbm_bytes_per_launch")
+                    # VALU-issue view of the same kernel (what actually bounds it): VALU wave-instructions
+                    # per launch from the profile's PMC pass over the live launch time; a SIMD issues one
+                    # wave64 VALU op per 2 cycles at 2.4 GHz (MI355X_MICROARCH.md, wave scheduling)
+                    valu = tr.get("sq", {}).get("SQ_INSTS_VALU")
+                    if valu:
+                        peak = 256 * 4 * 2.4e9 / 2
+                        ach = valu / (kernel_ms * 1e-3)
+                        issue = {"valu_wave_instr_per_s": ach, "peak": peak, "frac": ach / peak,
+                                 "source": f"SQ_INSTS_VALU per launch from profiles ({tr.get('tag')})"}
             except Exception:
                 traffic = None
         out = {
@@ -360,8 +370,8 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "step_kernel<float,27>" if args.precision == "fp32" else "step_kernel<double,27>",
                          "kernel_ms_per_launch": kernel_ms, "envs_per_launch": n,
-                         "algo_bytes_per_env_step": ALGO_BYTES_PER_ENV_STEP,
-                         "note": "latency/VALU-bound kernel; HBM fraction reported per BASELINE.json; measured "
+                         "algo_bytes_per_env_step": ALGO_BYTES_PER_ENV_STEP, "valu_issue": issue,
+                         "note": "latency-bound kernel (see valu_issue and DESIGN.md 3.1); HBM fraction reported per BASELINE.json; measured "
                                  "with all envs in one launch per step (the headline value uses "
                                  f"{n_groups} stream groups; step time {step_ms:.3f} ms)"},
             "cpu_baseline": cpu_res,

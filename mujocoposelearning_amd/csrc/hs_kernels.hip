@@ -1079,7 +1079,7 @@ struct Stepper {
       if (r < nrow) {
         int kid = s.row_kid[r];
         int kind = rk_kind(kid), id = rk_id(kid);
-        T pos, margin, dA;
+        T pos, margin, dA, rscale = 1;
         CPtr<T> sr;
         CPtr<T> si;
         if (kind <= RK_JHI) {
@@ -1110,6 +1110,9 @@ struct Stepper {
           T tran = m->body_invweight_tran[bb & 0xff] + m->body_invweight_tran[(bb >> 8) & 0xff];
           T mu = s.con_mu[id];
           dA = kind == RK_CN ? tran : tran + mu * mu * tran;
+          // pyramidal edges share one R: Rpy = 2 mu^2 R_edge / impratio (impratio = 1, enforced by the
+          // compiler); pinned by the reference's recorded MuJoCo state, tests/test_reference_pin.py
+          if (kind != RK_CN) rscale = 2 * mu * mu;
           rd[q] = kid;
           rc[q] = kind == RK_CN ? T(0) : (((kind - RK_P0) & 1) ? -mu : mu);
           dense = s.con_m1[id] != 0u;
@@ -1125,7 +1128,7 @@ struct Stepper {
           K = -sr[0] / (dmax * dmax);
           B = -sr[1] / dmax;
         }
-        T R = fmax(T(1e-15), (1 - imp) * dA / imp);
+        T R = rscale * fmax(T(1e-15), (1 - imp) * dA / imp);
         D[q] = T(1) / R;
         s.row_D[r] = D[q];
         ar[q] = -B * row_Jx(m, s, rd[q], rc[q]) - K * imp * (pos - margin);

@@ -403,6 +403,7 @@ struct Compiler {
     };
     if (!is("integrator", "Euler")) { err = "only integrator=\"Euler\" is supported (reference: MuJoCo default)"; return false; }
     if (!is("cone", "pyramidal")) { err = "only cone=\"pyramidal\" is supported"; return false; }
+    if (k->get("impratio") && nums(k->get("impratio"))[0] != 1.0) { err = "only impratio=1 is supported"; return false; }
     if (!zero("noslip_iterations")) { err = "noslip solver not supported"; return false; }
     if (!zero("density") || !zero("viscosity")) { err = "fluid forces (density/viscosity) not supported"; return false; }
     for (auto& f : k->kids)

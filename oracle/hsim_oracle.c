@@ -9,7 +9,9 @@
  * third-party C library that is NOT present in this container, so every stage below is a
  * restatement of its published pipeline (engine_forward.c / engine_core_smooth.c /
  * engine_collision_*.c / engine_core_constraint.c / engine_solver.c semantics), and the
- * result is "parity unpinned" against real mj_step.
+ * result is "parity unpinned" against real mj_step except where the
+ * reference's one recorded MuJoCo state pins it (tests/test_reference_pin.py: the reset step with
+ * three floor contacts, which pins the pyramidal contact regulariser below).
  *
  * Solver note: MuJoCo's Newton solver minimises the convex primal
  *   0.5 (a - a0)' M (a - a0) + sum_active 0.5 D (J a - aref)^2
@@ -559,6 +561,16 @@ static void make_constraint(const OrcModel* m, OrcData* d) {
     }
     d->efc_KBIP[r][0] = K; d->efc_KBIP[r][1] = B; d->efc_KBIP[r][2] = imp; d->efc_KBIP[r][3] = impP;
     d->efc_R[r] = fmax(MINVAL, (1 - imp) * d->efc_diagApprox[r] / imp);
+    if (d->efc_type[r] == ORC_CONTACT_PYRAMIDAL) {
+      /* mj_makeImpedance, pyramidal cones: every edge of a contact gets Rpy = 2 mu^2 R / impratio, R the
+       * edge's own (diagApprox = tran (1 + mu^2)).  Pinned at mu = 1, impratio = 1 (the only case
+       * humanoid.xml produces: floor friction 1) by the reference's recorded MuJoCo state
+       * (trajectories/humanoid_trajectory.xml initial_pose; tests/test_reference_pin.py): with R
+       * scaled by 1 the inferred pre-step velocities leave the reset-noise box, only factors in
+       * [1.95, 2.15] keep all 27 inside it. */
+      double mu = d->contact[id].friction[0];
+      d->efc_R[r] *= 2 * mu * mu / m->impratio;
+    }
     d->efc_D[r] = 1 / d->efc_R[r];
   }
 }

@@ -177,6 +177,8 @@ def compile_mjcf(path):
         raise ValueError("only integrator='Euler' is supported")
     if o.get("cone", "pyramidal") != "pyramidal":
         raise ValueError("only cone='pyramidal' is supported")
+    if float(o.get("impratio", 1)) != 1:
+        raise ValueError("only impratio=1 is supported")
     if float(o.get("noslip_iterations", 0)) != 0:
         raise ValueError("noslip solver not supported")
     if float(o.get("density", 0)) != 0 or float(o.get("viscosity", 0)) != 0:

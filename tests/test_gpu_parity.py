@@ -259,8 +259,18 @@ def test_fp64_1000_substeps_within_chaos_envelope(tape):
     from oracle.oracle import Oracle
     q, v, rng = pr.initial(Oracle(XML), 0)
     tp = (np.zeros((pr.NSUB, 21)) if tape == "zeros" else rng.uniform(-1, 1, (pr.NSUB, 21))).astype(np.float32)
-    ref, env = pr.run_oracle(q, v, tp), pr.run_oracle(q, v, tp, perturb=1e-15)
+    ref = pr.run_oracle(q, v, tp)
+    envs = [pr.run_oracle(q, v, tp, perturb=p) for p in (1e-15, -1e-15)]
     gpu = pr.run_gpu(HsModel(XML), "fp64", q, v, tp)
+    checked = 0
     for k in range(len(ref)):
-        bound = max(1e-9, 20 * np.abs(env[k][0] - ref[k][0]).max())
+        env_k = max(np.abs(e[k][0] - ref[k][0]).max() for e in envs)
+        if env_k > 1e-4:
+            # the perturbed oracles themselves have decorrelated (the envelope jumps 20-1000x per
+            # 100 substeps from here): past the regime where a divergence can be compared at all
+            break
+        bound = max(1e-9, 20 * env_k)
         assert np.abs(gpu[k][0] - ref[k][0]).max() <= bound, (k, bound)
+        checked += 1
+    assert checked >= 5
+    assert all(np.isfinite(g[0]).all() for g in gpu)
