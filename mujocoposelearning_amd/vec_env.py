@@ -17,6 +17,8 @@ global MT19937 (the per-env HumanoidEnv keeps the exact numpy stream).
 """
 from __future__ import annotations
 
+import copy
+
 import numpy as np
 
 from . import reward_functions as _rf
@@ -58,12 +60,17 @@ class HumanoidVecEnv(_Base):
         self.reward_config = cfg.get("reward_config", {"type": "default"})
         rtype = self.reward_config.get("type", "default")
         rid = _rf.device_reward_id(rtype)
-        if rid is None:
-            raise NotImplementedError(f"reward '{rtype}' is a user callable; the batched env needs a device reward "
-                                      f"(use HumanoidEnv for host-side custom rewards)")
         params = self.reward_config.get("params")
-        self.batch.configure(frame_skip=self.frame_skip, duration=self.duration, max_steps=750, reward_id=rid,
-                             autoreset=1, max_newton=max_newton, init_height=1.282, noise_scale=0.01,
+        # user-registered reward callables run on the host over per-env data views (slow, correct):
+        # the kernel then steps without a reward and without auto-reset, so the callable sees the
+        # pre-reset state; finished envs are reset by a second (masked) launch
+        self._host_reward = None if rid is not None else _rf.REWARD_FUNCTIONS[rtype]
+        # each SubprocVecEnv worker holds its own copy of reward_config (the callables may mutate params)
+        self._host_params = ([copy.deepcopy(params) for _ in range(n_envs)] if self._host_reward is not None
+                             else None)
+        self.batch.configure(frame_skip=self.frame_skip, duration=self.duration, max_steps=750,
+                             reward_id=rid if rid is not None else -1, autoreset=1 if rid is not None else 0,
+                             max_newton=max_newton, init_height=1.282, noise_scale=0.01,
                              kneel_params=params if rid == 1 and params else None)
         obs_space = Box(low=-np.inf, high=np.inf, shape=(self.batch.obs_dim,), dtype=np.float64)
         act_space = Box(low=-1, high=1, shape=(self.model.nu,), dtype=np.float32)
@@ -99,7 +106,30 @@ class HumanoidVecEnv(_Base):
         """actions: [N, nu] float32 tensor on the env's GPU (clipped to [-1, 1] by the caller, as
         SB3 does).  Returns device views (obs, reward, terminated, truncated) valid until the next
         call; ``self.batch.terminal_obs`` holds pre-reset obs of envs that just finished."""
+        if self._host_reward is not None:
+            return self._step_host_reward(actions)
         return self.batch.step(actions)
+
+    def _step_host_reward(self, actions):
+        """custom_env.py:201-211 with a host reward callable: step (no auto-reset), evaluate
+        ``REWARD_FUNCTIONS[type](data_i, params_i)`` per env on the pre-reset state (0 when
+        truncated), then reset the finished envs (SB3 auto-reset) with one masked launch."""
+        import torch
+        b = self.batch
+        obs, rew, term, trunc = b.step(actions)
+        views = _HostViews(b, self.model)
+        tr = trunc.cpu().numpy().astype(bool)
+        r = np.zeros(self.num_envs)
+        for i in range(self.num_envs):
+            if not tr[i]:
+                r[i] = float(self._host_reward(views.env(i), self._host_params[i] if self._host_params else None))
+        rew.copy_(torch.as_tensor(r, device=rew.device, dtype=rew.dtype))
+        b.total_reward.add_(rew)
+        done = (term != 0) | (trunc != 0)
+        if bool(done.any()):
+            b.terminal_obs[done] = obs[done]
+            b.reset(mask=done.to(torch.uint8))
+        return b.obs, rew, term, trunc
 
     # ---------------------------------------------------------------- SB3 VecEnv API
     def reset(self):
@@ -112,7 +142,8 @@ class HumanoidVecEnv(_Base):
     def step_wait(self):
         import torch
         a = torch.as_tensor(self._actions, device=self.batch.device)
-        obs, rew, term, trunc = self.batch.step(a)
+        obs, rew, term, trunc = self.step_tensors(a)
+        rew = rew.clone()
         obs_np = obs.double().cpu().numpy()
         rew_np = rew.double().cpu().numpy()
         term_np = term.cpu().numpy().astype(bool)
@@ -169,3 +200,34 @@ class HumanoidVecEnv(_Base):
         if isinstance(indices, int):
             return [indices]
         return indices
+
+
+class _HostViews:
+    """Host copies of one step's batched state (one device->host transfer per field) with per-env
+    MjData-like views for host reward callables (the fields reward_functions.py reads)."""
+
+    def __init__(self, batch, model):
+        self.m = model
+        self.qpos = batch.qpos.double().cpu().numpy()
+        self.qvel = batch.qvel.double().cpu().numpy()
+        self.ctrl = batch.ctrl.double().cpu().numpy()
+        self.time = batch.time.double().cpu().numpy()
+        self.obs = batch.obs.double().cpu().numpy()
+        self.com = batch.aux[:, 32:35].double().cpu().numpy()
+        fs = batch.full_state
+        self.cfrc = batch.cfrc_ext.double().cpu().numpy() if fs else None
+        self.linv = batch.subtree_linvel.double().cpu().numpy() if fs else None
+
+    def env(self, i):
+        from types import SimpleNamespace
+        m = self.m
+        o2 = (m.nq - 2) + m.nv
+        o3, o4 = o2 + 10 * m.nbody, o2 + 16 * m.nbody
+        com = np.full((m.nbody, 3), np.nan)
+        com[0] = com[1] = self.com[i]
+        return SimpleNamespace(
+            qpos=self.qpos[i], qvel=self.qvel[i], ctrl=self.ctrl[i], time=float(self.time[i]),
+            cinert=self.obs[i, o2:o3].reshape(m.nbody, 10), cvel=self.obs[i, o3:o4].reshape(m.nbody, 6),
+            qfrc_actuator=self.obs[i, o4:o4 + m.nv], subtree_com=com,
+            cfrc_ext=self.cfrc[i] if self.cfrc is not None else np.zeros((m.nbody, 6)),
+            subtree_linvel=self.linv[i] if self.linv is not None else np.zeros((m.nbody, 3)))

@@ -109,7 +109,9 @@ def build(force=False):
     src = os.path.join(HERE, "hsim_oracle.c")
     if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
         os.makedirs(os.path.dirname(LIB_PATH), exist_ok=True)
-        subprocess.check_call(["gcc", "-O2", "-fPIC", "-shared", "-std=c11", "-o", LIB_PATH, src, "-lm"])
+        tmp = f"{LIB_PATH}.{os.getpid()}.tmp"     # atomic: parallel test workers may build at once
+        subprocess.check_call(["gcc", "-O2", "-fPIC", "-shared", "-std=c11", "-o", tmp, src, "-lm"])
+        os.replace(tmp, LIB_PATH)
     return LIB_PATH
 
 
