@@ -191,8 +191,20 @@ class HumanoidVecEnv(_Base):
     def env_is_wrapped(self, wrapper_class, indices=None):
         return [False for _ in self._indices(indices)]
 
-    def get_images(self):
-        raise NotImplementedError("rendering is out of scope for this engine")
+    def get_images(self, indices=None, camera="side", height=480, width=640):
+        """SB3 VecEnv.get_images: one rgb frame per env (render.Renderer over GPU kinematics;
+        host ray casting, ~0.15 s per 480x640 frame, so meant for a few envs)."""
+        from types import SimpleNamespace
+
+        from .render import Renderer
+        if getattr(self, "_renderer", None) is None or (self._renderer.height, self._renderer.width) != (height, width):
+            self._renderer = Renderer(self.model, height=height, width=width)
+        out = []
+        for i in self._indices(indices):
+            self._renderer.update_scene(SimpleNamespace(_env=SimpleNamespace(_batch=self.batch, _idx=int(i))),
+                                        camera=camera)
+            out.append(self._renderer.render())
+        return out
 
     def _indices(self, indices):
         if indices is None:

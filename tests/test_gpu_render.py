@@ -82,3 +82,18 @@ def test_env_rgb_array_frames_and_video(tmp_path, monkeypatch):
     assert Image.open(p).n_frames == n
     assert env.frames == [] and env.renderer is None
     env.close()
+
+
+def test_vecenv_get_images(model):
+    from mujocoposelearning_amd.vec_env import HumanoidVecEnv
+    env = HumanoidVecEnv({"model_path": XML, "duration": 10.0, "reward_config": {"type": "stand"}, "frame_skip": 3},
+                         n_envs=4, model=model, seed=1)
+    env.reset()
+    rng = np.random.default_rng(1)
+    for _ in range(20):
+        env.step_async(rng.uniform(-1, 1, (4, 21)).astype(np.float32))
+        env.step_wait()
+    imgs = env.get_images(indices=[0, 3], height=96, width=128)
+    assert len(imgs) == 2 and imgs[0].shape == (96, 128, 3) and imgs[0].dtype == np.uint8
+    assert np.abs(imgs[0].astype(int) - imgs[1].astype(int)).sum() > 0     # different envs, different poses
+    env.close()
