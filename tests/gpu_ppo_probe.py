@@ -1,0 +1,41 @@
+"""PPO timing probe (bench train-leg workload): rollout vs update time per iteration."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+from mujocoposelearning_amd.model import HsModel  # noqa: E402
+from mujocoposelearning_amd.ppo import PPO  # noqa: E402
+from mujocoposelearning_amd.vec_env import HumanoidVecEnv  # noqa: E402
+
+XML = os.path.join(ROOT, "tests", "golden", "humanoid.xml")
+
+
+def run(n=4096, iters=3):
+    env = HumanoidVecEnv({"model_path": XML, "duration": 10.0, "reward_config": {"type": "stand"}, "frame_skip": 3},
+                         n_envs=n, model=HsModel(XML), seed=0)
+    ppo = PPO(env, n_steps=32, batch_size=32768, n_epochs=4, seed=0,
+              policy_kwargs={"activation_fn": "ReLU", "net_arch": {"pi": [256, 256], "vf": [256, 256]}})
+    tr, tu = [], []
+    for k in range(iters + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        adv, ret = ppo.collect_rollouts()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        ppo.train(adv, ret)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        if k:
+            tr.append(t1 - t0)
+            tu.append(t2 - t1)
+    print(f"rollout {1e3 * sum(tr) / iters:.1f} ms, update {1e3 * sum(tu) / iters:.1f} ms "
+          f"({1e3 * sum(tu) / iters / 16:.2f} ms per minibatch step)", flush=True)
+    env.close()
+
+
+if __name__ == "__main__":
+    run()
