@@ -20,6 +20,11 @@
  *   hs_last_error        <- mujoco's error callback / MjModel load error string
  *   hs_gae               <- SB3 RolloutBuffer.compute_returns_and_advantage (stable_baselines3 2.3.2
  *                           common/buffers.py), run by PPO.learn once per rollout (train_sb3.py:229)
+ *   hs_ppo_act           <- SB3 PPO.collect_rollouts per step (on_policy_algorithm.py, 2.3.2): the
+ *                           DiagGaussian sample + log_prob of ActorCriticPolicy.forward, np.clip of
+ *                           the actions, RolloutBuffer.add of actions/values/log_probs/episode_starts
+ *   hs_ppo_post          <- the same loop after env.step: TimeLimit.truncated bootstrap of the reward,
+ *                           dones, episode returns, new episode_starts, next obs into the buffer
  *
  * Conventions: status int (0 ok, <0 error, message via hs_last_error(), thread-local); the
  * model is immutable and shareable; a batch owns (or is bound to) device buffers; every call
@@ -139,6 +144,26 @@ int hs_synchronize(hs_batch* b);
 int hs_gae(const float* rewards, const float* values, const float* episode_starts, const float* last_values,
            const float* last_dones, float* advantages, float* returns, int T, int N, float gamma, float gae_lambda,
            void* stream);
+/* One PPO rollout step's policy sampling and buffer writes over N envs (A <= 32 actions):
+ * mean [N][mean_ld] (first A columns), value [N] at stride value_ld, log_std [A], episode_start
+ * [N] (all float32 device memory).  actions = mean + exp(log_std) * z with z ~ N(0, 1) from the
+ * counter-based Philox4x32-10 stream (seed, counter; z = 0 when deterministic != 0); writes
+ * actions [N][A] (unclipped, the buffer copy), actions_clipped [N][A] (clip to [-1, 1], what the
+ * env steps with), log_prob [N], values [N] and episode_starts_out [N].  Asynchronous on `stream`. */
+int hs_ppo_act(const float* mean, int mean_ld, const float* value, int value_ld, const float* log_std,
+               const float* episode_start, uint64_t seed, uint64_t counter, int deterministic, float* actions,
+               float* actions_clipped, float* log_prob, float* values, float* episode_starts_out, int N, int A,
+               void* stream);
+/* The rest of the PPO rollout step after the env step, over N envs: reward [N] float32,
+ * terminated / truncated [N] uint8, terminal_value [N] = V(terminal obs) float32.  Writes
+ * reward_out = reward + gamma * terminal_value where truncated && !terminated (else reward),
+ * done_out = terminated || truncated (uint8), ep_acc += reward (float64, zeroed where done, after
+ * ep_return_out = the accumulated value is written) and episode_start = done (float32).  Copies
+ * obs_floats float32 from obs to obs_out (the next rollout-buffer slot; NULL obs skips it).
+ * Asynchronous on `stream`. */
+int hs_ppo_post(const float* reward, const uint8_t* terminated, const uint8_t* truncated, const float* terminal_value,
+                float gamma, const float* obs, float* obs_out, uint64_t obs_floats, float* reward_out,
+                uint8_t* done_out, double* ep_acc, double* ep_return_out, float* episode_start, int N, void* stream);
 const char* hs_last_error(void);
 const char* hs_version(void);
 

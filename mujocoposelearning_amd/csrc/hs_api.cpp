@@ -405,6 +405,42 @@ int hs_get_debug(hs_batch* b, double* out, int n) {
   return 0;
 }
 
+int hs_ppo_act(const float* mean, int mean_ld, const float* value, int value_ld, const float* log_std,
+               const float* episode_start, uint64_t seed, uint64_t counter, int deterministic, float* actions,
+               float* actions_clipped, float* log_prob, float* values, float* episode_starts_out, int N, int A,
+               void* stream) {
+  if (N < 0 || A < 1 || A > 32) return fail("hs_ppo_act: need N >= 0 and 1 <= A <= 32");
+  if (mean_ld < A || value_ld < 1) return fail("hs_ppo_act: bad leading dimension");
+  if (N == 0) return 0;
+  if (!mean || !value || !log_std || !episode_start || !actions || !actions_clipped || !log_prob || !values ||
+      !episode_starts_out)
+    return fail("hs_ppo_act: null buffer");
+  return hip_ok(hs::launch_ppo_act(mean, mean_ld, value, value_ld, log_std, episode_start, seed, counter, deterministic,
+                                   actions, actions_clipped, log_prob, values, episode_starts_out, N, A,
+                                   (hipStream_t)stream),
+                "ppo_act_kernel")
+             ? 0
+             : -1;
+}
+
+int hs_ppo_post(const float* reward, const uint8_t* terminated, const uint8_t* truncated, const float* terminal_value,
+                float gamma, const float* obs, float* obs_out, uint64_t obs_floats, float* reward_out,
+                uint8_t* done_out, double* ep_acc, double* ep_return_out, float* episode_start, int N, void* stream) {
+  if (N < 0) return fail("hs_ppo_post: negative size");
+  if (N == 0) return 0;
+  if (!reward || !terminated || !truncated || !terminal_value || !reward_out || !done_out || !ep_acc ||
+      !ep_return_out || !episode_start)
+    return fail("hs_ppo_post: null buffer");
+  if (!obs) obs_floats = 0;
+  if (obs_floats && !obs_out) return fail("hs_ppo_post: null obs_out");
+  return hip_ok(hs::launch_ppo_post(reward, terminated, truncated, terminal_value, gamma, obs, obs_out,
+                                    (size_t)obs_floats, reward_out, done_out, ep_acc, ep_return_out, episode_start, N,
+                                    (hipStream_t)stream),
+                "ppo_post_kernel")
+             ? 0
+             : -1;
+}
+
 int hs_gae(const float* rewards, const float* values, const float* episode_starts, const float* last_values,
            const float* last_dones, float* advantages, float* returns, int T, int N, float gamma, float gae_lambda,
            void* stream) {

@@ -66,6 +66,15 @@ constexpr int KINDIM = MAXBODY * 12 + MAXGEOM * 6 + 3;
 template <typename T>
 hipError_t launch_kinematics(const DevModel<T>* dmodel, int nv, const T* qpos, T* out, hipStream_t stream);
 
+// PPO rollout bookkeeping around the policy GEMMs and the env step (ppo.hip)
+hipError_t launch_ppo_act(const float* mean, int mean_ld, const float* value, int value_ld, const float* log_std,
+                          const float* episode_start, uint64_t seed, uint64_t counter, int deterministic, float* act,
+                          float* act_clip, float* logp, float* val, float* start_out, int N, int A,
+                          hipStream_t stream);
+hipError_t launch_ppo_post(const float* reward, const uint8_t* terminated, const uint8_t* truncated,
+                           const float* terminal_value, float gamma, const float* obs, float* obs_out, size_t obs_floats,
+                           float* reward_out, uint8_t* done_out, double* ep_acc, double* ep_return_out,
+                           float* episode_start, int N, hipStream_t stream);
 // GAE reverse scan over [T][N] float32 rollout arrays (gae.hip)
 hipError_t launch_gae(const float* rew, const float* val, const float* start, const float* last_val,
                       const float* last_done, float* adv, float* ret, int T, int N, float gamma, float lam,

@@ -1,0 +1,168 @@
+// hsim PPO rollout kernels for gfx950 (MI355X).  PRODUCT CODE.
+//
+// The per-step bookkeeping of SB3 2.3.2 PPO.collect_rollouts (stable_baselines3/common/
+// on_policy_algorithm.py), which the reference's PPO.learn runs n_steps times per rollout
+// (train_sb3.py:229), as two launches per env step around the policy GEMMs and the env kernel:
+//
+//   ppo_act_kernel   ActorCriticPolicy.forward's DiagGaussianDistribution.sample() + log_prob()
+//                    (common/distributions.py) on the policy heads, the clip of the actions to
+//                    the action space (on_policy_algorithm.py: np.clip(actions, low, high)) and
+//                    the rollout-buffer writes of step t (actions, values, log_probs,
+//                    episode_starts; common/buffers.py RolloutBuffer.add)
+//   ppo_post_kernel  the step's reward bookkeeping: time-limit bootstrap
+//                    r += gamma V(terminal_obs) for envs with TimeLimit.truncated
+//                    (on_policy_algorithm.py: infos[idx]["TimeLimit.truncated"]), dones,
+//                    episode-return accumulation, the new episode_starts, and the copy of the
+//                    next observation into the rollout buffer's slot t+1
+//
+// Both are HBM/launch-bound elementwise work (no GEMM shape), so they are laid out for
+// coalescing: ppo_act maps a half-wave (32 lanes) onto one env's action vector (A <= 32), so
+// a wave touches two consecutive 84 B head rows and the log-prob sum is a 5-step DPP/swizzle
+// reduction within the half-wave; ppo_post moves the [N][D] observation copy as 16 B vectors.
+//
+// Noise: Philox4x32-10 (Salmon et al., SC'11) keyed by the 64-bit seed, counter =
+// (env * 32 + action index, rollout-step counter), and a Box-Muller transform of two of its
+// words: a counter-based stream, so every (env, step, action) draw is independent of the
+// launch shape and reproducible from (seed, counter).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace hs {
+namespace {
+
+struct U4 {
+  uint32_t x, y, z, w;
+};
+
+__device__ inline U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
+  constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; r++) {
+    const uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
+    const uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
+    c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += W0;
+    k1 += W1;
+  }
+  return c;
+}
+
+// standard normal from two uniform words (Box-Muller, u1 in (0, 1])
+__device__ inline float box_muller(uint32_t a, uint32_t b) {
+  const float u1 = ((float)(a >> 8) + 1.0f) * (1.0f / 16777216.0f);
+  const float u2 = (float)(b >> 8) * (1.0f / 16777216.0f);
+  return sqrtf(-2.0f * __logf(u1)) * __cosf(6.283185307179586f * u2);
+}
+
+// sum over the 32 lanes of a half-wave (xor butterfly stays inside the half)
+__device__ inline float half_sum(float v) {
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 32);
+  return v;
+}
+
+__global__ __launch_bounds__(256) void ppo_act_kernel(const float* __restrict__ mean, int mean_ld,
+                                                      const float* __restrict__ value, int value_ld,
+                                                      const float* __restrict__ log_std,
+                                                      const float* __restrict__ episode_start, uint32_t k0,
+                                                      uint32_t k1, uint32_t c0, uint32_t c1, int deterministic,
+                                                      float* __restrict__ act, float* __restrict__ act_clip,
+                                                      float* __restrict__ logp, float* __restrict__ val,
+                                                      float* __restrict__ start_out, int N, int A) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = gid >> 5, j = gid & 31;
+  if (n >= N) return;                         // whole half-waves exit together (N*32 lanes)
+  float term = 0.f;
+  if (j < A) {
+    const float m = mean[(size_t)n * mean_ld + j];
+    const float ls = log_std[j];
+    float z = 0.f;
+    if (!deterministic) {
+      const uint32_t id = (uint32_t)gid;      // env * 32 + action index
+      const U4 r = philox4x32_10(U4{id, (uint32_t)(n >> 27), c0, c1}, k0, k1);
+      z = box_muller(r.x, r.y);
+    }
+    const float a = m + __expf(ls) * z;
+    const size_t i = (size_t)n * A + j;
+    act[i] = a;
+    act_clip[i] = fminf(fmaxf(a, -1.0f), 1.0f);
+    // DiagGaussian log_prob: sum_j -((a-m)^2 / (2 sigma^2)) - log sigma - log(sqrt(2 pi))
+    term = -0.5f * z * z - ls - 0.91893853320467274f;
+  }
+  const float lp = half_sum(term);
+  if (j == 0) {
+    logp[n] = lp;
+    val[n] = value[(size_t)n * value_ld];
+    start_out[n] = episode_start[n];
+  }
+}
+
+__global__ __launch_bounds__(256) void ppo_post_kernel(const float* __restrict__ reward,
+                                                       const uint8_t* __restrict__ terminated,
+                                                       const uint8_t* __restrict__ truncated,
+                                                       const float* __restrict__ terminal_value, float gamma,
+                                                       const float* __restrict__ obs, float* __restrict__ obs_out,
+                                                       size_t obs_n, int vec4, float* __restrict__ reward_out,
+                                                       uint8_t* __restrict__ done_out, double* __restrict__ ep_acc,
+                                                       double* __restrict__ ep_return_out,
+                                                       float* __restrict__ episode_start, int N) {
+  const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  if (vec4) {   // 16 B-aligned pointers, obs_n = floats / 4
+    const float4* __restrict__ src = reinterpret_cast<const float4*>(obs);
+    float4* __restrict__ dst = reinterpret_cast<float4*>(obs_out);
+    for (size_t i = gid; i < obs_n; i += stride) dst[i] = src[i];
+  } else {
+    for (size_t i = gid; i < obs_n; i += stride) obs_out[i] = obs[i];
+  }
+  if (gid < (size_t)N) {
+    const bool term = terminated[gid] != 0, trunc = truncated[gid] != 0;
+    const float r = reward[gid];
+    // TimeLimit.truncated = truncated and not terminated: bootstrap from V(terminal obs)
+    reward_out[gid] = (trunc && !term) ? r + gamma * terminal_value[gid] : r;
+    const bool done = term || trunc;
+    const double acc = ep_acc[gid] + (double)r;
+    done_out[gid] = done;
+    ep_return_out[gid] = acc;
+    ep_acc[gid] = done ? 0.0 : acc;
+    episode_start[gid] = done ? 1.0f : 0.0f;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_ppo_act(const float* mean, int mean_ld, const float* value, int value_ld, const float* log_std,
+                          const float* episode_start, uint64_t seed, uint64_t counter, int deterministic, float* act,
+                          float* act_clip, float* logp, float* val, float* start_out, int N, int A,
+                          hipStream_t stream) {
+  if (N <= 0) return hipSuccess;
+  const size_t threads = (size_t)N * 32;
+  const int block = 256;
+  const dim3 grid((unsigned)((threads + block - 1) / block));
+  hipLaunchKernelGGL(ppo_act_kernel, grid, dim3(block), 0, stream, mean, mean_ld, value, value_ld, log_std,
+                     episode_start, (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)counter,
+                     (uint32_t)(counter >> 32), deterministic, act, act_clip, logp, val, start_out, N, A);
+  return hipGetLastError();
+}
+
+hipError_t launch_ppo_post(const float* reward, const uint8_t* terminated, const uint8_t* truncated,
+                           const float* terminal_value, float gamma, const float* obs, float* obs_out, size_t obs_floats,
+                           float* reward_out, uint8_t* done_out, double* ep_acc, double* ep_return_out,
+                           float* episode_start, int N, hipStream_t stream) {
+  if (N <= 0) return hipSuccess;
+  const int vec4 = obs_floats % 4 == 0 && ((uintptr_t)obs | (uintptr_t)obs_out) % 16 == 0;
+  const size_t obs_n = vec4 ? obs_floats / 4 : obs_floats;
+  const size_t work = obs_n > (size_t)N ? obs_n : (size_t)N;
+  const int block = 256;
+  // one 16 B vector per lane per pass, at most 8 passes' worth of workgroups resident
+  size_t blocks = (work + block - 1) / block;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks * block < (size_t)N) blocks = ((size_t)N + block - 1) / block;
+  hipLaunchKernelGGL(ppo_post_kernel, dim3((unsigned)blocks), dim3(block), 0, stream, reward, terminated, truncated,
+                     terminal_value, gamma, obs, obs_out, obs_n, vec4, reward_out, done_out, ep_acc, ep_return_out,
+                     episode_start, N);
+  return hipGetLastError();
+}
+
+}  // namespace hs

@@ -22,10 +22,47 @@ import torch
 import torch.nn as nn
 
 
+_SPLITK_ROWS = 2048      # rows per split-K slice of a weight gradient
+SPLIT_K = True           # module switch (A/B probes)
+
+
+class _SplitKLinearFn(torch.autograd.Function):
+    """y = x W^T + b whose weight gradient is computed as S batched [out x rows] x [rows x in]
+    products summed over S, instead of one GEMM with a K = batch-size reduction.  The library's
+    kernel for a 256 x 32768 x 352 weight gradient runs at a few TFLOP/s (one long reduction on few
+    tiles); split into 16 slices it fills the chip (tests/gpu_mlp_probe.py: minibatch fwd+bwd
+    1.45 -> 0.97 ms at 32768 samples)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, s):
+        ctx.save_for_backward(x, w)
+        ctx.s = s
+        return torch.addmm(b, x, w.t())
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        s = ctx.s
+        gx = g @ w if ctx.needs_input_grad[0] else None
+        gw = torch.bmm(g.view(s, -1, g.shape[1]).transpose(1, 2), x.view(s, -1, x.shape[1])).sum(0)
+        return gx, gw, g.sum(0), None
+
+
+class Linear(nn.Linear):
+    """nn.Linear (same parameters and state_dict keys, so SB3 checkpoints map 1:1) with split-K
+    weight gradients for large device minibatches; small or CPU batches take nn.Linear's path."""
+
+    def forward(self, x):
+        n = x.shape[0] if x.dim() == 2 else 0
+        if SPLIT_K and x.is_cuda and torch.is_grad_enabled() and n >= 2 * _SPLITK_ROWS and n % _SPLITK_ROWS == 0:
+            return _SplitKLinearFn.apply(x, self.weight, self.bias, n // _SPLITK_ROWS)
+        return super().forward(x)
+
+
 def _mlp(inp, sizes, act=nn.ReLU):
     layers, d = [], inp
     for s in sizes:
-        layers += [nn.Linear(d, s), act()]
+        layers += [Linear(d, s), act()]
         d = s
     return nn.Sequential(*layers), d
 
@@ -36,9 +73,10 @@ class ActorCritic(nn.Module):
         vf = pi if vf is None else vf
         self.pi_net, dp = _mlp(obs_dim, pi, activation)
         self.vf_net, dv = _mlp(obs_dim, vf, activation)
-        self.action_net = nn.Linear(dp, act_dim)
-        self.value_net = nn.Linear(dv, 1)
+        self.action_net = Linear(dp, act_dim)
+        self.value_net = Linear(dv, 1)
         self.log_std = nn.Parameter(torch.full((act_dim,), float(log_std_init)))
+        self._packed = None      # pack_heads() cache, rebuilt at the start of every rollout
         for mod, gain in ((self.pi_net, math.sqrt(2)), (self.vf_net, math.sqrt(2)), (self.action_net, 0.01),
                           (self.value_net, 1.0)):
             for m in mod.modules() if isinstance(mod, nn.Sequential) else [mod]:
@@ -68,6 +106,55 @@ class ActorCritic(nn.Module):
     @torch.no_grad()
     def value(self, obs):
         return self.value_net(self.vf_net(obs)).squeeze(-1)
+
+    # -- rollout-time forward (no autograd) -------------------------------------------------------
+    def _hidden(self, net):
+        return [m for m in net if isinstance(m, nn.Linear)]
+
+    @torch.no_grad()
+    def pack_heads(self):
+        """Stack the pi and vf MLPs into one chain of batched GEMMs for the rollout forward
+        (weights are constant over a rollout, so this runs once per collect_rollouts): layer 1 is
+        one [obs_dim x (h_pi + h_vf)] GEMM (both nets read the same obs), deeper layers one
+        2-batch GEMM each, and the heads one 2-batch GEMM whose vf half carries the value column
+        in column 0 of an A-wide block.  Needs equal pi/vf widths and ReLU; otherwise None and
+        heads() runs the two nets."""
+        lp, lv = self._hidden(self.pi_net), self._hidden(self.vf_net)
+        acts = {type(m) for m in list(self.pi_net) + list(self.vf_net) if not isinstance(m, nn.Linear)}
+        same = len(lp) == len(lv) >= 1 and all(a.weight.shape == b.weight.shape for a, b in zip(lp, lv))
+        if not same or acts != {nn.ReLU}:
+            self._packed = None
+            return None
+        A, H = self.action_net.out_features, lp[-1].out_features
+        w1 = torch.cat([lp[0].weight, lv[0].weight]).t().contiguous()
+        b1 = torch.cat([lp[0].bias, lv[0].bias])
+        mid = [(torch.stack([a.weight.t(), b.weight.t()]).contiguous(), torch.stack([a.bias, b.bias])[:, None, :])
+               for a, b in zip(lp[1:], lv[1:])]
+        w3 = torch.zeros(2, H, A, device=w1.device, dtype=w1.dtype)
+        w3[0] = self.action_net.weight.t()
+        w3[1, :, 0] = self.value_net.weight[0]
+        b3 = torch.zeros(2, 1, A, device=w1.device, dtype=w1.dtype)
+        b3[0, 0] = self.action_net.bias
+        b3[1, 0, 0] = self.value_net.bias[0]
+        self._packed = (w1, b1, mid, w3, b3)
+        return self._packed
+
+    @torch.no_grad()
+    def heads(self, obs):
+        """Rollout forward: (mean [N, A] view, value [N] strided view) from the packed GEMM chain
+        (pack_heads) or, for unequal pi/vf nets, the two MLPs."""
+        pk = getattr(self, "_packed", None)
+        if pk is None:
+            mean, value = self(obs)
+            return mean, value
+        w1, b1, mid, w3, b3 = pk
+        n = obs.shape[0]
+        h = torch.addmm(b1, obs, w1).relu_()                      # [N, 2H]
+        h = h.view(n, 2, -1).transpose(0, 1)                      # [2, N, H] (strided)
+        for w, b in mid:
+            h = torch.baddbmm(b, h, w).relu_()
+        out = torch.baddbmm(b3, h, w3)                            # [2, N, A]
+        return out[0], out[1, :, 0]
 
 
 def gae(rewards, values, dones, last_values, last_dones, gamma, lam):
@@ -110,6 +197,37 @@ def gae_device(rewards, values, dones, last_values, last_dones, gamma, lam):
     return adv, ret
 
 
+def ppo_act(mean, value, log_std, episode_start, seed, counter, deterministic, act_out, act_clip_out, logp_out,
+            val_out, start_out, stream=None):
+    """hs_ppo_act on device tensors (ppo.hip): Gaussian sample + log-prob + clip + buffer writes."""
+    from . import _lib
+    N, A = act_out.shape
+    assert mean.stride(1) == 1 and mean.shape == (N, A) and value.shape == (N,), (mean.shape, value.shape)
+    for t in (log_std, episode_start, act_out, act_clip_out, logp_out, val_out, start_out):
+        assert t.dtype == torch.float32 and t.is_contiguous()
+    st = torch.cuda.current_stream(mean.device).cuda_stream if stream is None else stream
+    _lib.check(_lib.lib().hs_ppo_act(mean.data_ptr(), mean.stride(0), value.data_ptr(), value.stride(0),
+                                     log_std.data_ptr(), episode_start.data_ptr(), int(seed) & (2 ** 64 - 1),
+                                     int(counter), int(bool(deterministic)), act_out.data_ptr(),
+                                     act_clip_out.data_ptr(), logp_out.data_ptr(), val_out.data_ptr(),
+                                     start_out.data_ptr(), N, A, st))
+
+
+def ppo_post(reward, terminated, truncated, terminal_value, gamma, obs, obs_out, reward_out, done_out, ep_acc,
+             ep_return_out, episode_start, stream=None):
+    """hs_ppo_post on device tensors (ppo.hip): reward bootstrap, dones, returns, next obs copy."""
+    from . import _lib
+    N = reward.shape[0]
+    assert terminated.dtype == torch.uint8 and truncated.dtype == torch.uint8 and done_out.dtype == torch.bool
+    assert ep_acc.dtype == torch.float64 and ep_return_out.dtype == torch.float64
+    assert obs.is_contiguous() and obs_out.is_contiguous() and obs.numel() == obs_out.numel()
+    st = torch.cuda.current_stream(reward.device).cuda_stream if stream is None else stream
+    _lib.check(_lib.lib().hs_ppo_post(reward.data_ptr(), terminated.data_ptr(), truncated.data_ptr(),
+                                      terminal_value.data_ptr(), float(gamma), obs.data_ptr(), obs_out.data_ptr(),
+                                      obs.numel(), reward_out.data_ptr(), done_out.data_ptr(), ep_acc.data_ptr(),
+                                      ep_return_out.data_ptr(), episode_start.data_ptr(), N, st))
+
+
 class PPO:
     """PPO over a device vec-env (HumanoidVecEnv's fast path).
 
@@ -141,7 +259,9 @@ class PPO:
         self.policy = ActorCritic(env.obs_dim, env.act_dim, net["pi"], net["vf"], act,
                                   pk.get("log_std_init", 0.0)).to(self.device)
         torch.manual_seed(seed + 7919 * rank)   # per-rank exploration noise / minibatch order
-        self.opt = torch.optim.Adam(self.policy.parameters(), lr=learning_rate, eps=1e-5)
+        # fused (single-kernel) Adam on a device; the same update rule and state_dict as foreach Adam
+        self.opt = torch.optim.Adam(self.policy.parameters(), lr=learning_rate, eps=1e-5,
+                                    fused=True if self.device.type == "cuda" else None)
         self.n_steps, self.batch_size, self.n_epochs = n_steps, batch_size, n_epochs
         self.gamma, self.gae_lambda, self.clip_range = gamma, gae_lambda, clip_range
         self.ent_coef, self.vf_coef, self.max_grad_norm = ent_coef, vf_coef, max_grad_norm
@@ -159,9 +279,43 @@ class PPO:
         self.ep_returns = []
         self.ep_acc = torch.zeros(N, dtype=torch.float64, device=dev)
         self.flat = [p for p in self.policy.parameters()]
+        # device rollout: the clipped actions the env steps with, and the Philox noise stream
+        self._act_clip = torch.zeros(N, A, dtype=f, device=dev)
+        self._noise_seed = (int(seed) + 7919 * rank) * 0x9E3779B97F4A7C15 % 2 ** 64
+        self._noise_counter = 0
         self.logger = {}
 
     def collect_rollouts(self):
+        if self.device.type == "cuda":
+            return self._collect_rollouts_device()
+        return self._collect_rollouts_torch()
+
+    def _collect_rollouts_device(self):
+        """collect_rollouts on the GPU: per env step the packed policy GEMM chain, one hs_ppo_act
+        launch (sample, log-prob, clip, buffer writes), the env kernel, the value of the terminal
+        obs (three GEMMs) and one hs_ppo_post launch (bootstrap, dones, returns, obs -> slot t+1).
+        No host synchronisation inside the loop."""
+        b, env, pol = self.buf, self.env, self.policy
+        T, N = self.n_steps, env.num_envs
+        pol.pack_heads()
+        b["obs"][0].copy_(self.obs)
+        gamma = float(self.gamma)
+        for t in range(T):
+            mean, value = pol.heads(b["obs"][t])
+            ppo_act(mean, value, pol.log_std.detach(), self.episode_start, self._noise_seed, self._noise_counter, False,
+                    b["act"][t], self._act_clip, b["logp"][t], b["val"][t], b["start"][t])
+            self._noise_counter += 1
+            obs, rew, term, trunc = env.step_tensors(self._act_clip)
+            tv = pol.value(env.terminal_obs.float())
+            nxt = b["obs"][t + 1] if t + 1 < T else self.obs
+            ppo_post(rew.float(), term.to(torch.uint8), trunc.to(torch.uint8), tv, gamma, obs.float(), nxt,
+                     b["rew"][t], b["done"][t], self.ep_acc, b["epret"][t], self.episode_start)
+        self.ep_returns += b["epret"][b["done"]].tolist()      # one device -> host transfer per rollout
+        self.num_timesteps += T * N * self.world_size
+        last_v = pol.value(self.obs)
+        return gae(b["rew"], b["val"], b["start"], last_v, self.episode_start, self.gamma, self.gae_lambda)
+
+    def _collect_rollouts_torch(self):
         """SB3 PPO.collect_rollouts on device.  No host synchronisation inside the loop: the
         timeout bootstrap r += gamma V(terminal_obs) is evaluated for every env and masked, and
         finished-episode returns are recorded in device buffers and read back once at the end."""

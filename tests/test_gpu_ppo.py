@@ -1,0 +1,134 @@
+"""HIP PPO rollout kernels (ppo.hip: hs_ppo_act / hs_ppo_post) against the torch restatement of
+SB3 2.3.2 collect_rollouts' per-step semantics (ppo.PPO._collect_rollouts_torch), and the device
+rollout's buffers against the policy they were sampled from.  SB3 itself is not importable here,
+so parity with SB3 is unpinned; these pin the kernels to the torch path's formulas."""
+import math
+
+import pytest
+import torch
+
+from conftest import XML
+
+pytestmark = pytest.mark.gpu
+
+
+def _act_inputs(N=4096, A=21, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    head = torch.randn(N, A + 3, device="cuda", generator=g)           # mean with a leading dim > A
+    value = torch.randn(N, 5, device="cuda", generator=g)              # value at stride 5
+    log_std = 0.3 * torch.randn(A, device="cuda", generator=g)
+    start = (torch.rand(N, device="cuda", generator=g) < 0.3).float()
+    return head[:, :A], value[:, 0], log_std, start
+
+
+def _run_act(mean, value, log_std, start, seed, counter, det):
+    from mujocoposelearning_amd.ppo import ppo_act
+    N, A = mean.shape
+    out = [torch.full((N, A), float("nan"), device="cuda") for _ in range(2)] + \
+          [torch.full((N,), float("nan"), device="cuda") for _ in range(3)]
+    ppo_act(mean, value, log_std, start, seed, counter, det, *out)
+    torch.cuda.synchronize()
+    return out
+
+
+def test_ppo_act_deterministic_and_logp():
+    mean, value, log_std, start = _act_inputs()
+    a, ac, lp, v, st = _run_act(mean, value, log_std, start, 1, 0, True)
+    assert torch.equal(a, mean) and torch.equal(ac, mean.clamp(-1, 1))
+    assert torch.equal(v, value) and torch.equal(st, start)
+    ref = (-log_std - 0.5 * math.log(2 * math.pi)).sum().expand_as(lp)
+    assert torch.allclose(lp, ref, rtol=1e-6, atol=1e-5)
+
+
+def test_ppo_act_sample_matches_diag_gaussian_log_prob():
+    from mujocoposelearning_amd.ppo import ActorCritic
+    mean, value, log_std, start = _act_inputs(seed=1)
+    a, ac, lp, v, st = _run_act(mean, value, log_std, start, 12345, 7, False)
+    # log_prob of the returned actions under the torch DiagGaussian formula (ActorCritic._logp)
+    pol = ActorCritic(8, mean.shape[1]).cuda()
+    with torch.no_grad():
+        pol.log_std.copy_(log_std)
+        ref = pol._logp(mean, a)
+    assert torch.allclose(lp, ref, rtol=1e-5, atol=2e-4), float((lp - ref).abs().max())
+    assert torch.equal(ac, a.clamp(-1, 1)) and torch.equal(v, value) and torch.equal(st, start)
+    z = (a - mean) / log_std.exp()
+    assert abs(float(z.mean())) < 0.02 and abs(float(z.std()) - 1) < 0.02
+    # per-action-column moments (no lane/column bias) and no correlation between neighbours
+    assert float(z.mean(0).abs().max()) < 0.06 and float((z.std(0) - 1).abs().max()) < 0.06
+    assert abs(float((z[:, :-1] * z[:, 1:]).mean())) < 0.02
+    # counter-based stream: reproducible from (seed, counter), fresh for counter + 1
+    a2 = _run_act(mean, value, log_std, start, 12345, 7, False)[0]
+    a3 = _run_act(mean, value, log_std, start, 12345, 8, False)[0]
+    assert torch.equal(a, a2) and not torch.equal(a, a3)
+
+
+def test_ppo_act_rejects_bad_shapes():
+    from mujocoposelearning_amd import _lib
+    L = _lib.lib()
+    assert L.hs_ppo_act(None, 40, None, 1, None, None, 0, 0, 0, None, None, None, None, None, 8, 33, None) < 0
+    assert b"A <= 32" in L.hs_last_error()
+    assert L.hs_ppo_act(None, 4, None, 1, None, None, 0, 0, 0, None, None, None, None, None, 8, 8, None) < 0
+    assert L.hs_ppo_post(None, None, None, None, 0.9, None, None, 0, None, None, None, None, None, 4, None) < 0
+
+
+def test_ppo_post_matches_torch_bookkeeping():
+    from mujocoposelearning_amd.ppo import ppo_post
+    N, D, gamma = 4097, 351, 0.99          # odd sizes: exercises the non-float4 obs copy
+    g = torch.Generator(device="cuda").manual_seed(3)
+    rew = torch.randn(N, device="cuda", generator=g)
+    term = (torch.rand(N, device="cuda", generator=g) < 0.2).to(torch.uint8)
+    trunc = (torch.rand(N, device="cuda", generator=g) < 0.2).to(torch.uint8)
+    tv = torch.randn(N, device="cuda", generator=g)
+    obs = torch.randn(N, D, device="cuda", generator=g)
+    acc0 = torch.randn(N, device="cuda", generator=g).double()
+    for d in (D, 352):
+        o = obs if d == D else torch.randn(N, d, device="cuda", generator=g)
+        obs_out = torch.zeros_like(o)
+        rew_out = torch.zeros(N, device="cuda")
+        done = torch.zeros(N, dtype=torch.bool, device="cuda")
+        acc = acc0.clone()
+        epret = torch.zeros(N, dtype=torch.float64, device="cuda")
+        start = torch.full((N,), 0.5, device="cuda")
+        ppo_post(rew, term, trunc, tv, gamma, o, obs_out, rew_out, done, acc, epret, start)
+        torch.cuda.synchronize()
+        # the torch restatement (PPO._collect_rollouts_torch)
+        t, tr = term.bool(), trunc.bool()
+        boot = (tr & ~t).float()
+        r_ref = rew + gamma * torch.where(boot > 0, tv, torch.zeros_like(tv))
+        d_ref = t | tr
+        acc_ref = acc0 + rew.double()
+        assert torch.allclose(rew_out, r_ref, rtol=1e-6, atol=1e-6)
+        assert torch.equal(done, d_ref) and torch.equal(epret, acc_ref)
+        assert torch.equal(acc, acc_ref.masked_fill(d_ref, 0.0)) and torch.equal(start, d_ref.float())
+        assert torch.equal(obs_out, o)
+
+
+def test_device_rollout_buffers_consistent_with_policy():
+    """One device rollout on the humanoid batch: the buffered log-probs and values are the
+    policy's own on the buffered (obs, action) pairs, obs slots chain step to step, and the
+    clipped actions the env stepped with are the buffered actions clipped."""
+    from mujocoposelearning_amd.model import HsModel
+    from mujocoposelearning_amd.ppo import PPO
+    from mujocoposelearning_amd.vec_env import HumanoidVecEnv
+    env = HumanoidVecEnv({"model_path": XML, "duration": 0.2, "reward_config": {"type": "stand"}, "frame_skip": 3},
+                         n_envs=256, model=HsModel(XML), seed=0)
+    ppo = PPO(env, n_steps=24, batch_size=1024, n_epochs=1, seed=0,
+              policy_kwargs={"activation_fn": "ReLU", "net_arch": {"pi": [256, 256], "vf": [256, 256]}})
+    obs0 = ppo.obs.clone()
+    adv, ret = ppo.collect_rollouts()
+    b = ppo.buf
+    torch.cuda.synchronize()
+    assert torch.equal(b["obs"][0], obs0)
+    with torch.no_grad():
+        T, N = b["obs"].shape[:2]
+        logp, _, v = ppo.policy.evaluate(b["obs"].reshape(T * N, -1), b["act"].reshape(T * N, -1))
+    assert torch.allclose(logp, b["logp"].reshape(-1), rtol=1e-4, atol=2e-3)
+    assert torch.allclose(v, b["val"].reshape(-1), rtol=1e-4, atol=1e-4)
+    assert torch.equal(ppo._act_clip, b["act"][-1].clamp(-1, 1))
+    # duration 0.2 s (~13 env steps): the envs, reset together, all finish at the same step inside
+    # the 24-step rollout, and the next step's episode_start flags are set
+    all_done = [t for t in range(T - 1) if bool(b["done"][t].all())]
+    assert all_done and bool((b["start"][all_done[0] + 1] == 1).all()) and len(ppo.ep_returns) >= N
+    assert not bool(b["done"][:all_done[0]].any())
+    assert torch.isfinite(adv).all() and torch.isfinite(ret).all()
+    env.close()

@@ -247,3 +247,43 @@ def test_load_sb3_named_zip_and_predict(tmp_path):
     np.testing.assert_allclose(act, mean, rtol=1e-6, atol=1e-6)
     a1, _ = model.predict(obs[0], deterministic=True)
     assert a1.shape == (3,)
+
+
+@pytest.mark.gpu
+def test_splitk_linear_grads_match_dense_linear():
+    """The split-K weight gradient (ppo.Linear on large device minibatches) equals nn.Linear's
+    gradient to fp32 summation-order tolerance (rel 1e-4 of the gradient's scale)."""
+    from mujocoposelearning_amd import ppo as ppo_mod
+    torch.manual_seed(0)
+    dev = "cuda"
+    for rows in (2 * ppo_mod._SPLITK_ROWS, 16 * ppo_mod._SPLITK_ROWS):
+        lin = ppo_mod.Linear(352, 256).to(dev)
+        ref = torch.nn.Linear(352, 256).to(dev)
+        ref.load_state_dict(lin.state_dict())
+        x = torch.randn(rows, 352, device=dev, requires_grad=True)
+        g = torch.randn(rows, 256, device=dev)
+        (lin(x) * g).sum().backward()
+        gx, gw, gb = x.grad.clone(), lin.weight.grad, lin.bias.grad
+        x.grad = None
+        (ref(x) * g).sum().backward()
+        for a, b in ((gx, x.grad), (gw, ref.weight.grad), (gb, ref.bias.grad)):
+            assert torch.allclose(a, b, rtol=1e-4, atol=1e-4 * float(b.abs().max())), float((a - b).abs().max())
+
+
+def test_packed_heads_match_two_nets():
+    """ActorCritic.pack_heads/heads (the rollout forward as one stacked GEMM chain) equals the
+    separate pi/vf MLP forward; unequal nets fall back to the two-net forward."""
+    torch.manual_seed(0)
+    pol = ActorCritic(352, 21, (256, 256), (256, 256), torch.nn.ReLU)
+    for p in pol.parameters():                    # non-trivial biases too
+        torch.nn.init.normal_(p, std=0.05)
+    obs = torch.randn(64, 352)
+    assert pol.pack_heads() is not None
+    mean, value = pol.heads(obs)
+    rm, rv = pol(obs)
+    assert torch.allclose(mean, rm, atol=1e-5) and torch.allclose(value, rv, atol=1e-5)
+    pol2 = ActorCritic(352, 21, (64, 64), (32,), torch.nn.ReLU)
+    assert pol2.pack_heads() is None
+    m2, v2 = pol2.heads(obs)
+    r2m, r2v = pol2(obs)
+    assert torch.equal(m2, r2m) and torch.equal(v2, r2v)
