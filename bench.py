@@ -181,26 +181,37 @@ def main():
     # rollout mode: policy MLP[256,256] forward + sampling + env step (on device)
     rollout = None
     if not args.no_rollout:
-        from mujocoposelearning_amd.ppo import ActorCritic
-        pol = ActorCritic(env.batch.obs_dim, model.nu, (256, 256)).to(dev)
+        from mujocoposelearning_amd.ppo import ActorCritic, ppo_act
+        pol = ActorCritic(env.batch.obs_dim, model.nu, (256, 256), activation=torch.nn.ReLU).to(dev)
+        pol.pack_heads()
+        ls = pol.log_std.detach()
+        start = torch.zeros(n, device=dev)
+        act, clip = torch.empty(n, model.nu, device=dev), torch.empty(n, model.nu, device=dev)
+        logp, val, st_out = (torch.empty(n, device=dev) for _ in range(3))
         obs = env.batch.obs
+
+        def policy_step(obs, k):
+            # the PPO rollout's policy half (ppo.PPO._collect_rollouts_device): packed pi/vf GEMM
+            # chain + hs_ppo_act (Gaussian sample, log-prob, clip, buffer writes), then the env
+            mean, value = pol.heads(obs)
+            ppo_act(mean, value, ls, start, 1 + rank, k, False, act, clip, logp, val, st_out)
+            return env.step_tensors(clip)[0]
+
         with torch.no_grad():
             for k in range(5):
-                a, _, _ = pol.act(obs.float())
-                obs, *_ = env.step_tensors(a.clamp_(-1, 1))
+                obs = policy_step(obs, k)
             barrier()
             tr0 = time.perf_counter()
             rs = max(10, args.steps // 2)
             for k in range(rs):
-                a, _, _ = pol.act(obs.float())
-                obs, *_ = env.step_tensors(a.clamp_(-1, 1))
+                obs = policy_step(obs, 5 + k)
             barrier()
             rel = time.perf_counter() - tr0
         t = torch.tensor([rel], dtype=torch.float64, device=red_dev)
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         rollout = dict(value=n * rs * world / float(t.item()), unit="env_steps/s",
-                       note="policy MLP[256,256] (pi+vf) forward + diag-Gaussian sample + clip + env step")
+                       note="policy MLP[256,256] (pi+vf, packed GEMM chain) forward + hs_ppo_act (diag-Gaussian sample, log-prob, clip) + env step")
 
     # extra sim-only leg: the same n envs as free-running stream groups (no per-step join; the
     # action tape is open-loop, so every env still takes exactly the same steps)

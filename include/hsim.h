@@ -25,6 +25,10 @@
  *                           the actions, RolloutBuffer.add of actions/values/log_probs/episode_starts
  *   hs_ppo_post          <- the same loop after env.step: TimeLimit.truncated bootstrap of the reward,
  *                           dones, episode returns, new episode_starts, next obs into the buffer
+ *   hs_gauss_logp(_grad) <- DiagGaussianDistribution.log_prob of the buffered actions in the PPO
+ *                           update (SB3 ActorCriticPolicy.evaluate_actions) and its backward
+ *   hs_colsum            <- the bias-gradient and split-K weight-gradient reductions of the PPO
+ *                           update's loss.backward() (SB3 PPO.train, ppo.py; train_sb3.py:229)
  *
  * Conventions: status int (0 ok, <0 error, message via hs_last_error(), thread-local); the
  * model is immutable and shareable; a batch owns (or is bound to) device buffers; every call
@@ -164,6 +168,19 @@ int hs_ppo_act(const float* mean, int mean_ld, const float* value, int value_ld,
 int hs_ppo_post(const float* reward, const uint8_t* terminated, const uint8_t* truncated, const float* terminal_value,
                 float gamma, const float* obs, float* obs_out, uint64_t obs_floats, float* reward_out,
                 uint8_t* done_out, double* ep_acc, double* ep_return_out, float* episode_start, int N, void* stream);
+/* out[c] = sum_r x[r][c] over a row-major [rows][cols] float32 device matrix, in a fixed
+ * summation order (deterministic).  `workspace` must hold hs_colsum_workspace(rows, cols) floats
+ * (may be NULL when that is 0).  Asynchronous on `stream`. */
+/* logp[n] = sum_j (-z^2/2 - log_std[j]) - A log(sqrt(2 pi)), z = (actions[n][j] - mean[n][j]) /
+ * exp(log_std[j]); mean [N][mean_ld], actions [N][A] contiguous, A <= 32.  The backward, given
+ * g_logp [N]: g_mean[n][j] = g z / sigma and gls_rows[n][j] = g (z^2 - 1), whose column sums
+ * (hs_colsum) are dL/dlog_std.  Asynchronous on `stream`. */
+int hs_gauss_logp(const float* mean, int mean_ld, const float* actions, const float* log_std, float* logp, int N,
+                  int A, void* stream);
+int hs_gauss_logp_grad(const float* mean, int mean_ld, const float* actions, const float* log_std,
+                       const float* g_logp, float* g_mean, float* gls_rows, int N, int A, void* stream);
+uint64_t hs_colsum_workspace(uint64_t rows, uint64_t cols);
+int hs_colsum(const float* x, uint64_t rows, uint64_t cols, float* workspace, float* out, void* stream);
 const char* hs_last_error(void);
 const char* hs_version(void);
 

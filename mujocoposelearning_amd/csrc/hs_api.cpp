@@ -441,6 +441,38 @@ int hs_ppo_post(const float* reward, const uint8_t* terminated, const uint8_t* t
              : -1;
 }
 
+int hs_gauss_logp(const float* mean, int mean_ld, const float* actions, const float* log_std, float* logp, int N,
+                  int A, void* stream) {
+  if (N < 0 || A < 1 || A > 32 || mean_ld < A) return fail("hs_gauss_logp: need N >= 0, 1 <= A <= 32, mean_ld >= A");
+  if (N == 0) return 0;
+  if (!mean || !actions || !log_std || !logp) return fail("hs_gauss_logp: null buffer");
+  return hip_ok(hs::launch_gauss_logp(mean, mean_ld, actions, log_std, logp, N, A, (hipStream_t)stream),
+                "gauss_logp_kernel")
+             ? 0
+             : -1;
+}
+
+int hs_gauss_logp_grad(const float* mean, int mean_ld, const float* actions, const float* log_std,
+                       const float* g_logp, float* g_mean, float* gls_rows, int N, int A, void* stream) {
+  if (N < 0 || A < 1 || mean_ld < A) return fail("hs_gauss_logp_grad: need N >= 0, A >= 1, mean_ld >= A");
+  if (N == 0) return 0;
+  if (!mean || !actions || !log_std || !g_logp || !g_mean || !gls_rows) return fail("hs_gauss_logp_grad: null buffer");
+  return hip_ok(hs::launch_gauss_logp_grad(mean, mean_ld, actions, log_std, g_logp, g_mean, gls_rows, N, A,
+                                           (hipStream_t)stream),
+                "gauss_logp_grad_kernel")
+             ? 0
+             : -1;
+}
+
+uint64_t hs_colsum_workspace(uint64_t rows, uint64_t cols) { return hs::colsum_workspace(rows, cols); }
+
+int hs_colsum(const float* x, uint64_t rows, uint64_t cols, float* workspace, float* out, void* stream) {
+  if (cols == 0) return 0;
+  if (!out || (rows && !x)) return fail("hs_colsum: null buffer");
+  if (hs::colsum_workspace(rows, cols) && !workspace) return fail("hs_colsum: workspace required");
+  return hip_ok(hs::launch_colsum(x, rows, cols, workspace, out, (hipStream_t)stream), "colsum_kernel") ? 0 : -1;
+}
+
 int hs_gae(const float* rewards, const float* values, const float* episode_starts, const float* last_values,
            const float* last_dones, float* advantages, float* returns, int T, int N, float gamma, float gae_lambda,
            void* stream) {

@@ -75,6 +75,16 @@ hipError_t launch_ppo_post(const float* reward, const uint8_t* terminated, const
                            const float* terminal_value, float gamma, const float* obs, float* obs_out, size_t obs_floats,
                            float* reward_out, uint8_t* done_out, double* ep_acc, double* ep_return_out,
                            float* episode_start, int N, hipStream_t stream);
+// column sums of a row-major [rows][cols] float32 matrix (ppo.hip); workspace of
+// colsum_workspace(rows, cols) floats (0: none needed)
+size_t colsum_workspace(size_t rows, size_t cols);
+hipError_t launch_colsum(const float* x, size_t rows, size_t cols, float* workspace, float* out, hipStream_t stream);
+// diagonal-Gaussian log-prob of given actions and its backward (ppo.hip)
+hipError_t launch_gauss_logp(const float* mean, int mean_ld, const float* act, const float* log_std, float* logp, int N,
+                             int A, hipStream_t stream);
+hipError_t launch_gauss_logp_grad(const float* mean, int mean_ld, const float* act, const float* log_std,
+                                  const float* g_logp, float* g_mean, float* gls_rows, int N, int A,
+                                  hipStream_t stream);
 // GAE reverse scan over [T][N] float32 rollout arrays (gae.hip)
 hipError_t launch_gae(const float* rew, const float* val, const float* start, const float* last_val,
                       const float* last_done, float* adv, float* ret, int T, int N, float gamma, float lam,

@@ -130,7 +130,103 @@ __global__ __launch_bounds__(256) void ppo_post_kernel(const float* __restrict__
   }
 }
 
+
+// DiagGaussianDistribution.log_prob of given actions (SB3 common/distributions.py), the PPO
+// update's evaluate_actions, and its backward: with z = (a - mean) / sigma and upstream g = dL/dlogp,
+//   logp       = sum_j (-z_j^2 / 2 - log sigma_j) - A log(sqrt(2 pi))
+//   dL/dmean_j = g z_j / sigma_j
+//   dL/dlog sigma_j = sum_rows g (z_j^2 - 1)     (the per-row terms are written to `gls_rows`;
+//                                                the batch sum is colsum_kernel's)
+// Half-wave per row (A <= 32), as ppo_act_kernel.
+__global__ __launch_bounds__(256) void gauss_logp_kernel(const float* __restrict__ mean, int mean_ld,
+                                                         const float* __restrict__ act,
+                                                         const float* __restrict__ log_std,
+                                                         float* __restrict__ logp, int N, int A) {
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = gid >> 5, j = gid & 31;
+  if (n >= N) return;
+  float term = 0.f;
+  if (j < A) {
+    const float ls = log_std[j];
+    const float z = (act[(size_t)n * A + j] - mean[(size_t)n * mean_ld + j]) * __expf(-ls);
+    term = -0.5f * z * z - ls - 0.91893853320467274f;
+  }
+  const float lp = half_sum(term);
+  if (j == 0) logp[n] = lp;
+}
+
+__global__ __launch_bounds__(256) void gauss_logp_grad_kernel(const float* __restrict__ mean, int mean_ld,
+                                                              const float* __restrict__ act,
+                                                              const float* __restrict__ log_std,
+                                                              const float* __restrict__ g_logp,
+                                                              float* __restrict__ g_mean,
+                                                              float* __restrict__ gls_rows, int N, int A) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;   // element of [N][A]
+  if (i >= (size_t)N * A) return;
+  const size_t n = i / A;
+  const int j = (int)(i - n * A);
+  const float ls = log_std[j];
+  const float inv = __expf(-ls);
+  const float z = (act[i] - mean[n * mean_ld + j]) * inv;
+  const float g = g_logp[n];
+  g_mean[i] = g * z * inv;
+  gls_rows[i] = g * (z * z - 1.0f);
+}
+
+// Column sums of a row-major [rows][cols] float32 matrix: out[c] = sum_r x[r][c].  The PPO
+// update's bias gradients (sum of the output gradient over the minibatch, [32768][256]) and the
+// split-K weight-gradient finish (sum over S slices of [S][out*in]).  A workgroup is a tile of
+// 64 columns (a wave reads 256 contiguous bytes of a row per load) x 16 row phases (waves); each
+// lane runs 4 independent accumulation chains over its rows, then the 16 phases are combined
+// through LDS.  grid.y splits the rows into chunks whose partial rows a second launch
+// (grid.y = 1) sums: fixed summation order, so results are run-to-run deterministic (no float
+// atomics), and every lane's dependent-load chain stays short.
+constexpr int CS_COLS = 64, CS_PHASES = 16;
+
+__global__ __launch_bounds__(CS_COLS* CS_PHASES) void colsum_kernel(const float* __restrict__ x, size_t rows,
+                                                                     size_t cols, size_t rows_per_chunk,
+                                                                     float* __restrict__ out) {
+  __shared__ float part[CS_PHASES][CS_COLS];
+  const int lane = threadIdx.x, ph = threadIdx.y;
+  const size_t c = (size_t)blockIdx.x * CS_COLS + lane;
+  const size_t r0 = (size_t)blockIdx.y * rows_per_chunk;
+  const size_t r1 = r0 + rows_per_chunk < rows ? r0 + rows_per_chunk : rows;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (c < cols) {
+    const float* __restrict__ p = x + c;
+    const size_t step = (size_t)CS_PHASES * cols;
+    size_t r = r0 + ph;
+    for (; r + 3 * CS_PHASES < r1; r += 4 * CS_PHASES) {
+      const float* q = p + r * cols;
+      a0 += q[0];
+      a1 += q[step];
+      a2 += q[2 * step];
+      a3 += q[3 * step];
+    }
+    for (; r < r1; r += CS_PHASES) a0 += p[r * cols];
+  }
+  part[ph][lane] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (ph == 0 && c < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < CS_PHASES; k++) t += part[k][lane];
+    out[(size_t)blockIdx.y * cols + c] = t;
+  }
+}
+
 }  // namespace
+
+// row chunks for colsum: enough workgroups to fill the chip (~1024) with >= 32 rows each;
+// one chunk (a single launch) when the column tiles alone give that parallelism
+static size_t colsum_chunks(size_t rows, size_t cols) {
+  const size_t ctiles = (cols + CS_COLS - 1) / CS_COLS;
+  if (ctiles >= 512 || rows <= 4 * CS_PHASES) return 1;
+  size_t chunks = 512 / ctiles;                 // ~512 workgroups of 16 waves
+  const size_t maxc = rows / (4 * CS_PHASES);   // >= 4 rows per lane
+  if (chunks > maxc) chunks = maxc;
+  return chunks < 1 ? 1 : chunks;
+}
 
 hipError_t launch_ppo_act(const float* mean, int mean_ld, const float* value, int value_ld, const float* log_std,
                           const float* episode_start, uint64_t seed, uint64_t counter, int deterministic, float* act,
@@ -162,6 +258,48 @@ hipError_t launch_ppo_post(const float* reward, const uint8_t* terminated, const
   hipLaunchKernelGGL(ppo_post_kernel, dim3((unsigned)blocks), dim3(block), 0, stream, reward, terminated, truncated,
                      terminal_value, gamma, obs, obs_out, obs_n, vec4, reward_out, done_out, ep_acc, ep_return_out,
                      episode_start, N);
+  return hipGetLastError();
+}
+
+size_t colsum_workspace(size_t rows, size_t cols) {
+  const size_t chunks = colsum_chunks(rows, cols);
+  return chunks > 1 ? chunks * cols : 0;
+}
+
+hipError_t launch_colsum(const float* x, size_t rows, size_t cols, float* workspace, float* out, hipStream_t stream) {
+  if (cols == 0) return hipSuccess;
+  const dim3 block(CS_COLS, CS_PHASES);
+  const unsigned ctiles = (unsigned)((cols + CS_COLS - 1) / CS_COLS);
+  const size_t chunks = colsum_chunks(rows, cols);
+  if (rows == 0) return hipMemsetAsync(out, 0, cols * sizeof(float), stream);
+  if (chunks <= 1) {
+    hipLaunchKernelGGL(colsum_kernel, dim3(ctiles, 1), block, 0, stream, x, rows, cols, rows, out);
+    return hipGetLastError();
+  }
+  const size_t rpc = (rows + chunks - 1) / chunks;
+  hipLaunchKernelGGL(colsum_kernel, dim3(ctiles, (unsigned)chunks), block, 0, stream, x, rows, cols, rpc,
+                     workspace);
+  hipLaunchKernelGGL(colsum_kernel, dim3(ctiles, 1), block, 0, stream, (const float*)workspace, chunks, cols,
+                     chunks, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_gauss_logp(const float* mean, int mean_ld, const float* act, const float* log_std, float* logp, int N,
+                             int A, hipStream_t stream) {
+  if (N <= 0) return hipSuccess;
+  const size_t threads = (size_t)N * 32;
+  hipLaunchKernelGGL(gauss_logp_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, stream, mean, mean_ld,
+                     act, log_std, logp, N, A);
+  return hipGetLastError();
+}
+
+hipError_t launch_gauss_logp_grad(const float* mean, int mean_ld, const float* act, const float* log_std,
+                                  const float* g_logp, float* g_mean, float* gls_rows, int N, int A,
+                                  hipStream_t stream) {
+  if (N <= 0) return hipSuccess;
+  const size_t el = (size_t)N * A;
+  hipLaunchKernelGGL(gauss_logp_grad_kernel, dim3((unsigned)((el + 255) / 256)), dim3(256), 0, stream, mean, mean_ld,
+                     act, log_std, g_logp, g_mean, gls_rows, N, A);
   return hipGetLastError();
 }
 

@@ -43,9 +43,61 @@ class _SplitKLinearFn(torch.autograd.Function):
     def backward(ctx, g):
         x, w = ctx.saved_tensors
         s = ctx.s
+        g = g.contiguous()
         gx = g @ w if ctx.needs_input_grad[0] else None
-        gw = torch.bmm(g.view(s, -1, g.shape[1]).transpose(1, 2), x.view(s, -1, x.shape[1])).sum(0)
-        return gx, gw, g.sum(0), None
+        part = torch.bmm(g.view(s, -1, g.shape[1]).transpose(1, 2), x.view(s, -1, x.shape[1]))   # [S, out, in]
+        gw = colsum(part.view(s, -1)).view_as(w)
+        return gx, gw, colsum(g), None
+
+
+class _GaussLogpFn(torch.autograd.Function):
+    """DiagGaussianDistribution.log_prob(actions) for mean [N, A] (A <= 32) on a device: one
+    hs_gauss_logp launch forward; backward one hs_gauss_logp_grad launch (dL/dmean and the
+    per-row dL/dlog_std terms) + hs_colsum over the rows."""
+
+    @staticmethod
+    def forward(ctx, mean, actions, log_std):
+        from . import _lib
+        if mean.stride(1) != 1:
+            mean = mean.contiguous()
+        actions = actions.contiguous()
+        N, A = mean.shape
+        logp = torch.empty(N, dtype=torch.float32, device=mean.device)
+        st = torch.cuda.current_stream(mean.device).cuda_stream
+        _lib.check(_lib.lib().hs_gauss_logp(mean.data_ptr(), mean.stride(0), actions.data_ptr(), log_std.data_ptr(),
+                                            logp.data_ptr(), N, A, st))
+        ctx.save_for_backward(mean, actions, log_std)
+        return logp
+
+    @staticmethod
+    def backward(ctx, g):
+        from . import _lib
+        mean, actions, log_std = ctx.saved_tensors
+        N, A = mean.shape
+        g = g.contiguous()
+        g_mean = torch.empty(N, A, dtype=torch.float32, device=mean.device)
+        rows = torch.empty(N, A, dtype=torch.float32, device=mean.device)
+        st = torch.cuda.current_stream(mean.device).cuda_stream
+        _lib.check(_lib.lib().hs_gauss_logp_grad(mean.data_ptr(), mean.stride(0), actions.data_ptr(),
+                                                 log_std.data_ptr(), g.data_ptr(), g_mean.data_ptr(), rows.data_ptr(),
+                                                 N, A, st))
+        return g_mean, None, colsum(rows)
+
+
+def colsum(x):
+    """Column sums of a contiguous [rows, cols] float32 device matrix through hs_colsum
+    (ppo.hip): deterministic, and 3-5x faster than torch's dim-0 reduction at the PPO update's
+    shapes ([32768, 256] bias gradients, [16, 90112] split-K finishes)."""
+    from . import _lib
+    assert x.dim() == 2 and x.is_contiguous() and x.dtype == torch.float32 and x.is_cuda
+    rows, cols = x.shape
+    L = _lib.lib()
+    ws_n = int(L.hs_colsum_workspace(rows, cols))
+    ws = torch.empty(ws_n, dtype=torch.float32, device=x.device) if ws_n else None
+    out = torch.empty(cols, dtype=torch.float32, device=x.device)
+    _lib.check(L.hs_colsum(x.data_ptr(), rows, cols, ws.data_ptr() if ws is not None else None, out.data_ptr(),
+                           torch.cuda.current_stream(x.device).cuda_stream))
+    return out
 
 
 class Linear(nn.Linear):
@@ -88,9 +140,19 @@ class ActorCritic(nn.Module):
         return self.action_net(self.pi_net(obs)), self.value_net(self.vf_net(obs)).squeeze(-1)
 
     def _logp(self, mean, actions):
+        """DiagGaussian log_prob; on a device through hs_gauss_logp (+ its HIP backward)."""
+        if mean.is_cuda and mean.shape[-1] <= 32:
+            return _GaussLogpFn.apply(mean, actions, self.log_std)
+        return self._logp_torch(mean, actions)
+
+    def _logp_torch(self, mean, actions):
         std = self.log_std.exp()
         z = (actions - mean) / std
         return (-0.5 * z * z - self.log_std - 0.5 * math.log(2 * math.pi)).sum(-1)
+
+    def entropy(self):
+        """DiagGaussian entropy (state-independent std, so the same for every sample)."""
+        return (0.5 + 0.5 * math.log(2 * math.pi) + self.log_std).sum()
 
     @torch.no_grad()
     def act(self, obs, deterministic=False):
@@ -260,8 +322,13 @@ class PPO:
                                   pk.get("log_std_init", 0.0)).to(self.device)
         torch.manual_seed(seed + 7919 * rank)   # per-rank exploration noise / minibatch order
         # fused (single-kernel) Adam on a device; the same update rule and state_dict as foreach Adam
+        cuda = self.device.type == "cuda"
         self.opt = torch.optim.Adam(self.policy.parameters(), lr=learning_rate, eps=1e-5,
-                                    fused=True if self.device.type == "cuda" else None)
+                                    fused=True if cuda else None, capturable=cuda)
+        # on a device the minibatch step replays as HIP graphs (see _build_graphs); the update is
+        # launch-bound without them (~1.3 ms of kernels per 32768-sample step, ~1.7 ms eager)
+        self.graphs = cuda
+        self._graphs = None
         self.n_steps, self.batch_size, self.n_epochs = n_steps, batch_size, n_epochs
         self.gamma, self.gae_lambda, self.clip_range = gamma, gae_lambda, clip_range
         self.ent_coef, self.vf_coef, self.max_grad_norm = ent_coef, vf_coef, max_grad_norm
@@ -363,28 +430,35 @@ class PPO:
             g.copy_(flat[o:o + n].view_as(g))
             o += n
 
+    def _minibatch_loss(self, obs, act, old_logp, adv, ret, idx):
+        """SB3 PPO.train's per-minibatch loss (clipped surrogate + vf_coef MSE - ent_coef entropy)."""
+        mean, v = self.policy(obs[idx])
+        logp = self.policy._logp(mean, act[idx])
+        ent_mean = self.policy.entropy()            # = evaluate()'s per-sample entropy, averaged
+        a = adv[idx]
+        if a.numel() > 1:
+            a = (a - a.mean()) / (a.std() + 1e-8)
+        ratio = torch.exp(logp - old_logp[idx])
+        pg = -torch.min(a * ratio, a * ratio.clamp(1 - self.clip_range, 1 + self.clip_range)).mean()
+        vf = torch.nn.functional.mse_loss(ret[idx], v)
+        return pg + self.ent_coef * (-ent_mean) + self.vf_coef * vf, pg, vf
+
     def train(self, adv, ret):
         b = self.buf
         T, N = self.n_steps, self.env.num_envs
-        obs = b["obs"].reshape(T * N, -1)
-        act = b["act"].reshape(T * N, -1)
-        old_logp, old_v = b["logp"].reshape(-1), b["val"].reshape(-1)
-        adv, ret = adv.reshape(-1), ret.reshape(-1)
         M = T * N
+        if self.device.type == "cuda" and self.graphs and M % self.batch_size == 0:
+            return self._train_graphed(adv, ret)
+        obs = b["obs"].reshape(M, -1)
+        act = b["act"].reshape(M, -1)
+        old_logp = b["logp"].reshape(-1)
+        adv, ret = adv.reshape(-1), ret.reshape(-1)
         stats = []
         for epoch in range(self.n_epochs):
             perm = torch.randperm(M, device=self.device)
             for s in range(0, M, self.batch_size):
-                idx = perm[s:s + self.batch_size]
-                logp, ent, v = self.policy.evaluate(obs[idx], act[idx])
-                a = adv[idx]
-                if a.numel() > 1:
-                    a = (a - a.mean()) / (a.std() + 1e-8)
-                ratio = torch.exp(logp - old_logp[idx])
-                pg = -torch.min(a * ratio, a * ratio.clamp(1 - self.clip_range, 1 + self.clip_range)).mean()
-                vf = torch.nn.functional.mse_loss(ret[idx], v)
-                loss = pg + self.ent_coef * (-ent.mean()) + self.vf_coef * vf
-                self.opt.zero_grad(set_to_none=False)
+                loss, pg, vf = self._minibatch_loss(obs, act, old_logp, adv, ret, perm[s:s + self.batch_size])
+                self.opt.zero_grad(set_to_none=True)
                 loss.backward()
                 self._allreduce_grads()
                 torch.nn.utils.clip_grad_norm_(self.policy.parameters(), self.max_grad_norm)
@@ -392,6 +466,82 @@ class PPO:
                 stats.append((pg.detach(), vf.detach()))
         pg = torch.stack([s[0] for s in stats]).mean().item()
         vf = torch.stack([s[1] for s in stats]).mean().item()
+        return dict(policy_loss=pg, value_loss=vf)
+
+    # -- HIP-graph update ----------------------------------------------------------------------
+    def _build_graphs(self):
+        """Capture one minibatch step as two HIP graphs over static buffers: G1 = gather by the
+        static index buffer + forward + loss + backward (gradients land in graph-owned .grad
+        tensors), G2 = clip_grad_norm + capturable fused Adam.  The per-step gradient all-reduce
+        (world > 1) runs eagerly between them on those same .grad tensors.  The warm-up steps
+        capture needs are undone (parameters and Adam state restored in place), so graphed
+        training takes exactly the eager path's optimizer steps."""
+        b, M, bs = self.buf, self.n_steps * self.env.num_envs, self.batch_size
+        dev = self.device
+        self._g_idx = torch.zeros(bs, dtype=torch.long, device=dev)
+        self._g_adv = torch.zeros(M, dtype=torch.float32, device=dev)
+        self._g_ret = torch.zeros(M, dtype=torch.float32, device=dev)
+        self._g_stats = torch.zeros(2, dtype=torch.float32, device=dev)
+        src = (b["obs"].view(M, -1), b["act"].view(M, -1), b["logp"].view(-1), self._g_adv, self._g_ret)
+        params = list(self.policy.parameters())
+
+        def g1_body():
+            loss, pg, vf = self._minibatch_loss(*src, self._g_idx)
+            loss.backward()
+            self._g_stats.add_(torch.stack([pg.detach(), vf.detach()]))
+
+        def g2_body():
+            torch.nn.utils.clip_grad_norm_(params, self.max_grad_norm)
+            self.opt.step()
+
+        saved_p = [p.detach().clone() for p in params]
+        saved_s = {id(p): {k: v.clone() for k, v in self.opt.state[p].items()} for p in params if p in self.opt.state}
+        self._g_idx.copy_(torch.arange(bs, device=dev))
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                self.opt.zero_grad(set_to_none=True)
+                g1_body()
+                g2_body()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self.opt.zero_grad(set_to_none=True)
+        pool = torch.cuda.graph_pool_handle()
+        g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g1, pool=pool):
+            g1_body()
+        with torch.cuda.graph(g2, pool=pool):
+            g2_body()
+        with torch.no_grad():                      # undo the warm-up steps in place
+            for p, q in zip(params, saved_p):
+                p.copy_(q)
+            for p in params:
+                st, old = self.opt.state.get(p, {}), saved_s.get(id(p))
+                for k, v in st.items():
+                    if old is not None and k in old:
+                        v.copy_(old[k])
+                    elif torch.is_tensor(v):
+                        v.zero_()
+        self._graphs = (g1, g2)
+
+    def _train_graphed(self, adv, ret):
+        if self._graphs is None:
+            self._build_graphs()
+        g1, g2 = self._graphs
+        M, bs = self.n_steps * self.env.num_envs, self.batch_size
+        self._g_adv.copy_(adv.reshape(-1))
+        self._g_ret.copy_(ret.reshape(-1))
+        self._g_stats.zero_()
+        n = 0
+        for epoch in range(self.n_epochs):
+            perm = torch.randperm(M, device=self.device)
+            for s in range(0, M, bs):
+                self._g_idx.copy_(perm[s:s + bs])
+                g1.replay()
+                self._allreduce_grads()
+                g2.replay()
+                n += 1
+        pg, vf = (self._g_stats / n).tolist()
         return dict(policy_loss=pg, value_loss=vf)
 
     def learn(self, total_timesteps, callback=None, log_interval=1):
@@ -439,5 +589,6 @@ class PPO:
         """Load weights + optimizer state from an SB3-layout zip (ours or SB3's own)."""
         from .sb3_format import load_sb3_zip
         data = load_sb3_zip(path, self.policy, self.opt, map_location=self.device)
+        self._graphs = None          # optimizer state tensors were replaced: recapture
         self.num_timesteps = int(data.get("num_timesteps", 0))
         return self

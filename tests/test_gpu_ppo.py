@@ -48,7 +48,7 @@ def test_ppo_act_sample_matches_diag_gaussian_log_prob():
     pol = ActorCritic(8, mean.shape[1]).cuda()
     with torch.no_grad():
         pol.log_std.copy_(log_std)
-        ref = pol._logp(mean, a)
+        ref = pol._logp_torch(mean, a)
     assert torch.allclose(lp, ref, rtol=1e-5, atol=2e-4), float((lp - ref).abs().max())
     assert torch.equal(ac, a.clamp(-1, 1)) and torch.equal(v, value) and torch.equal(st, start)
     z = (a - mean) / log_std.exp()
@@ -131,4 +131,71 @@ def test_device_rollout_buffers_consistent_with_policy():
     assert all_done and bool((b["start"][all_done[0] + 1] == 1).all()) and len(ppo.ep_returns) >= N
     assert not bool(b["done"][:all_done[0]].any())
     assert torch.isfinite(adv).all() and torch.isfinite(ret).all()
+    env.close()
+
+
+@pytest.mark.parametrize("rows,cols", [(32768, 256), (32768, 21), (32768, 1), (16, 90112), (2, 5), (100, 300),
+                                       (0, 7)])
+def test_colsum_matches_fp64_sum(rows, cols):
+    from mujocoposelearning_amd.ppo import colsum
+    g = torch.Generator(device="cuda").manual_seed(rows + cols)
+    x = torch.randn(rows, cols, device="cuda", generator=g)
+    out = colsum(x)
+    out2 = colsum(x)
+    ref = x.double().sum(0).float()
+    assert torch.equal(out, out2)                                   # fixed summation order
+    assert torch.allclose(out, ref, rtol=1e-5, atol=1e-5 * max(1.0, rows ** 0.5)), float((out - ref).abs().max())
+
+
+def test_gauss_logp_forward_backward_match_torch():
+    """hs_gauss_logp / hs_gauss_logp_grad (the update's log-prob) == the torch DiagGaussian
+    formula and its autograd gradients (mean through a strided view, as the packed heads give)."""
+    from mujocoposelearning_amd.ppo import ActorCritic
+    N, A = 32768, 21
+    g = torch.Generator(device="cuda").manual_seed(5)
+    pol = ActorCritic(8, A).cuda()
+    with torch.no_grad():
+        pol.log_std.copy_(0.4 * torch.randn(A, device="cuda", generator=g))
+    base = torch.randn(N, A + 1, device="cuda", generator=g)
+    act = torch.randn(N, A, device="cuda", generator=g)
+    w = torch.randn(N, device="cuda", generator=g)
+    out = []
+    for fn in (pol._logp, pol._logp_torch):
+        m = base.clone().requires_grad_()
+        pol.log_std.grad = None
+        lp = fn(m[:, :A], act)
+        (lp * w).sum().backward()
+        out.append((lp.detach(), m.grad[:, :A].clone(), pol.log_std.grad.clone()))
+    (lp, gm, gls), (lp_r, gm_r, gls_r) = out
+    assert torch.allclose(lp, lp_r, rtol=1e-5, atol=1e-4)
+    assert torch.allclose(gm, gm_r, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(gls, gls_r, rtol=1e-4, atol=1e-3 * float(gls_r.abs().max())), float((gls - gls_r).abs().max())
+
+
+def test_graphed_update_matches_eager_update():
+    """PPO.train replayed as HIP graphs (G1 fwd+bwd, G2 clip+Adam) takes the same optimizer steps
+    as the eager loop: same rollout, same minibatch permutations -> same weights and losses."""
+    from mujocoposelearning_amd.model import HsModel
+    from mujocoposelearning_amd.ppo import PPO
+    from mujocoposelearning_amd.vec_env import HumanoidVecEnv
+    env = HumanoidVecEnv({"model_path": XML, "duration": 10.0, "reward_config": {"type": "stand"}, "frame_skip": 3},
+                         n_envs=512, model=HsModel(XML), seed=0)
+    kw = dict(n_steps=16, batch_size=2048, n_epochs=2, seed=0,
+              policy_kwargs={"activation_fn": "ReLU", "net_arch": {"pi": [256, 256], "vf": [256, 256]}})
+    pa, pb = PPO(env, **kw), PPO(env, **kw)
+    pb.graphs = False
+    adv, ret = pa.collect_rollouts()
+    for k in pa.buf:
+        pb.buf[k].copy_(pa.buf[k])
+    res = []
+    for p in (pa, pb):
+        for it in range(2):                 # the second call replays the graphs captured by the first
+            torch.manual_seed(100 + it)
+            res.append(p.train(adv, ret))
+    assert pa._graphs is not None and pb._graphs is None
+    for x, y in zip(pa.policy.parameters(), pb.policy.parameters()):
+        assert torch.allclose(x, y, rtol=1e-4, atol=1e-6), float((x - y).abs().max())
+    for ra, rb in zip(res[:2], res[2:]):
+        assert abs(ra["policy_loss"] - rb["policy_loss"]) < 1e-4 and abs(ra["value_loss"] - rb["value_loss"]) < 1e-3 * (
+            1 + abs(rb["value_loss"]))
     env.close()
