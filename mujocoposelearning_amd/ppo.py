@@ -411,18 +411,21 @@ class PPO:
         last_v = pol.value(self.obs)
         return gae(b["rew"], b["val"], b["start"], last_v, self.episode_start, self.gamma, self.gae_lambda)
 
-    def _allreduce_grads(self):
-        if self.world_size == 1:
-            return
+    def _allreduce_flat(self, flat):
         import torch.distributed as dist
-        grads = [p.grad for p in self.flat]
-        flat = torch.cat([g.reshape(-1) for g in grads])
         if flat.is_cuda and dist.get_backend() == "gloo":     # multi-rank rehearsal without RCCL
             host = flat.cpu()
             dist.all_reduce(host)
             flat.copy_(host)
         else:
             dist.all_reduce(flat)        # ONE RCCL all-reduce per optimizer step (xGMI ring)
+
+    def _allreduce_grads(self):
+        if self.world_size == 1:
+            return
+        grads = [p.grad for p in self.flat]
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        self._allreduce_flat(flat)
         flat /= self.world_size
         o = 0
         for g in grads:
@@ -472,8 +475,9 @@ class PPO:
     def _build_graphs(self):
         """Capture one minibatch step as two HIP graphs over static buffers: G1 = gather by the
         static index buffer + forward + loss + backward (gradients land in graph-owned .grad
-        tensors), G2 = clip_grad_norm + capturable fused Adam.  The per-step gradient all-reduce
-        (world > 1) runs eagerly between them on those same .grad tensors.  The warm-up steps
+        tensors and, for world > 1, are packed into one flat bucket), G2 = unpack/average the
+        bucket + clip_grad_norm + capturable fused Adam.  The per-step RCCL all-reduce of the
+        bucket (world > 1) is the one eager call between the two replays.  The warm-up steps
         capture needs are undone (parameters and Adam state restored in place), so graphed
         training takes exactly the eager path's optimizer steps."""
         b, M, bs = self.buf, self.n_steps * self.env.num_envs, self.batch_size
@@ -485,12 +489,23 @@ class PPO:
         src = (b["obs"].view(M, -1), b["act"].view(M, -1), b["logp"].view(-1), self._g_adv, self._g_ret)
         params = list(self.policy.parameters())
 
+        world = self.world_size
+        self._g_flat = torch.zeros(sum(p.numel() for p in params), dtype=torch.float32, device=dev) if world > 1 else None
+
         def g1_body():
             loss, pg, vf = self._minibatch_loss(*src, self._g_idx)
             loss.backward()
             self._g_stats.add_(torch.stack([pg.detach(), vf.detach()]))
+            if world > 1:                # the gradient bucket the eager all-reduce sends
+                torch.cat([p.grad.reshape(-1) for p in params], out=self._g_flat)
 
         def g2_body():
+            if world > 1:                # averaged bucket back into the .grad tensors
+                o = 0
+                for p in params:
+                    n = p.numel()
+                    p.grad.copy_(self._g_flat[o:o + n].view_as(p.grad)).mul_(1.0 / world)
+                    o += n
             torch.nn.utils.clip_grad_norm_(params, self.max_grad_norm)
             self.opt.step()
 
@@ -538,7 +553,8 @@ class PPO:
             for s in range(0, M, bs):
                 self._g_idx.copy_(perm[s:s + bs])
                 g1.replay()
-                self._allreduce_grads()
+                if self.world_size > 1:
+                    self._allreduce_flat(self._g_flat)
                 g2.replay()
                 n += 1
         pg, vf = (self._g_stats / n).tolist()

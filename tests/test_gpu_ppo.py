@@ -199,3 +199,59 @@ def test_graphed_update_matches_eager_update():
         assert abs(ra["policy_loss"] - rb["policy_loss"]) < 1e-4 and abs(ra["value_loss"] - rb["value_loss"]) < 1e-3 * (
             1 + abs(rb["value_loss"]))
     env.close()
+
+
+def _graphed_world2_worker(rank, world, port, out_dir):
+    import os
+    import torch.distributed as dist
+    from mujocoposelearning_amd.model import HsModel
+    from mujocoposelearning_amd.ppo import PPO
+    from mujocoposelearning_amd.vec_env import HumanoidVecEnv
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)     # both ranks share the one GPU
+    calls = []
+    real = dist.all_reduce
+
+    def counting(t, *a, **k):
+        calls.append(t.numel())
+        return real(t, *a, **k)
+    dist.all_reduce = counting
+    try:
+        env = HumanoidVecEnv({"model_path": XML, "duration": 10.0, "reward_config": {"type": "stand"},
+                              "frame_skip": 3}, n_envs=256, model=HsModel(XML), seed=10 + rank)
+        kw = dict(n_steps=8, batch_size=1024, n_epochs=2, seed=0,
+                  policy_kwargs={"activation_fn": "ReLU", "net_arch": {"pi": [64, 64], "vf": [64, 64]}})
+        pa, pb = PPO(env, **kw), PPO(env, **kw)
+        pb.graphs = False
+        adv, ret = pa.collect_rollouts()
+        for k in pa.buf:
+            pb.buf[k].copy_(pa.buf[k])
+        for p in (pa, pb):
+            torch.manual_seed(7)
+            p.train(adv, ret)
+        flat = [torch.cat([q.detach().reshape(-1) for q in p.policy.parameters()]).cpu() for p in (pa, pb)]
+        torch.save({"graphed": flat[0], "eager": flat[1], "calls": calls}, os.path.join(out_dir, f"r{rank}.pt"))
+        env.close()
+    finally:
+        dist.all_reduce = real
+        dist.destroy_process_group()
+
+
+def test_graphed_update_world2_allreduce(tmp_path):
+    """world 2 (gloo rehearsal, two ranks on one GPU): the graphed update packs the gradient
+    bucket in G1, all-reduces it once per optimizer step between the replays, and ends with the
+    same weights as the eager update on both ranks."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.start_processes(_graphed_world2_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    r = [torch.load(tmp_path / f"r{i}.pt", weights_only=True) for i in range(2)]
+    assert torch.equal(r[0]["graphed"], r[1]["graphed"]), "ranks diverged in the graphed update"
+    assert torch.allclose(r[0]["graphed"], r[0]["eager"], rtol=1e-4, atol=1e-6)
+    n = r[0]["graphed"].numel()
+    # 2 epochs x (8 x 256 / 1024) minibatches, graphed + eager: 8 buckets of n
+    assert r[0]["calls"] == [n] * 8
