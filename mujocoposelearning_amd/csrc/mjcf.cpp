@@ -401,6 +401,10 @@ struct Compiler {
       for (double x : nums(k->get(a))) if (x != 0) return false;
       return true;
     };
+    if (!is("solver", "Newton")) {
+      err = "only solver=\"Newton\" is supported (MuJoCo default, what the reference runs; PGS is in the oracle only)";
+      return false;
+    }
     if (!is("integrator", "Euler")) { err = "only integrator=\"Euler\" is supported (reference: MuJoCo default)"; return false; }
     if (!is("cone", "pyramidal")) { err = "only cone=\"pyramidal\" is supported"; return false; }
     if (k->get("impratio") && nums(k->get("impratio"))[0] != 1.0) { err = "only impratio=1 is supported"; return false; }

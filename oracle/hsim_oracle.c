@@ -768,6 +768,75 @@ static void solve_newton(const OrcModel* m, OrcData* d) {
   }
 }
 
+/* ------------------------------------------------------------------ PGS solver */
+/* mj_solPGS (engine_solver.c, MuJoCo 3.2.5) for scalar inequality rows (joint/tendon limits,
+ * frictionless contacts, pyramidal edges -- every row this model class produces): projected
+ * Gauss-Seidel on the dual
+ *   min_f 0.5 f' AR f + f' b  s.t. f >= 0,   AR = J M^-1 J' + diag(R),  b = J qacc_smooth - aref,
+ * sweeping the rows in efc order, f_i <- max(0, f_i - (AR_i f + b_i) / AR_ii), until a sweep's cost
+ * decrease times scale = 1 / (meaninertia max(1, nv)) falls below the tolerance.  Warm start
+ * (mj_fwdConstraint): the forces the primal map assigns to qacc_warmstart, f = -D (J a - aref)_-,
+ * kept only if their dual cost is negative (else f = 0).  Then qacc = qacc_smooth + M^-1 J' f.
+ * The dual of this problem is the primal Newton minimises, so both give the same forces at
+ * convergence (tests/test_oracle_physics.py::test_pgs_and_newton_converge_to_same_forces). */
+static void solve_pgs(const OrcModel* m, OrcData* d) {
+  int nv = m->nv, ne = d->nefc;
+  static double L[OMAXV][OMAXV], MJ[OMAXEFC][OMAXV], AR[OMAXEFC][OMAXEFC];
+  double b[OMAXEFC], f[OMAXEFC];
+  chol(L, d->qM, nv);
+  for (int r = 0; r < ne; r++) chol_solve(MJ[r], L, d->efc_J[r], nv);
+  for (int i = 0; i < ne; i++) {
+    for (int k = 0; k <= i; k++) {
+      double t = 0;
+      for (int j = 0; j < nv; j++) t += d->efc_J[i][j] * MJ[k][j];
+      AR[i][k] = AR[k][i] = t;
+    }
+    AR[i][i] += d->efc_R[i];
+    double t = -d->efc_aref[i];
+    for (int j = 0; j < nv; j++) t += d->efc_J[i][j] * d->qacc_smooth[j];
+    b[i] = t;
+  }
+  /* warm start from qacc_warmstart through the primal force map */
+  double cost = 0;
+  for (int i = 0; i < ne; i++) {
+    double jar = -d->efc_aref[i];
+    for (int j = 0; j < nv; j++) jar += d->efc_J[i][j] * d->qacc_warmstart[j];
+    f[i] = jar < 0 ? -d->efc_D[i] * jar : 0;
+  }
+  for (int i = 0; i < ne; i++) {
+    double t = 0;
+    for (int k = 0; k < ne; k++) t += AR[i][k] * f[k];
+    cost += f[i] * (0.5 * t + b[i]);
+  }
+  if (cost > 0) memset(f, 0, sizeof(double) * ne);
+  double scale = 1.0 / (m->meaninertia * (nv > 1 ? nv : 1));
+  int it;
+  for (it = 0; it < m->iterations;) {
+    double improvement = 0;
+    for (int i = 0; i < ne; i++) {
+      double res = b[i];
+      for (int k = 0; k < ne; k++) res += AR[i][k] * f[k];
+      double ari = AR[i][i] < MINVAL ? MINVAL : AR[i][i];
+      double old = f[i], nf = old - res / ari;
+      if (nf < 0) nf = 0;
+      double delta = nf - old;
+      f[i] = nf;
+      improvement -= delta * res + 0.5 * AR[i][i] * delta * delta;
+    }
+    it++;
+    if (improvement * scale < m->tolerance) break;
+  }
+  d->solver_niter = it;
+  memset(d->qfrc_constraint, 0, sizeof(double) * nv);
+  for (int r = 0; r < ne; r++) {
+    d->efc_force[r] = f[r];
+    for (int k = 0; k < nv; k++) d->qfrc_constraint[k] += d->efc_J[r][k] * f[r];
+  }
+  double dq[OMAXV];
+  chol_solve(dq, L, d->qfrc_constraint, nv);
+  for (int k = 0; k < nv; k++) d->qacc[k] = d->qacc_smooth[k] + dq[k];
+}
+
 /* ------------------------------------------------------------------ mj_forward */
 void orc_forward(const OrcModel* m, OrcData* d) {
   int nv = m->nv;
@@ -790,6 +859,8 @@ void orc_forward(const OrcModel* m, OrcData* d) {
     memcpy(d->qacc, d->qacc_smooth, sizeof(double) * nv);
     memset(d->qfrc_constraint, 0, sizeof(double) * nv);
     d->solver_niter = 0;
+  } else if (m->solver == 1) {
+    solve_pgs(m, d);
   } else {
     solve_newton(m, d);
   }

@@ -21,6 +21,7 @@ typedef struct {
   int nq, nv, nu, nbody, njnt, ngeom, ntendon, npair;
   double timestep, gravity[3], impratio, tolerance, meaninertia;
   int iterations;
+  int solver;                                  /* 0 = Newton (MuJoCo default), 1 = PGS */
   int body_parentid[OMAXB], body_rootid[OMAXB], body_weldid[OMAXB];
   int body_jntnum[OMAXB], body_jntadr[OMAXB], body_dofnum[OMAXB], body_dofadr[OMAXB];
   double body_pos[OMAXB][3], body_quat[OMAXB][4], body_ipos[OMAXB][3];

@@ -172,6 +172,10 @@ def compile_mjcf(path):
     gravity = np.array([float(x) for x in o.get("gravity", "0 0 -9.81").split()])
     iterations = int(float(o.get("iterations", 100)))
     tolerance = float(o.get("tolerance", 1e-8))
+    solvers = {"Newton": 0, "PGS": 1}
+    if o.get("solver", "Newton") not in solvers:
+        raise ValueError("only solver='Newton' (MuJoCo default) or 'PGS' is supported")
+    solver = solvers[o.get("solver", "Newton")]
     # options that change the dynamics beyond what the restatement covers are rejected, not ignored
     if o.get("integrator", "Euler") != "Euler":
         raise ValueError("only integrator='Euler' is supported")
@@ -278,6 +282,7 @@ def compile_mjcf(path):
     M["opt_impratio"] = 1.0
     M["opt_tolerance"] = tolerance
     M["opt_iterations"] = iterations
+    M["opt_solver"] = solver
     M["opt_ls_iterations"] = 50
     M["nbody"], M["njnt"], M["ngeom"] = nbody, njnt, ngeom
     M["body_name"] = [b["name"] for b in bodies]

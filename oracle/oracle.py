@@ -32,7 +32,7 @@ class OrcModel(C.Structure):
     _fields_ = [
         ("nq", I), ("nv", I), ("nu", I), ("nbody", I), ("njnt", I), ("ngeom", I), ("ntendon", I), ("npair", I),
         ("timestep", D), ("gravity", _a(D, 3)), ("impratio", D), ("tolerance", D), ("meaninertia", D),
-        ("iterations", I),
+        ("iterations", I), ("solver", I),
         ("body_parentid", _a(I, OMAXB)), ("body_rootid", _a(I, OMAXB)), ("body_weldid", _a(I, OMAXB)),
         ("body_jntnum", _a(I, OMAXB)), ("body_jntadr", _a(I, OMAXB)), ("body_dofnum", _a(I, OMAXB)),
         ("body_dofadr", _a(I, OMAXB)),
@@ -155,6 +155,7 @@ def pack_model(M):
     om.tolerance = M["opt_tolerance"]
     om.meaninertia = M["stat_meaninertia"]
     om.iterations = M["opt_iterations"]
+    om.solver = M.get("opt_solver", 0)
     for k in ("body_parentid", "body_rootid", "body_weldid", "body_jntnum", "body_jntadr", "body_dofnum",
               "body_dofadr", "body_pos", "body_quat", "body_ipos", "body_mass", "body_subtreemass",
               "body_invweight0", "jnt_type", "jnt_qposadr", "jnt_dofadr", "jnt_bodyid", "jnt_limited",

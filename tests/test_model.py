@@ -172,3 +172,22 @@ def test_unsupported_options_fail_loudly_in_both_compilers(tmp_path, option):
         HsModel(p)
     with pytest.raises(ValueError):
         compile_mjcf(p)
+
+
+@pytest.mark.parametrize("solver", ["PGS", "CG"])
+def test_non_newton_solvers_rejected_by_the_engine(tmp_path, solver):
+    """The engine runs MuJoCo's default Newton solver (what the reference's humanoid.xml gets); an
+    explicit other solver is an error, never silently replaced.  The oracle accepts PGS (checker
+    cross-validation, tests/test_oracle_physics.py) and rejects CG."""
+    from mujocoposelearning_amd._lib import HsimError
+    from mujocoposelearning_amd.model import HsModel
+    from oracle.model import compile_mjcf
+    p = _variant(tmp_path, f'<option solver="{solver}"/>')
+    with pytest.raises(HsimError, match="solver"):
+        HsModel(p)
+    if solver == "CG":
+        with pytest.raises(ValueError):
+            compile_mjcf(p)
+    else:
+        assert compile_mjcf(p)["opt_solver"] == 1
+    assert HsModel(_variant(tmp_path, '<option solver="Newton"/>')) is not None

@@ -345,3 +345,56 @@ def test_full_flag_off_keeps_reference_zeros(orc):
     for _ in range(50):
         orc.step(None, 1)
     assert not orc.get("cfrc_ext").any() and not orc.get("subtree_linvel").any()
+
+
+def _pgs_vs_newton_state(key, seed):
+    from oracle.oracle import Oracle, pack_model
+    out = []
+    for solver in (0, 1):
+        o = Oracle(XML)
+        o.M = dict(o.M, opt_solver=solver, opt_iterations=20000 if solver else 100, opt_tolerance=1e-30)
+        o.m = pack_model(o.M)
+        o.reset_data()
+        q = o.M["keyframes"][key].copy()
+        q[2] -= 0.005
+        o.qpos[:] = q
+        o.qvel[:] = np.random.default_rng(seed).normal(0, 0.5, 27)
+        o.forward()
+        ne = o.d.nefc
+        out.append((o.arr("efc_force", ne).copy(), o.get("qacc"), o.d.solver_niter, ne))
+    return out
+
+
+@pytest.mark.parametrize("key,seed", [("squat", 1), ("prone", 2), ("supine", 3), ("stand_on_left_leg", 4)])
+def test_pgs_and_newton_converge_to_same_forces(key, seed):
+    """the primal Newton solver (MuJoCo default, what the reference runs) and
+    the dual PGS solver (<option solver="PGS">) solve the same convex problem, so at convergence
+    they give the same constraint forces and accelerations -- an independent check of the Newton
+    solve that does not reuse its active-set logic."""
+    (fn, an, itn, ne), (fp, ap, itp, ne2) = _pgs_vs_newton_state(key, seed)
+    assert ne == ne2 and ne > 0 and itp > 10
+    scale = max(1.0, np.abs(fn).max())
+    # measured: <= 2.4e-12 absolute on forces up to 1.2e3 (Newton 2-5 iterations, PGS 150-20000 sweeps)
+    assert np.abs(fp - fn).max() < 1e-9 * scale, np.abs(fp - fn).max()
+    assert np.abs(ap - an).max() < 1e-9 * max(1.0, np.abs(an).max())
+
+
+def test_pgs_stopping_rule_and_option_parsing(tmp_path):
+    """<option solver="PGS" iterations tolerance> reaches the oracle; the default tolerance stops
+    PGS early (MuJoCo's improvement * scale < tolerance rule), and unknown solvers are rejected."""
+    from oracle.model import compile_mjcf
+    from oracle.oracle import Oracle
+    src = open(XML).read()
+    x = tmp_path / "pgs.xml"
+    x.write_text(src.replace('<option timestep="0.005"/>', '<option timestep="0.005" solver="PGS" iterations="50"/>'))
+    o = Oracle(str(x))
+    assert o.m.solver == 1 and o.m.iterations == 50
+    q = o.M["keyframes"]["prone"].copy()
+    q[2] -= 0.005
+    o.qpos[:] = q
+    o.forward()
+    assert 0 < o.d.solver_niter <= 50 and o.d.nefc > 0
+    bad = tmp_path / "cg.xml"
+    bad.write_text(src.replace('<option timestep="0.005"/>', '<option timestep="0.005" solver="CG"/>'))
+    with pytest.raises(ValueError, match="solver"):
+        compile_mjcf(str(bad))
