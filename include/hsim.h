@@ -159,18 +159,19 @@ int hs_ppo_act(const float* mean, int mean_ld, const float* value, int value_ld,
                float* actions_clipped, float* log_prob, float* values, float* episode_starts_out, int N, int A,
                void* stream);
 /* The rest of the PPO rollout step after the env step, over N envs: reward [N] float32,
- * terminated / truncated [N] uint8, terminal_value [N] = V(terminal obs) float32.  Writes
- * reward_out = reward + gamma * terminal_value where truncated && !terminated (else reward),
- * done_out = terminated || truncated (uint8), ep_acc += reward (float64, zeroed where done, after
- * ep_return_out = the accumulated value is written) and episode_start = done (float32).  Copies
- * obs_floats float32 from obs to obs_out (the next rollout-buffer slot; NULL obs skips it).
- * Asynchronous on `stream`. */
+ * terminated / truncated [N] uint8.  boot = truncated && !terminated (TimeLimit.truncated).
+ * Immediate bootstrap: terminal_value [N] = V(terminal obs) given -> reward_out = reward +
+ * gamma * terminal_value where boot (else reward).  Deferred bootstrap: terminal_value NULL ->
+ * reward_out = reward, boot_out [N] uint8 = boot, and for boot envs the terminal_obs row (obs_dim
+ * float32) is copied to boot_obs_out (row n); the caller adds gamma V(row) at the end of the
+ * rollout.  Both: done_out = terminated || truncated (uint8), ep_acc += reward (float64, zeroed
+ * where done, after ep_return_out = the accumulated value is written), episode_start = done
+ * (float32), and obs_floats float32 copied from obs to obs_out (the next rollout-buffer slot;
+ * NULL obs skips it).  Asynchronous on `stream`. */
 int hs_ppo_post(const float* reward, const uint8_t* terminated, const uint8_t* truncated, const float* terminal_value,
-                float gamma, const float* obs, float* obs_out, uint64_t obs_floats, float* reward_out,
-                uint8_t* done_out, double* ep_acc, double* ep_return_out, float* episode_start, int N, void* stream);
-/* out[c] = sum_r x[r][c] over a row-major [rows][cols] float32 device matrix, in a fixed
- * summation order (deterministic).  `workspace` must hold hs_colsum_workspace(rows, cols) floats
- * (may be NULL when that is 0).  Asynchronous on `stream`. */
+                const float* terminal_obs, float* boot_obs_out, uint8_t* boot_out, int obs_dim, float gamma,
+                const float* obs, float* obs_out, uint64_t obs_floats, float* reward_out, uint8_t* done_out,
+                double* ep_acc, double* ep_return_out, float* episode_start, int N, void* stream);
 /* logp[n] = sum_j (-z^2/2 - log_std[j]) - A log(sqrt(2 pi)), z = (actions[n][j] - mean[n][j]) /
  * exp(log_std[j]); mean [N][mean_ld], actions [N][A] contiguous, A <= 32.  The backward, given
  * g_logp [N]: g_mean[n][j] = g z / sigma and gls_rows[n][j] = g (z^2 - 1), whose column sums
@@ -179,6 +180,9 @@ int hs_gauss_logp(const float* mean, int mean_ld, const float* actions, const fl
                   int A, void* stream);
 int hs_gauss_logp_grad(const float* mean, int mean_ld, const float* actions, const float* log_std,
                        const float* g_logp, float* g_mean, float* gls_rows, int N, int A, void* stream);
+/* out[c] = sum_r x[r][c] over a row-major [rows][cols] float32 device matrix, in a fixed
+ * summation order (deterministic).  `workspace` must hold hs_colsum_workspace(rows, cols) floats
+ * (may be NULL when that is 0).  Asynchronous on `stream`. */
 uint64_t hs_colsum_workspace(uint64_t rows, uint64_t cols);
 int hs_colsum(const float* x, uint64_t rows, uint64_t cols, float* workspace, float* out, void* stream);
 const char* hs_last_error(void);

@@ -424,18 +424,20 @@ int hs_ppo_act(const float* mean, int mean_ld, const float* value, int value_ld,
 }
 
 int hs_ppo_post(const float* reward, const uint8_t* terminated, const uint8_t* truncated, const float* terminal_value,
-                float gamma, const float* obs, float* obs_out, uint64_t obs_floats, float* reward_out,
-                uint8_t* done_out, double* ep_acc, double* ep_return_out, float* episode_start, int N, void* stream) {
+                const float* terminal_obs, float* boot_obs_out, uint8_t* boot_out, int obs_dim, float gamma,
+                const float* obs, float* obs_out, uint64_t obs_floats, float* reward_out, uint8_t* done_out,
+                double* ep_acc, double* ep_return_out, float* episode_start, int N, void* stream) {
   if (N < 0) return fail("hs_ppo_post: negative size");
   if (N == 0) return 0;
-  if (!reward || !terminated || !truncated || !terminal_value || !reward_out || !done_out || !ep_acc ||
-      !ep_return_out || !episode_start)
+  if (!reward || !terminated || !truncated || !reward_out || !done_out || !ep_acc || !ep_return_out || !episode_start)
     return fail("hs_ppo_post: null buffer");
+  if (!terminal_value && (!terminal_obs || !boot_obs_out || !boot_out || obs_dim < 1))
+    return fail("hs_ppo_post: need terminal_value, or terminal_obs + boot_obs_out + boot_out + obs_dim (deferred)");
   if (!obs) obs_floats = 0;
   if (obs_floats && !obs_out) return fail("hs_ppo_post: null obs_out");
-  return hip_ok(hs::launch_ppo_post(reward, terminated, truncated, terminal_value, gamma, obs, obs_out,
-                                    (size_t)obs_floats, reward_out, done_out, ep_acc, ep_return_out, episode_start, N,
-                                    (hipStream_t)stream),
+  return hip_ok(hs::launch_ppo_post(reward, terminated, truncated, terminal_value, terminal_obs, boot_obs_out, boot_out,
+                                    obs_dim, gamma, obs, obs_out, (size_t)obs_floats, reward_out, done_out, ep_acc,
+                                    ep_return_out, episode_start, N, (hipStream_t)stream),
                 "ppo_post_kernel")
              ? 0
              : -1;

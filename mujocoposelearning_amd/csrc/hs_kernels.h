@@ -72,9 +72,10 @@ hipError_t launch_ppo_act(const float* mean, int mean_ld, const float* value, in
                           float* act_clip, float* logp, float* val, float* start_out, int N, int A,
                           hipStream_t stream);
 hipError_t launch_ppo_post(const float* reward, const uint8_t* terminated, const uint8_t* truncated,
-                           const float* terminal_value, float gamma, const float* obs, float* obs_out, size_t obs_floats,
-                           float* reward_out, uint8_t* done_out, double* ep_acc, double* ep_return_out,
-                           float* episode_start, int N, hipStream_t stream);
+                           const float* terminal_value, const float* terminal_obs, float* boot_obs_out,
+                           uint8_t* boot_out, int obs_dim, float gamma, const float* obs, float* obs_out,
+                           size_t obs_floats, float* reward_out, uint8_t* done_out, double* ep_acc,
+                           double* ep_return_out, float* episode_start, int N, hipStream_t stream);
 // column sums of a row-major [rows][cols] float32 matrix (ppo.hip); workspace of
 // colsum_workspace(rows, cols) floats (0: none needed)
 size_t colsum_workspace(size_t rows, size_t cols);

@@ -10,7 +10,8 @@
 //                    the rollout-buffer writes of step t (actions, values, log_probs,
 //                    episode_starts; common/buffers.py RolloutBuffer.add)
 //   ppo_post_kernel  the step's reward bookkeeping: time-limit bootstrap
-//                    r += gamma V(terminal_obs) for envs with TimeLimit.truncated
+//                    r += gamma V(terminal_obs) for envs with TimeLimit.truncated (or, deferred,
+//                    the boot flags and terminal-obs rows for one batched V at rollout end)
 //                    (on_policy_algorithm.py: infos[idx]["TimeLimit.truncated"]), dones,
 //                    episode-return accumulation, the new episode_starts, and the copy of the
 //                    next observation into the rollout buffer's slot t+1
@@ -101,12 +102,15 @@ __global__ __launch_bounds__(256) void ppo_act_kernel(const float* __restrict__ 
 __global__ __launch_bounds__(256) void ppo_post_kernel(const float* __restrict__ reward,
                                                        const uint8_t* __restrict__ terminated,
                                                        const uint8_t* __restrict__ truncated,
-                                                       const float* __restrict__ terminal_value, float gamma,
+                                                       const float* __restrict__ terminal_value,
+                                                       const float* __restrict__ terminal_obs,
+                                                       float* __restrict__ boot_obs_out,
+                                                       uint8_t* __restrict__ boot_out, float gamma,
                                                        const float* __restrict__ obs, float* __restrict__ obs_out,
                                                        size_t obs_n, int vec4, float* __restrict__ reward_out,
                                                        uint8_t* __restrict__ done_out, double* __restrict__ ep_acc,
                                                        double* __restrict__ ep_return_out,
-                                                       float* __restrict__ episode_start, int N) {
+                                                       float* __restrict__ episode_start, int N, int obs_dim) {
   const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   if (vec4) {   // 16 B-aligned pointers, obs_n = floats / 4
@@ -119,8 +123,19 @@ __global__ __launch_bounds__(256) void ppo_post_kernel(const float* __restrict__
   if (gid < (size_t)N) {
     const bool term = terminated[gid] != 0, trunc = truncated[gid] != 0;
     const float r = reward[gid];
-    // TimeLimit.truncated = truncated and not terminated: bootstrap from V(terminal obs)
-    reward_out[gid] = (trunc && !term) ? r + gamma * terminal_value[gid] : r;
+    // TimeLimit.truncated = truncated and not terminated: bootstrap from V(terminal obs), now
+    // (terminal_value given) or deferred to the end of the rollout (boot flag + the terminal obs
+    // row kept in boot_obs_out; rows are copied only for the rare boot envs)
+    const bool boot = trunc && !term;
+    if (terminal_value) {
+      reward_out[gid] = boot ? r + gamma * terminal_value[gid] : r;
+    } else {
+      reward_out[gid] = r;
+      boot_out[gid] = boot;
+      if (boot)
+        for (int k = 0; k < obs_dim; k++)
+          boot_obs_out[gid * obs_dim + k] = terminal_obs[gid * obs_dim + k];
+    }
     const bool done = term || trunc;
     const double acc = ep_acc[gid] + (double)r;
     done_out[gid] = done;
@@ -243,9 +258,10 @@ hipError_t launch_ppo_act(const float* mean, int mean_ld, const float* value, in
 }
 
 hipError_t launch_ppo_post(const float* reward, const uint8_t* terminated, const uint8_t* truncated,
-                           const float* terminal_value, float gamma, const float* obs, float* obs_out, size_t obs_floats,
-                           float* reward_out, uint8_t* done_out, double* ep_acc, double* ep_return_out,
-                           float* episode_start, int N, hipStream_t stream) {
+                           const float* terminal_value, const float* terminal_obs, float* boot_obs_out,
+                           uint8_t* boot_out, int obs_dim, float gamma, const float* obs, float* obs_out,
+                           size_t obs_floats, float* reward_out, uint8_t* done_out, double* ep_acc,
+                           double* ep_return_out, float* episode_start, int N, hipStream_t stream) {
   if (N <= 0) return hipSuccess;
   const int vec4 = obs_floats % 4 == 0 && ((uintptr_t)obs | (uintptr_t)obs_out) % 16 == 0;
   const size_t obs_n = vec4 ? obs_floats / 4 : obs_floats;
@@ -256,8 +272,8 @@ hipError_t launch_ppo_post(const float* reward, const uint8_t* terminated, const
   if (blocks > 2048) blocks = 2048;
   if (blocks * block < (size_t)N) blocks = ((size_t)N + block - 1) / block;
   hipLaunchKernelGGL(ppo_post_kernel, dim3((unsigned)blocks), dim3(block), 0, stream, reward, terminated, truncated,
-                     terminal_value, gamma, obs, obs_out, obs_n, vec4, reward_out, done_out, ep_acc, ep_return_out,
-                     episode_start, N);
+                     terminal_value, terminal_obs, boot_obs_out, boot_out, gamma, obs, obs_out, obs_n, vec4,
+                     reward_out, done_out, ep_acc, ep_return_out, episode_start, N, obs_dim);
   return hipGetLastError();
 }
 

@@ -276,17 +276,27 @@ def ppo_act(mean, value, log_std, episode_start, seed, counter, deterministic, a
 
 
 def ppo_post(reward, terminated, truncated, terminal_value, gamma, obs, obs_out, reward_out, done_out, ep_acc,
-             ep_return_out, episode_start, stream=None):
-    """hs_ppo_post on device tensors (ppo.hip): reward bootstrap, dones, returns, next obs copy."""
+             ep_return_out, episode_start, terminal_obs=None, boot_obs_out=None, boot_out=None, stream=None):
+    """hs_ppo_post on device tensors (ppo.hip): reward bootstrap, dones, returns, next obs copy.
+    terminal_value None = deferred bootstrap: boot flags -> boot_out, terminal-obs rows of the
+    boot envs -> boot_obs_out (the caller adds gamma V(row) at the end of the rollout)."""
     from . import _lib
     N = reward.shape[0]
     assert terminated.dtype == torch.uint8 and truncated.dtype == torch.uint8 and done_out.dtype == torch.bool
     assert ep_acc.dtype == torch.float64 and ep_return_out.dtype == torch.float64
     assert obs.is_contiguous() and obs_out.is_contiguous() and obs.numel() == obs_out.numel()
+    ptr = lambda t: None if t is None else t.data_ptr()     # noqa: E731
+    D = 0
+    if terminal_value is None:
+        assert terminal_obs.is_contiguous() and boot_obs_out.is_contiguous() and boot_out.dtype in (torch.bool,
+                                                                                                torch.uint8)
+        D = terminal_obs.shape[1]
+        assert boot_obs_out.shape == terminal_obs.shape == (N, D)
     st = torch.cuda.current_stream(reward.device).cuda_stream if stream is None else stream
     _lib.check(_lib.lib().hs_ppo_post(reward.data_ptr(), terminated.data_ptr(), truncated.data_ptr(),
-                                      terminal_value.data_ptr(), float(gamma), obs.data_ptr(), obs_out.data_ptr(),
-                                      obs.numel(), reward_out.data_ptr(), done_out.data_ptr(), ep_acc.data_ptr(),
+                                      ptr(terminal_value), ptr(terminal_obs), ptr(boot_obs_out), ptr(boot_out), D,
+                                      float(gamma), obs.data_ptr(), obs_out.data_ptr(), obs.numel(),
+                                      reward_out.data_ptr(), done_out.data_ptr(), ep_acc.data_ptr(),
                                       ep_return_out.data_ptr(), episode_start.data_ptr(), N, st))
 
 
@@ -340,6 +350,9 @@ class PPO:
                         val=torch.zeros(T, N, dtype=f, device=dev), logp=torch.zeros(T, N, dtype=f, device=dev),
                         done=torch.zeros(T, N, dtype=torch.bool, device=dev),
                         epret=torch.zeros(T, N, dtype=torch.float64, device=dev))
+        if dev.type == "cuda":   # device rollout: deferred TimeLimit bootstrap (flags + terminal obs rows)
+            self.buf.update(boot=torch.zeros(T, N, dtype=torch.bool, device=dev),
+                            tobs=torch.zeros(T, N, D, dtype=f, device=dev))
         self.obs = env.reset_tensors().float().clone()
         self.episode_start = torch.ones(N, dtype=f, device=dev)
         self.num_timesteps = 0
@@ -359,9 +372,11 @@ class PPO:
 
     def _collect_rollouts_device(self):
         """collect_rollouts on the GPU: per env step the packed policy GEMM chain, one hs_ppo_act
-        launch (sample, log-prob, clip, buffer writes), the env kernel, the value of the terminal
-        obs (three GEMMs) and one hs_ppo_post launch (bootstrap, dones, returns, obs -> slot t+1).
-        No host synchronisation inside the loop."""
+        launch (sample, log-prob, clip, buffer writes), the env kernel and one hs_ppo_post launch
+        (dones, returns, obs -> slot t+1, and the TimeLimit.truncated envs' flags and terminal obs).
+        No host synchronisation inside the loop.  The bootstrap r += gamma V(terminal obs) of the
+        truncated envs is applied once after the loop, with one value forward over just those rows
+        (the policy is fixed during the rollout, so this equals SB3's per-step evaluation)."""
         b, env, pol = self.buf, self.env, self.policy
         T, N = self.n_steps, env.num_envs
         pol.pack_heads()
@@ -373,11 +388,14 @@ class PPO:
                     b["act"][t], self._act_clip, b["logp"][t], b["val"][t], b["start"][t])
             self._noise_counter += 1
             obs, rew, term, trunc = env.step_tensors(self._act_clip)
-            tv = pol.value(env.terminal_obs.float())
             nxt = b["obs"][t + 1] if t + 1 < T else self.obs
-            ppo_post(rew.float(), term.to(torch.uint8), trunc.to(torch.uint8), tv, gamma, obs.float(), nxt,
-                     b["rew"][t], b["done"][t], self.ep_acc, b["epret"][t], self.episode_start)
+            ppo_post(rew.float(), term.to(torch.uint8), trunc.to(torch.uint8), None, gamma, obs.float(), nxt,
+                     b["rew"][t], b["done"][t], self.ep_acc, b["epret"][t], self.episode_start,
+                     terminal_obs=env.terminal_obs.float(), boot_obs_out=b["tobs"][t], boot_out=b["boot"][t])
         self.ep_returns += b["epret"][b["done"]].tolist()      # one device -> host transfer per rollout
+        boot = b["boot"].view(-1).nonzero().squeeze(1)
+        if boot.numel():                                        # deferred TimeLimit bootstrap
+            b["rew"].view(-1)[boot] += self.gamma * pol.value(b["tobs"].view(T * N, -1)[boot])
         self.num_timesteps += T * N * self.world_size
         last_v = pol.value(self.obs)
         return gae(b["rew"], b["val"], b["start"], last_v, self.episode_start, self.gamma, self.gae_lambda)

@@ -68,7 +68,8 @@ def test_ppo_act_rejects_bad_shapes():
     assert L.hs_ppo_act(None, 40, None, 1, None, None, 0, 0, 0, None, None, None, None, None, 8, 33, None) < 0
     assert b"A <= 32" in L.hs_last_error()
     assert L.hs_ppo_act(None, 4, None, 1, None, None, 0, 0, 0, None, None, None, None, None, 8, 8, None) < 0
-    assert L.hs_ppo_post(None, None, None, None, 0.9, None, None, 0, None, None, None, None, None, 4, None) < 0
+    assert L.hs_ppo_post(None, None, None, None, None, None, None, 0, 0.9, None, None, 0, None, None, None, None, None,
+                         4, None) < 0
 
 
 def test_ppo_post_matches_torch_bookkeeping():
@@ -90,6 +91,15 @@ def test_ppo_post_matches_torch_bookkeeping():
         epret = torch.zeros(N, dtype=torch.float64, device="cuda")
         start = torch.full((N,), 0.5, device="cuda")
         ppo_post(rew, term, trunc, tv, gamma, o, obs_out, rew_out, done, acc, epret, start)
+        # deferred mode: raw rewards, boot flags and the boot envs' terminal-obs rows
+        tobs = torch.randn(N, 7, device="cuda", generator=g)
+        bobs = torch.zeros(N, 7, device="cuda")
+        bflag = torch.zeros(N, dtype=torch.bool, device="cuda")
+        rew_d = torch.zeros(N, device="cuda")
+        acc_d = acc0.clone()
+        ppo_post(rew, term, trunc, None, gamma, o, torch.zeros_like(o), rew_d, torch.zeros_like(done), acc_d,
+                 torch.zeros_like(epret), torch.zeros_like(start), terminal_obs=tobs, boot_obs_out=bobs,
+                 boot_out=bflag)
         torch.cuda.synchronize()
         # the torch restatement (PPO._collect_rollouts_torch)
         t, tr = term.bool(), trunc.bool()
@@ -101,6 +111,12 @@ def test_ppo_post_matches_torch_bookkeeping():
         assert torch.equal(done, d_ref) and torch.equal(epret, acc_ref)
         assert torch.equal(acc, acc_ref.masked_fill(d_ref, 0.0)) and torch.equal(start, d_ref.float())
         assert torch.equal(obs_out, o)
+        bt = tr & ~t
+        assert torch.equal(rew_d, rew) and torch.equal(bflag, bt) and torch.equal(acc_d, acc)
+        assert torch.equal(bobs[bt], tobs[bt]) and not bobs[~bt].any()
+        # the deferred bootstrap applied afterwards == the immediate one
+        rew_d[bt] += gamma * tv[bt]
+        assert torch.allclose(rew_d, r_ref, rtol=1e-6, atol=1e-6)
 
 
 def test_device_rollout_buffers_consistent_with_policy():
@@ -255,3 +271,32 @@ def test_graphed_update_world2_allreduce(tmp_path):
     n = r[0]["graphed"].numel()
     # 2 epochs x (8 x 256 / 1024) minibatches, graphed + eager: 8 buckets of n
     assert r[0]["calls"] == [n] * 8
+
+
+def test_device_rollout_deferred_timelimit_bootstrap():
+    """max_steps 10 < duration: every env is truncated (not terminated) at env step 10, so the
+    device rollout's deferred bootstrap must add gamma V(terminal obs) to exactly those rewards
+    (the reference's truncated reward itself is 0, custom_env.py:201-206)."""
+    from mujocoposelearning_amd.model import HsModel
+    from mujocoposelearning_amd.ppo import PPO
+    from mujocoposelearning_amd.vec_env import HumanoidVecEnv
+    env = HumanoidVecEnv({"model_path": XML, "duration": 10.0, "reward_config": {"type": "stand"}, "frame_skip": 3},
+                         n_envs=128, model=HsModel(XML), seed=0)
+    env.batch.configure(max_steps=10)
+    ppo = PPO(env, n_steps=16, batch_size=512, n_epochs=1, seed=0, gamma=0.9,
+              policy_kwargs={"activation_fn": "ReLU", "net_arch": {"pi": [64, 64], "vf": [64, 64]}})
+    ppo.collect_rollouts()
+    b = ppo.buf
+    torch.cuda.synchronize()
+    steps = [t for t in range(16) if bool(b["boot"][t].any())]
+    assert len(steps) == 1 and bool(b["boot"][steps[0]].all()), steps
+    t = steps[0]
+    with torch.no_grad():
+        expect = 0.9 * ppo.policy.value(b["tobs"][t])
+    assert torch.allclose(b["rew"][t], expect, rtol=1e-5, atol=1e-6)
+    assert bool(b["done"][t].all()) and bool((b["start"][t + 1] == 1).all())
+    # the kept terminal obs is the pre-reset state, not the post-reset obs of slot t+1
+    assert float((b["tobs"][t] - b["obs"][t + 1]).abs().max()) > 1e-3
+    others = [k for k in range(16) if k != t]
+    assert not bool(b["tobs"][others].any())
+    env.close()
