@@ -151,11 +151,13 @@ int hs_gae(const float* rewards, const float* values, const float* episode_start
 /* One PPO rollout step's policy sampling and buffer writes over N envs (A <= 32 actions):
  * mean [N][mean_ld] (first A columns), value [N] at stride value_ld, log_std [A], episode_start
  * [N] (all float32 device memory).  actions = mean + exp(log_std) * z with z ~ N(0, 1) from the
- * counter-based Philox4x32-10 stream (seed, counter; z = 0 when deterministic != 0); writes
+ * counter-based Philox4x32-10 stream (seed, counter + *counter_base when counter_base (a device
+ * uint64) is not NULL -- graph replays then draw fresh noise; z = 0 when deterministic != 0); writes
  * actions [N][A] (unclipped, the buffer copy), actions_clipped [N][A] (clip to [-1, 1], what the
  * env steps with), log_prob [N], values [N] and episode_starts_out [N].  Asynchronous on `stream`. */
 int hs_ppo_act(const float* mean, int mean_ld, const float* value, int value_ld, const float* log_std,
-               const float* episode_start, uint64_t seed, uint64_t counter, int deterministic, float* actions,
+               const float* episode_start, uint64_t seed, uint64_t counter, const uint64_t* counter_base,
+               int deterministic, float* actions,
                float* actions_clipped, float* log_prob, float* values, float* episode_starts_out, int N, int A,
                void* stream);
 /* The rest of the PPO rollout step after the env step, over N envs: reward [N] float32,

@@ -75,7 +75,7 @@ def lib():
         "hs_get_debug": (i, [vp, vp, i]),
         "hs_synchronize": (i, [vp]),
         "hs_gae": (i, [vp, vp, vp, vp, vp, vp, vp, i, i, C.c_float, C.c_float, vp]),
-        "hs_ppo_act": (i, [vp, i, vp, i, vp, vp, u64, u64, i, vp, vp, vp, vp, vp, i, i, vp]),
+        "hs_ppo_act": (i, [vp, i, vp, i, vp, vp, u64, u64, vp, i, vp, vp, vp, vp, vp, i, i, vp]),
         "hs_ppo_post": (i, [vp, vp, vp, vp, vp, vp, vp, i, C.c_float, vp, vp, u64, vp, vp, vp, vp, vp, i, vp]),
         "hs_gauss_logp": (i, [vp, i, vp, vp, vp, i, i, vp]),
         "hs_gauss_logp_grad": (i, [vp, i, vp, vp, vp, vp, vp, i, i, vp]),

@@ -406,7 +406,8 @@ int hs_get_debug(hs_batch* b, double* out, int n) {
 }
 
 int hs_ppo_act(const float* mean, int mean_ld, const float* value, int value_ld, const float* log_std,
-               const float* episode_start, uint64_t seed, uint64_t counter, int deterministic, float* actions,
+               const float* episode_start, uint64_t seed, uint64_t counter, const uint64_t* counter_base,
+               int deterministic, float* actions,
                float* actions_clipped, float* log_prob, float* values, float* episode_starts_out, int N, int A,
                void* stream) {
   if (N < 0 || A < 1 || A > 32) return fail("hs_ppo_act: need N >= 0 and 1 <= A <= 32");
@@ -415,7 +416,8 @@ int hs_ppo_act(const float* mean, int mean_ld, const float* value, int value_ld,
   if (!mean || !value || !log_std || !episode_start || !actions || !actions_clipped || !log_prob || !values ||
       !episode_starts_out)
     return fail("hs_ppo_act: null buffer");
-  return hip_ok(hs::launch_ppo_act(mean, mean_ld, value, value_ld, log_std, episode_start, seed, counter, deterministic,
+  return hip_ok(hs::launch_ppo_act(mean, mean_ld, value, value_ld, log_std, episode_start, seed, counter, counter_base,
+                                   deterministic,
                                    actions, actions_clipped, log_prob, values, episode_starts_out, N, A,
                                    (hipStream_t)stream),
                 "ppo_act_kernel")

@@ -68,7 +68,8 @@ hipError_t launch_kinematics(const DevModel<T>* dmodel, int nv, const T* qpos, T
 
 // PPO rollout bookkeeping around the policy GEMMs and the env step (ppo.hip)
 hipError_t launch_ppo_act(const float* mean, int mean_ld, const float* value, int value_ld, const float* log_std,
-                          const float* episode_start, uint64_t seed, uint64_t counter, int deterministic, float* act,
+                          const float* episode_start, uint64_t seed, uint64_t counter, const uint64_t* counter_base,
+                          int deterministic, float* act,
                           float* act_clip, float* logp, float* val, float* start_out, int N, int A,
                           hipStream_t stream);
 hipError_t launch_ppo_post(const float* reward, const uint8_t* terminated, const uint8_t* truncated,

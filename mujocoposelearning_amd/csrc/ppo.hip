@@ -67,7 +67,8 @@ __global__ __launch_bounds__(256) void ppo_act_kernel(const float* __restrict__ 
                                                       const float* __restrict__ value, int value_ld,
                                                       const float* __restrict__ log_std,
                                                       const float* __restrict__ episode_start, uint32_t k0,
-                                                      uint32_t k1, uint32_t c0, uint32_t c1, int deterministic,
+                                                      uint32_t k1, uint64_t counter,
+                                                      const uint64_t* __restrict__ counter_base, int deterministic,
                                                       float* __restrict__ act, float* __restrict__ act_clip,
                                                       float* __restrict__ logp, float* __restrict__ val,
                                                       float* __restrict__ start_out, int N, int A) {
@@ -81,7 +82,8 @@ __global__ __launch_bounds__(256) void ppo_act_kernel(const float* __restrict__ 
     float z = 0.f;
     if (!deterministic) {
       const uint32_t id = (uint32_t)gid;      // env * 32 + action index
-      const U4 r = philox4x32_10(U4{id, (uint32_t)(n >> 27), c0, c1}, k0, k1);
+      const uint64_t c = counter + (counter_base ? *counter_base : 0ull);
+      const U4 r = philox4x32_10(U4{id, (uint32_t)(n >> 27), (uint32_t)c, (uint32_t)(c >> 32)}, k0, k1);
       z = box_muller(r.x, r.y);
     }
     const float a = m + __expf(ls) * z;
@@ -244,7 +246,8 @@ static size_t colsum_chunks(size_t rows, size_t cols) {
 }
 
 hipError_t launch_ppo_act(const float* mean, int mean_ld, const float* value, int value_ld, const float* log_std,
-                          const float* episode_start, uint64_t seed, uint64_t counter, int deterministic, float* act,
+                          const float* episode_start, uint64_t seed, uint64_t counter, const uint64_t* counter_base,
+                          int deterministic, float* act,
                           float* act_clip, float* logp, float* val, float* start_out, int N, int A,
                           hipStream_t stream) {
   if (N <= 0) return hipSuccess;
@@ -252,8 +255,8 @@ hipError_t launch_ppo_act(const float* mean, int mean_ld, const float* value, in
   const int block = 256;
   const dim3 grid((unsigned)((threads + block - 1) / block));
   hipLaunchKernelGGL(ppo_act_kernel, grid, dim3(block), 0, stream, mean, mean_ld, value, value_ld, log_std,
-                     episode_start, (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)counter,
-                     (uint32_t)(counter >> 32), deterministic, act, act_clip, logp, val, start_out, N, A);
+                     episode_start, (uint32_t)seed, (uint32_t)(seed >> 32), counter, counter_base, deterministic, act,
+                     act_clip, logp, val, start_out, N, A);
   return hipGetLastError();
 }
 

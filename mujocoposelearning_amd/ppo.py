@@ -111,6 +111,11 @@ class Linear(nn.Linear):
         return super().forward(x)
 
 
+def _flat_packed(pk):
+    w1, b1, mid, w3, b3 = pk
+    return [w1, b1] + [t for wb in mid for t in wb] + [w3, b3]
+
+
 def _mlp(inp, sizes, act=nn.ReLU):
     layers, d = [], inp
     for s in sizes:
@@ -198,7 +203,13 @@ class ActorCritic(nn.Module):
         b3 = torch.zeros(2, 1, A, device=w1.device, dtype=w1.dtype)
         b3[0, 0] = self.action_net.bias
         b3[1, 0, 0] = self.value_net.bias[0]
-        self._packed = (w1, b1, mid, w3, b3)
+        new = (w1, b1, mid, w3, b3)
+        old = self._packed
+        if old is not None and all(a.shape == b.shape for a, b in zip(_flat_packed(old), _flat_packed(new))):
+            for a, b in zip(_flat_packed(old), _flat_packed(new)):    # in place: captured graphs stay valid
+                a.copy_(b)
+            return old
+        self._packed = new
         return self._packed
 
     @torch.no_grad()
@@ -260,8 +271,10 @@ def gae_device(rewards, values, dones, last_values, last_dones, gamma, lam):
 
 
 def ppo_act(mean, value, log_std, episode_start, seed, counter, deterministic, act_out, act_clip_out, logp_out,
-            val_out, start_out, stream=None):
-    """hs_ppo_act on device tensors (ppo.hip): Gaussian sample + log-prob + clip + buffer writes."""
+            val_out, start_out, stream=None, counter_base=None):
+    """hs_ppo_act on device tensors (ppo.hip): Gaussian sample + log-prob + clip + buffer writes.
+    The Philox counter is ``counter`` plus, if given, the int64 device scalar ``counter_base``
+    (read by the kernel, so a captured graph draws fresh noise on every replay)."""
     from . import _lib
     N, A = act_out.shape
     assert mean.stride(1) == 1 and mean.shape == (N, A) and value.shape == (N,), (mean.shape, value.shape)
@@ -270,7 +283,8 @@ def ppo_act(mean, value, log_std, episode_start, seed, counter, deterministic, a
     st = torch.cuda.current_stream(mean.device).cuda_stream if stream is None else stream
     _lib.check(_lib.lib().hs_ppo_act(mean.data_ptr(), mean.stride(0), value.data_ptr(), value.stride(0),
                                      log_std.data_ptr(), episode_start.data_ptr(), int(seed) & (2 ** 64 - 1),
-                                     int(counter), int(bool(deterministic)), act_out.data_ptr(),
+                                     int(counter), None if counter_base is None else counter_base.data_ptr(),
+                                     int(bool(deterministic)), act_out.data_ptr(),
                                      act_clip_out.data_ptr(), logp_out.data_ptr(), val_out.data_ptr(),
                                      start_out.data_ptr(), N, A, st))
 
@@ -362,7 +376,8 @@ class PPO:
         # device rollout: the clipped actions the env steps with, and the Philox noise stream
         self._act_clip = torch.zeros(N, A, dtype=f, device=dev)
         self._noise_seed = (int(seed) + 7919 * rank) * 0x9E3779B97F4A7C15 % 2 ** 64
-        self._noise_counter = 0
+        self._noise_ctr = torch.zeros(1, dtype=torch.int64, device=dev)    # Philox step counter (device)
+        self._rollout_graph = None
         self.logger = {}
 
     def collect_rollouts(self):
@@ -380,18 +395,12 @@ class PPO:
         b, env, pol = self.buf, self.env, self.policy
         T, N = self.n_steps, env.num_envs
         pol.pack_heads()
-        b["obs"][0].copy_(self.obs)
-        gamma = float(self.gamma)
-        for t in range(T):
-            mean, value = pol.heads(b["obs"][t])
-            ppo_act(mean, value, pol.log_std.detach(), self.episode_start, self._noise_seed, self._noise_counter, False,
-                    b["act"][t], self._act_clip, b["logp"][t], b["val"][t], b["start"][t])
-            self._noise_counter += 1
-            obs, rew, term, trunc = env.step_tensors(self._act_clip)
-            nxt = b["obs"][t + 1] if t + 1 < T else self.obs
-            ppo_post(rew.float(), term.to(torch.uint8), trunc.to(torch.uint8), None, gamma, obs.float(), nxt,
-                     b["rew"][t], b["done"][t], self.ep_acc, b["epret"][t], self.episode_start,
-                     terminal_obs=env.terminal_obs.float(), boot_obs_out=b["tobs"][t], boot_out=b["boot"][t])
+        if self.graphs and self._rollout_graph is None and getattr(env, "graph_safe", False):
+            self._capture_rollout()
+        if self._rollout_graph is not None:
+            self._rollout_graph.replay()
+        else:
+            self._rollout_body()
         self.ep_returns += b["epret"][b["done"]].tolist()      # one device -> host transfer per rollout
         boot = b["boot"].view(-1).nonzero().squeeze(1)
         if boot.numel():                                        # deferred TimeLimit bootstrap
@@ -399,6 +408,44 @@ class PPO:
         self.num_timesteps += T * N * self.world_size
         last_v = pol.value(self.obs)
         return gae(b["rew"], b["val"], b["start"], last_v, self.episode_start, self.gamma, self.gae_lambda)
+
+    def _rollout_body(self):
+        """The T env steps of a device rollout (what the rollout graph captures)."""
+        b, env, pol = self.buf, self.env, self.policy
+        T = self.n_steps
+        gamma = float(self.gamma)
+        b["obs"][0].copy_(self.obs)
+        for t in range(T):
+            mean, value = pol.heads(b["obs"][t])
+            ppo_act(mean, value, pol.log_std.detach(), self.episode_start, self._noise_seed, t, False,
+                    b["act"][t], self._act_clip, b["logp"][t], b["val"][t], b["start"][t],
+                    counter_base=self._noise_ctr)
+            obs, rew, term, trunc = env.step_tensors(self._act_clip)
+            nxt = b["obs"][t + 1] if t + 1 < T else self.obs
+            ppo_post(rew.float(), term.to(torch.uint8), trunc.to(torch.uint8), None, gamma, obs.float(), nxt,
+                     b["rew"][t], b["done"][t], self.ep_acc, b["epret"][t], self.episode_start,
+                     terminal_obs=env.terminal_obs.float(), boot_obs_out=b["tobs"][t], boot_out=b["boot"][t])
+        self._noise_ctr.add_(T)
+
+    def _capture_rollout(self):
+        """Capture the whole T-step device rollout as one HIP graph (policy GEMMs, hs_ppo_act, the
+        env kernel, hs_ppo_post per step): one host call per rollout.  Every pointer it uses is
+        persistent (rollout buffers, the env batch's buffers, pack_heads' weight copies) and the
+        noise counter lives in device memory, so replays are exactly the eager loop.  Only the
+        side-effect-free policy forward is warmed up (GEMM library handles); the env steps are
+        recorded, not executed, during capture."""
+        pol, b, dev = self.policy, self.buf, self.device
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side), torch.no_grad():
+            for _ in range(2):
+                pol.heads(b["obs"][0])
+                pol.value(self.obs)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._rollout_body()
+        self._rollout_graph = g
 
     def _collect_rollouts_torch(self):
         """SB3 PPO.collect_rollouts on device.  No host synchronisation inside the loop: the

@@ -95,6 +95,12 @@ class HumanoidVecEnv(_Base):
         return self.batch.device
 
     @property
+    def graph_safe(self):
+        """step_tensors is launches only (device reward, one stream, no host sync), so a trainer
+        may capture it in a HIP graph."""
+        return self._host_reward is None and getattr(self.batch, "_streams", None) is None
+
+    @property
     def terminal_obs(self):
         """[N, obs_dim] device tensor: pre-reset obs of envs whose episode ended in the last step."""
         return self.batch.terminal_obs

@@ -65,9 +65,9 @@ def test_ppo_act_sample_matches_diag_gaussian_log_prob():
 def test_ppo_act_rejects_bad_shapes():
     from mujocoposelearning_amd import _lib
     L = _lib.lib()
-    assert L.hs_ppo_act(None, 40, None, 1, None, None, 0, 0, 0, None, None, None, None, None, 8, 33, None) < 0
+    assert L.hs_ppo_act(None, 40, None, 1, None, None, 0, 0, None, 0, None, None, None, None, None, 8, 33, None) < 0
     assert b"A <= 32" in L.hs_last_error()
-    assert L.hs_ppo_act(None, 4, None, 1, None, None, 0, 0, 0, None, None, None, None, None, 8, 8, None) < 0
+    assert L.hs_ppo_act(None, 4, None, 1, None, None, 0, 0, None, 0, None, None, None, None, None, 8, 8, None) < 0
     assert L.hs_ppo_post(None, None, None, None, None, None, None, 0, 0.9, None, None, 0, None, None, None, None, None,
                          4, None) < 0
 
@@ -300,3 +300,30 @@ def test_device_rollout_deferred_timelimit_bootstrap():
     others = [k for k in range(16) if k != t]
     assert not bool(b["tobs"][others].any())
     env.close()
+
+
+def test_graphed_rollout_matches_eager_rollout():
+    """The device rollout captured as one HIP graph (PPO._capture_rollout) writes exactly what the
+    eager loop writes: two identical envs + policies, one graphed and one eager, two rollouts
+    each (the second replays the graph with fresh noise and a reset inside)."""
+    from mujocoposelearning_amd.model import HsModel
+    from mujocoposelearning_amd.ppo import PPO
+    from mujocoposelearning_amd.vec_env import HumanoidVecEnv
+    model = HsModel(XML)
+    cfg = {"model_path": XML, "duration": 0.2, "reward_config": {"type": "stand"}, "frame_skip": 3}
+    envs = [HumanoidVecEnv(cfg, n_envs=256, model=model, seed=0) for _ in range(2)]
+    kw = dict(n_steps=12, batch_size=1024, n_epochs=1, seed=0,
+              policy_kwargs={"activation_fn": "ReLU", "net_arch": {"pi": [256, 256], "vf": [256, 256]}})
+    pa, pb = PPO(envs[0], **kw), PPO(envs[1], **kw)
+    pb.graphs = False
+    assert envs[0].graph_safe
+    for it in range(2):
+        ra, rb = pa.collect_rollouts(), pb.collect_rollouts()
+        torch.cuda.synchronize()
+        assert pa._rollout_graph is not None and pb._rollout_graph is None
+        for k in ("obs", "act", "rew", "start", "val", "logp", "done", "epret"):
+            assert torch.equal(pa.buf[k], pb.buf[k]), (it, k)
+        assert torch.equal(ra[0], rb[0]) and torch.equal(ra[1], rb[1])
+        assert pa.ep_returns == pb.ep_returns
+    for e in envs:
+        e.close()
