@@ -92,6 +92,7 @@ hs::StepParams params_of(const hs_batch* b, int mode, int nsub) {
   p.noise_scale = b->cfg.noise_scale;
   p.seed = b->seed;
   for (int k = 0; k < 9; k++) p.kneel[k] = b->cfg.kneel_params[k];
+  p.solver = b->model->host.solver == 1 ? hs::SOLVER_PGS : hs::SOLVER_NEWTON;
   return p;
 }
 

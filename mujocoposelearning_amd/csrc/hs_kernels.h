@@ -52,7 +52,9 @@ struct StepParams {
   uint64_t seed;
   double kneel[9];       // target_height, min_height, max_roll_pitch, com_radius, energy_w, posture_w,
                          // com_w, foot_w, alive_w (reward_functions.py:71-81)
+  int solver;            // SOLVER_NEWTON (MuJoCo default) or SOLVER_PGS: selects the kernel instance
 };
+enum Solver { SOLVER_NEWTON = 0, SOLVER_PGS = 1 };
 
 // actions: [N][nu] float32 (may be null in MODE_RESET); reset_mask: [N] (null = all);
 // noise_qpos/noise_qvel: [N][nq]/[N][nv] host-supplied reset noise (null = device RNG).

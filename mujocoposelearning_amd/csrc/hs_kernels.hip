@@ -376,6 +376,17 @@ struct Scratch {
   } u;
 };
 
+// PGS solver scratch (the <option solver="PGS"> kernel instance only; the Newton instance never
+// allocates it): rows [0, PGS_CACHE) keep J_r and M^-1 J_r' per dof, every row its AR_rr and aref
+constexpr int PGS_CACHE = 32;
+template <typename T>
+struct PgsCache {
+  T J[PGS_CACHE][MAXDOF];
+  T MJ[PGS_CACHE][MAXDOF];
+  T AR[MAXEFC];
+  T ar[MAXEFC];
+};
+
 // ------------------------------------------------------------------ narrow phase
 template <typename T>
 struct Con {
@@ -1340,6 +1351,152 @@ struct Stepper {
     HS_STAMP(clk, 12);
   }
 
+  // lane (dof) j's entry of constraint row r's Jacobian (the same per-row Jacobians row_Jx applies
+  // through body velocities and the Newton Hessian's dense rank-1 terms use)
+  __device__ __forceinline__ T row_J_lane(int r) {
+    if (sl >= NV) return T(0);
+    const int kid = s.row_kid[r];
+    const int kind = rk_kind(kid), id = rk_id(kid);
+    if (kind <= RK_JHI) return m->jnt_dofadr[id] == sl ? (kind == RK_JLO ? T(1) : T(-1)) : T(0);
+    if (kind <= RK_THI) {
+      T v = 0;
+      for (int w = 0; w < m->ten_nwrap[id]; w++)
+        if (m->ten_wrapdof[id][w] == sl) v += m->ten_wrapcoef[id][w];
+      return kind == RK_TLO ? v : -v;
+    }
+    const int in2 = bit(s.con_m2[id], sl), in1 = bit(s.con_m1[id], sl);
+    if (in1 == in2) return T(0);
+    T rr[3] = {s.con_pos[id][0] - s.com[0], s.con_pos[id][1] - s.com[1], s.con_pos[id][2] - s.com[2]};
+    T w[3], u[3];
+    cross3(cd, rr, w);
+    T jp[3] = {cd[3] + w[0], cd[4] + w[1], cd[5] + w[2]};
+    row_u(m, s, kind, id, u);
+    const T v = dot3(u, jp);
+    return in2 ? v : -v;
+  }
+
+  // mj_solPGS (<option solver="PGS">), restating oracle/hsim_oracle.c solve_pgs: projected
+  // Gauss-Seidel on the dual  min 0.5 f'AR f + f'b, f >= 0  (AR = J M^-1 J' + R, b = J qacc_smooth -
+  // aref), rows swept in efc order.  Without forming AR: qacc = qacc_smooth + M^-1 J' f is kept
+  // per dof lane, so a row's residual is J_r qacc + R_r f_r - aref_r (one half-wave sum) and its
+  // update adds delta M^-1 J_r' to qacc.  M is factored once (row-per-lane Cholesky); J_r and
+  // M^-1 J_r' of the first PGS_CACHE rows are kept in LDS, later rows are rebuilt per sweep.
+  // Warm start: the forces of qacc_warmstart under the primal map, kept if their dual cost is
+  // negative.  Stops when a sweep's improvement * scale < tolerance, or after maxit sweeps.
+  __device__ __forceinline__ void solve_pgs(T xws, int maxit, const T (&D)[RPL], const T (&ar)[RPL],
+                                            const int (&rd)[RPL], const T (&rc)[RPL], PgsCache<T>& pc) {
+    phase_begin();
+    const int nefc = s.nefc;
+    const uint32_t bch = chain_mask(m, sl, nb);
+    bool vr[RPL];
+#pragma unroll
+    for (int q = 0; q < RPL; q++) {
+      vr[q] = sl + HL * q < nefc;
+      if (vr[q]) pc.ar[sl + HL * q] = ar[q];
+    }
+    T L[NV];
+#pragma unroll
+    for (int j = 0; j < NV; j++) L[j] = Mr[j];
+    T dinv = 0;
+    chol_rows<NV>(L, dinv, sl, s.u.n.cb);
+    const T qs = chol_solve<NV>(L, dinv, sl < NV ? fsmooth : T(0), sl);     // qacc_smooth
+    // warm start: f = -D (J xws - aref)_-, kept only if its dual cost is negative
+    if (sl < NV) s.vx[sl] = xws;
+    WSYNC();
+    map_vx<NV>(s, sl, nb, bch);
+    T f[RPL];
+#pragma unroll
+    for (int q = 0; q < RPL; q++) {
+      T jar = vr[q] ? row_Jx(m, s, rd[q], rc[q]) - ar[q] : T(0);
+      f[q] = jar < 0 ? -D[q] * jar : T(0);
+      if (vr[q]) s.row_f[sl + HL * q] = f[q];
+    }
+    WSYNC();
+    contact_aggregates(m, s, sl);
+    const T y = sl < NV ? jtf_lane(m, s, sl, cd) : T(0);
+    T z = chol_solve<NV>(L, dinv, y, sl);                                   // M^-1 J' f
+    if (sl >= NV) z = 0;
+    if (sl < NV) s.vx[sl] = z;
+    WSYNC();
+    map_vx<NV>(s, sl, nb, bch);
+    T c = 0, jz[RPL];
+#pragma unroll
+    for (int q = 0; q < RPL; q++) jz[q] = vr[q] ? row_Jx(m, s, rd[q], rc[q]) : T(0);
+    WSYNC();
+    if (sl < NV) s.vx[sl] = qs;
+    WSYNC();
+    map_vx<NV>(s, sl, nb, bch);
+#pragma unroll
+    for (int q = 0; q < RPL; q++)
+      if (vr[q]) c += f[q] * (T(0.5) * jz[q] + T(0.5) * f[q] / D[q] + row_Jx(m, s, rd[q], rc[q]) - ar[q]);
+    const bool keep = hsum(c) <= T(0);
+    T x = sl < NV ? (keep ? qs + z : qs) : T(0);
+    if (!keep) {
+#pragma unroll
+      for (int q = 0; q < RPL; q++)
+        if (vr[q]) s.row_f[sl + HL * q] = 0;
+    }
+    // rows that exist in either half of the wave (wave-uniform loop bound)
+    int maxr = nefc;
+    maxr = max(maxr, __shfl_xor(maxr, HL));
+    // per-row AR_rr (and the cached J_r, M^-1 J_r')
+    for (int r = 0; r < maxr; r++) {
+      const bool live = r < nefc;
+      T jr = live ? row_J_lane(r) : T(0);
+      T mj = chol_solve<NV>(L, dinv, jr, sl);
+      if (sl >= NV) mj = 0;
+      const T a = hsum(jr * mj) + (live ? T(1) / s.row_D[r] : T(0));
+      if (r < PGS_CACHE && sl < MAXDOF) { pc.J[r][sl] = jr; pc.MJ[r][sl] = mj; }
+      if (live && sl == 0) pc.AR[r] = a;
+    }
+    WSYNC();
+    const T scale = m->newton_scale, tol = m->pgs_tol;
+    bool done = false;
+    int it = 0;
+    for (int sweep = 0; sweep < maxit; sweep++) {
+      m = opaque(m);
+      sl = opaque_v(sl);
+      T improvement = 0;
+      for (int r = 0; r < maxr; r++) {
+        const bool live = r < nefc && !done;
+        T jr, mj;
+        if (r < PGS_CACHE) {
+          jr = sl < MAXDOF ? pc.J[r][sl] : T(0);
+          mj = sl < MAXDOF ? pc.MJ[r][sl] : T(0);
+        } else {
+          jr = r < nefc ? row_J_lane(r) : T(0);
+          mj = chol_solve<NV>(L, dinv, jr, sl);
+          if (sl >= NV) mj = 0;
+        }
+        const T fr = r < nefc ? s.row_f[r] : T(0);
+        const T Dr = r < nefc ? s.row_D[r] : T(1);
+        const T arr = r < nefc ? pc.AR[r] : T(1);
+        const T res = hsum(jr * x) + fr / Dr - (r < nefc ? pc.ar[r] : T(0));
+        T nf = fr - res / (arr < T(1e-15) ? T(1e-15) : arr);
+        nf = nf < T(0) ? T(0) : nf;
+        const T delta = live ? nf - fr : T(0);
+        x += delta * mj;
+        improvement -= delta * res + T(0.5) * arr * delta * delta;
+        if (live && sl == 0) s.row_f[r] = nf;
+      }
+      if (!done) it++;
+      done = done || (improvement * scale < tol);
+      if (__ballot(!done) == 0) break;
+      // re-anchor qacc = qacc_smooth + M^-1 J' f on the current forces once per sweep: the
+      // incremental updates accumulate rounding (fp32 PGS drifts over thousands of sweeps)
+      WSYNC();
+      contact_aggregates(m, s, sl);
+      T zz = chol_solve<NV>(L, dinv, sl < NV ? jtf_lane(m, s, sl, cd) : T(0), sl);
+      x = sl < NV ? qs + zz : T(0);
+    }
+    niter = it;
+    WSYNC();
+    contact_aggregates(m, s, sl);
+    fcon = sl < NV ? jtf_lane(m, s, sl, cd) : T(0);
+    qacc = sl < NV ? x : T(0);
+    WSYNC();
+  }
+
   // full_state: contact part of mj_rnePostConstraint (cfrc_ext, at the root subtree com: body 2 of a
   // contact gets +[(p - com) x F, F], body 1 the opposite, world skipped) and mj_subtreeVel's linear
   // part (m v_com of every body = m lin + ang x (m d) from cvel / cinert, summed over subtrees).
@@ -1445,8 +1602,9 @@ __device__ __forceinline__ void reset_state(MPtr<T> m, Scratch<T>& s, int sl, T&
   WSYNC();
 }
 
-template <typename T, int NV>
-__device__ __forceinline__ void physics_step(Stepper<T, NV>& st, KPtr<T> k, T& time, T& xws, int* warn) {
+template <typename T, int NV, bool PGS>
+__device__ __forceinline__ void physics_step(Stepper<T, NV>& st, KPtr<T> k, T& time, T& xws, int* warn,
+                                             PgsCache<T>* pc) {
   MPtr<T> m = st.m;
   Scratch<T>& s = st.s;
   const int sl = st.sl;
@@ -1470,7 +1628,10 @@ __device__ __forceinline__ void physics_step(Stepper<T, NV>& st, KPtr<T> k, T& t
     HS_STAMP(st.clk, 3);
     if (st.rows(D, ar, rd, rc)) warn[WARN_OVERFLOW]++;
     HS_STAMP(st.clk, 5);
-    st.solve(xws, opaque(k)->p.max_newton, sizeof(T) == 8 ? T(1e-13) : T(1e-7), D, ar, rd, rc);
+    if constexpr (PGS)
+      st.solve_pgs(xws, opaque(k)->p.max_newton, D, ar, rd, rc, *pc);
+    else
+      st.solve(xws, opaque(k)->p.max_newton, sizeof(T) == 8 ? T(1e-13) : T(1e-7), D, ar, rd, rc);
     bool ba = sl < m->nv && isbad(st.qacc);
     bool redo = hballot(ba, up) != 0 && attempt == 0;
     if (__ballot(redo) == 0) break;          // wave-uniform loop control
@@ -1629,11 +1790,16 @@ __device__ __forceinline__ void commit(MPtr<T> m, KPtr<T> k, const Stepper<T, NV
 }
 
 // ------------------------------------------------------------------ the kernel
-template <typename T, int NV>
+template <typename T, int NV, bool PGS = false>
 // 2 waves/SIMD (the VGPR budget of 256) for the fp32 engine; the fp64 parity engine needs more
-// registers and runs at 1
-__global__ __launch_bounds__(64, sizeof(T) == 4 ? 2 : 1) void step_kernel(KArgs<T> /* read via kernarg ptr */) {
+// registers and runs at 1.  PGS: the <option solver="PGS"> instance (its own LDS cache).
+__global__ __launch_bounds__(64, (sizeof(T) == 4 && !PGS) ? 2 : 1) void step_kernel(KArgs<T> /* read via kernarg ptr */) {
   __shared__ Scratch<T> smem[2];
+  PgsCache<T>* pcache = nullptr;
+  if constexpr (PGS) {
+    __shared__ PgsCache<T> pgs_smem[2];
+    pcache = &pgs_smem[threadIdx.x >= HL ? 1 : 0];
+  }
   const KPtr<T> ka = (KPtr<T>)__builtin_amdgcn_kernarg_segment_ptr();
   const int lane = threadIdx.x;
   const bool up = lane >= HL;
@@ -1759,7 +1925,7 @@ __global__ __launch_bounds__(64, sizeof(T) == 4 ? 2 : 1) void step_kernel(KArgs<
       if (sl < nu && opaque(ka)->actions) s.ctrl[sl] = act;
       WSYNC();
     }
-    physics_step(st, ka, time, xws, warn);
+    physics_step<T, NV, PGS>(st, ka, time, xws, warn, pcache);
 #ifdef HS_TIMING
     tot_iter += st.niter;
 #endif
@@ -1816,8 +1982,12 @@ hipError_t launch_step(const DevModel<T>* dmodel, int nv, const EnvBuffers<T>& b
   dim3 grid((nenv + 1) / 2), block(WAVE);
   switch (nv) {
     case 27:
-      hipLaunchKernelGGL((step_kernel<T, 27>), grid, block, 0, stream,
-                         KArgs<T>{(MPtr<T>)dmodel, b, actions, reset_mask, noise_qpos, noise_qvel, p, nenv});
+      if (p.solver == SOLVER_PGS)
+        hipLaunchKernelGGL((step_kernel<T, 27, true>), grid, block, 0, stream,
+                           KArgs<T>{(MPtr<T>)dmodel, b, actions, reset_mask, noise_qpos, noise_qvel, p, nenv});
+      else
+        hipLaunchKernelGGL((step_kernel<T, 27>), grid, block, 0, stream,
+                           KArgs<T>{(MPtr<T>)dmodel, b, actions, reset_mask, noise_qpos, noise_qvel, p, nenv});
       break;
     default:
       return hipErrorInvalidValue;

@@ -73,6 +73,7 @@ struct DevModel {
   T ten_wrapcoef[MAXTEN][MAXWRAP], ten_range[MAXTEN][2], ten_solref[MAXTEN][2], ten_solimp[MAXTEN][SOLIMP];
   T ten_margin[MAXTEN], ten_invweight0[MAXTEN];
   T qpos0[MAXQ];
+  T pgs_tol;                          // <option tolerance> (the PGS stopping rule; Newton solves exactly)
 };
 
 }  // namespace hs

@@ -401,9 +401,11 @@ struct Compiler {
       for (double x : nums(k->get(a))) if (x != 0) return false;
       return true;
     };
-    if (!is("solver", "Newton")) {
-      err = "only solver=\"Newton\" is supported (MuJoCo default, what the reference runs; PGS is in the oracle only)";
-      return false;
+    if (k->get("solver")) {
+      const std::string sv = k->get("solver");
+      if (sv == "Newton") m.solver = 0;
+      else if (sv == "PGS") m.solver = 1;
+      else { err = "only solver=\"Newton\" (MuJoCo default) or \"PGS\" is supported"; return false; }
     }
     if (!is("integrator", "Euler")) { err = "only integrator=\"Euler\" is supported (reference: MuJoCo default)"; return false; }
     if (!is("cone", "pyramidal")) { err = "only cone=\"pyramidal\" is supported"; return false; }
@@ -841,6 +843,7 @@ int model_field(const HostModel& m, const std::string& name, double* out, int n)
   else if (name == "opt_gravity") v = {m.gravity[0], m.gravity[1], m.gravity[2]};
   else if (name == "opt_iterations") v = {(double)m.iterations};
   else if (name == "opt_tolerance") v = {m.tolerance};
+  else if (name == "opt_solver") v = {(double)m.solver};
   else if (name == "stat_meaninertia") v = {m.meaninertia};
   else if (name == "body_parentid") I(m.body_parentid);
   else if (name == "body_rootid") I(m.body_rootid);
@@ -944,6 +947,7 @@ bool build_dev_model(const HostModel& m, DevModel<T>& d, std::string& err) {
   d.timestep = (T)m.timestep;
   for (int k = 0; k < 3; k++) d.gravity[k] = (T)m.gravity[k];
   d.newton_scale = (T)(1.0 / (m.meaninertia * std::max(1, m.nv)));
+  d.pgs_tol = (T)m.tolerance;
   d.total_mass = (T)m.body_subtreemass[0];
   // levels by depth
   std::vector<int> depth(m.nbody, 0);

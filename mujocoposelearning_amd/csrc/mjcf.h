@@ -15,7 +15,8 @@ struct HostModel {
   int nq = 0, nv = 0, nu = 0, nbody = 0, njnt = 0, ngeom = 0, ntendon = 0;
   double timestep = 0.002, gravity[3] = {0, 0, -9.81}, meaninertia = 1;
   int iterations = 100;          // <option iterations> (MuJoCo default): the default Newton cap
-  double tolerance = 1e-8;       // <option tolerance> (the engine solves to the exact minimiser)
+  double tolerance = 1e-8;       // <option tolerance> (Newton solves to the exact minimiser; PGS stops on it)
+  int solver = 0;                // <option solver>: 0 Newton (MuJoCo default), 1 PGS
   std::vector<std::string> body_name, jnt_name, geom_name, actuator_name, tendon_name;
   std::vector<int> body_parentid, body_rootid, body_weldid, body_jntadr, body_jntnum, body_dofadr, body_dofnum;
   std::vector<double> body_pos, body_quat, body_ipos, body_iquat, body_inertia, body_inertia_full;  // 3,4,3,4,3,9
