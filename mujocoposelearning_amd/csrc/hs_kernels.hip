@@ -7,8 +7,9 @@
 //   reward_functions.py:66-261 stand / kneeling / walk rewards (device plug-ins)
 //   SB3 SubprocVecEnv auto-reset semantics (train_sb3.py:203)
 // and MuJoCo 3.2.5's mj_step pipeline (custom_env.py:121,160): kinematics, com, collision, CRB,
-// RNE, actuation, constraint assembly, primal Newton solver (pyramidal cones), Euler with
-// implicit joint damping.
+// RNE, actuation, constraint assembly, primal Newton solver (pyramidal cones; MuJoCo's default) or,
+// in the <option solver="PGS"> instance, projected Gauss-Seidel on the dual, Euler with implicit
+// joint damping.
 //
 // Execution model: TWO ENVS PER WAVEFRONT.  Lanes 0-31 step env 2w, lanes 32-63 env 2w+1; a
 // half-wave maps its 32 lanes to bodies / dofs / geoms / joints / contacts / constraint rows
