@@ -27,6 +27,8 @@
  *                           dones, episode returns, new episode_starts, next obs into the buffer
  *   hs_gauss_logp(_grad) <- DiagGaussianDistribution.log_prob of the buffered actions in the PPO
  *                           update (SB3 ActorCriticPolicy.evaluate_actions) and its backward
+ *   hs_ppo_loss(_grad)   <- SB3 PPO.train's minibatch loss: advantage normalisation, clipped
+ *                           surrogate, value MSE (stable_baselines3 2.3.2 ppo/ppo.py) and its backward
  *   hs_colsum            <- the bias-gradient and split-K weight-gradient reductions of the PPO
  *                           update's loss.backward() (SB3 PPO.train, ppo.py; train_sb3.py:229)
  *
@@ -185,6 +187,21 @@ int hs_gauss_logp_grad(const float* mean, int mean_ld, const float* actions, con
 /* out[c] = sum_r x[r][c] over a row-major [rows][cols] float32 device matrix, in a fixed
  * summation order (deterministic).  `workspace` must hold hs_colsum_workspace(rows, cols) floats
  * (may be NULL when that is 0).  Asynchronous on `stream`. */
+/* SB3 PPO minibatch loss over B samples gathered by idx [B] (int64) from the rollout arrays
+ * advantages / returns / old_log_prob [M]: log_prob [B] and values [B] are the policy's on the
+ * minibatch.  a = advantages[idx] normalised (mean, unbiased std + 1e-8; not when B == 1),
+ * r = exp(log_prob - old_log_prob[idx]); writes policy_loss = -mean(min(a r, a clip(r, 1 -+ clip)))
+ * and value_loss = mean((returns[idx] - values)^2) (device scalars).  `workspace` holds
+ * hs_ppo_loss_workspace(B) floats: the forward leaves the gathered minibatch and the
+ * normalisation there for the backward, which, given the upstream device scalars g_pg, g_vf,
+ * writes dL/dlog_prob [B] and dL/dvalues [B] with torch's min/clamp derivative conventions.
+ * Fixed reduction order (deterministic); asynchronous on `stream`. */
+uint64_t hs_ppo_loss_workspace(int B);
+int hs_ppo_loss(const float* log_prob, const float* values, const int64_t* idx, const float* advantages,
+                const float* returns, const float* old_log_prob, int B, float clip, float* policy_loss,
+                float* value_loss, float* workspace, void* stream);
+int hs_ppo_loss_grad(const float* log_prob, const float* values, int B, float clip, const float* workspace,
+                     const float* g_pg, const float* g_vf, float* g_log_prob, float* g_values, void* stream);
 uint64_t hs_colsum_workspace(uint64_t rows, uint64_t cols);
 int hs_colsum(const float* x, uint64_t rows, uint64_t cols, float* workspace, float* out, void* stream);
 const char* hs_last_error(void);

@@ -469,6 +469,36 @@ int hs_gauss_logp_grad(const float* mean, int mean_ld, const float* actions, con
              : -1;
 }
 
+uint64_t hs_ppo_loss_workspace(int B) { return B > 0 ? hs::ppo_loss_workspace(B) : 0; }
+
+int hs_ppo_loss(const float* log_prob, const float* values, const int64_t* idx, const float* advantages,
+                const float* returns, const float* old_log_prob, int B, float clip, float* policy_loss,
+                float* value_loss, float* workspace, void* stream) {
+  if (B < 0) return fail("hs_ppo_loss: negative size");
+  if (B == 0) return 0;
+  if (!log_prob || !values || !idx || !advantages || !returns || !old_log_prob || !policy_loss || !value_loss ||
+      !workspace)
+    return fail("hs_ppo_loss: null buffer");
+  return hip_ok(hs::launch_ppo_loss_fwd(log_prob, values, idx, advantages, returns, old_log_prob, B, clip, policy_loss,
+                                        value_loss, workspace, (hipStream_t)stream),
+                "ppo loss kernels")
+             ? 0
+             : -1;
+}
+
+int hs_ppo_loss_grad(const float* log_prob, const float* values, int B, float clip, const float* workspace,
+                     const float* g_pg, const float* g_vf, float* g_log_prob, float* g_values, void* stream) {
+  if (B < 0) return fail("hs_ppo_loss_grad: negative size");
+  if (B == 0) return 0;
+  if (!log_prob || !values || !workspace || !g_pg || !g_vf || !g_log_prob || !g_values)
+    return fail("hs_ppo_loss_grad: null buffer");
+  return hip_ok(hs::launch_ppo_loss_bwd(log_prob, values, B, clip, workspace, g_pg, g_vf, g_log_prob, g_values,
+                                        (hipStream_t)stream),
+                "ppo_loss_bwd_kernel")
+             ? 0
+             : -1;
+}
+
 uint64_t hs_colsum_workspace(uint64_t rows, uint64_t cols) { return hs::colsum_workspace(rows, cols); }
 
 int hs_colsum(const float* x, uint64_t rows, uint64_t cols, float* workspace, float* out, void* stream) {

@@ -89,6 +89,14 @@ hipError_t launch_gauss_logp(const float* mean, int mean_ld, const float* act, c
 hipError_t launch_gauss_logp_grad(const float* mean, int mean_ld, const float* act, const float* log_std,
                                   const float* g_logp, float* g_mean, float* gls_rows, int N, int A,
                                   hipStream_t stream);
+// SB3 PPO minibatch loss (clipped surrogate + value MSE) forward / backward (ppo.hip); workspace
+// of ppo_loss_workspace(B) floats, written by the forward and read by the backward
+size_t ppo_loss_workspace(int B);
+hipError_t launch_ppo_loss_fwd(const float* logp, const float* v, const int64_t* idx, const float* adv,
+                               const float* ret, const float* old_logp, int B, float clip, float* pg, float* vf,
+                               float* ws, hipStream_t stream);
+hipError_t launch_ppo_loss_bwd(const float* logp, const float* v, int B, float clip, const float* ws,
+                               const float* g_pg, const float* g_vf, float* g_logp, float* g_v, hipStream_t stream);
 // GAE reverse scan over [T][N] float32 rollout arrays (gae.hip)
 hipError_t launch_gae(const float* rew, const float* val, const float* start, const float* last_val,
                       const float* last_done, float* adv, float* ret, int T, int N, float gamma, float lam,

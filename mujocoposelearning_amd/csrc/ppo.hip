@@ -190,6 +190,156 @@ __global__ __launch_bounds__(256) void gauss_logp_grad_kernel(const float* __res
   gls_rows[i] = g * (z * z - 1.0f);
 }
 
+// SB3 PPO.train's per-minibatch loss terms (stable_baselines3 2.3.2 ppo/ppo.py) over a minibatch
+// gathered by idx from the rollout arrays (the torch restatement is ~25 small kernels):
+//   a     = adv[idx];  a_n = (a - mean(a)) / (std(a) + 1e-8)       (std unbiased; skipped if B = 1)
+//   r     = exp(logp - old_logp[idx])
+//   pg    = -mean(min(a_n r, a_n clamp(r, 1 - clip, 1 + clip)))
+//   vf    = mean((ret[idx] - v)^2)
+// Backward (torch's derivative conventions: min splits ties, clamp passes its closed interval):
+//   dpg/dlogp_i = -(1/B) r_i dmin_i,  dmin_i = a_n [s1 < s2] + a_n [r in range] [s1 > s2] + ties / 2
+//   dvf/dv_i    = 2 (v_i - ret_i) / B
+// The random gathers bound the work (each lane of a gather touches its own cache line), so they
+// are spread over LOSS_BLOCKS-wide grids: loss_gather writes the gathered a / old_logp / ret
+// compactly (the backward reads those coalesced) with per-block sums of a - a_0 and (a - a_0)^2
+// (shifted by the minibatch's first advantage against cancellation); loss_terms reduces those
+// partials in a fixed order (deterministic) and forms per-block surrogate / MSE sums; loss_final
+// writes the two scalars.  Workspace: 3 B + 4 blocks floats + 2 stats.
+constexpr int LOSS_TPB = 256;
+
+__device__ inline float block_sum256(float v, float* red) {
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(LOSS_TPB) void loss_gather_kernel(const int64_t* __restrict__ idx,
+                                                               const float* __restrict__ adv,
+                                                               const float* __restrict__ ret,
+                                                               const float* __restrict__ old_logp, int B,
+                                                               float* __restrict__ ws) {
+  __shared__ float red[LOSS_TPB / 64];
+  const int i = blockIdx.x * LOSS_TPB + threadIdx.x;
+  float* a_g = ws;
+  float* old_g = ws + B;
+  float* ret_g = ws + 2 * (size_t)B;
+  float* part = ws + 3 * (size_t)B;            // [blocks][4]: sum d, sum d^2, sum pg, sum vf
+  const float a0 = adv[idx[0]];
+  float d = 0.f;
+  if (i < B) {
+    const int64_t j = idx[i];
+    const float a = adv[j];
+    a_g[i] = a;
+    old_g[i] = old_logp[j];
+    ret_g[i] = ret[j];
+    d = a - a0;
+  }
+  const float s1 = block_sum256(d, red);
+  const float s2 = block_sum256(d * d, red);
+  if (threadIdx.x == 0) {
+    part[4 * blockIdx.x + 0] = s1;
+    part[4 * blockIdx.x + 1] = s2;
+  }
+}
+
+// sum over blocks of part[4 k + c], by one full wave (lane-strided, then a fixed xor tree: the
+// same order in every block and every run)
+__device__ inline float wave_part_sum(const float* part, int nblk, int c) {
+  const int l = threadIdx.x & 63;
+  float t = 0.f;
+  for (int k = l; k < nblk; k += 64) t += part[4 * k + c];
+  for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o);
+  return t;
+}
+
+// mean and 1 / (std + 1e-8) from the per-block shifted sums (called by a whole wave)
+__device__ inline void loss_stats(const float* ws, int B, int nblk, float a0, float& mean, float& inv) {
+  const float* part = ws + 3 * (size_t)B;
+  const float s1 = wave_part_sum(part, nblk, 0), s2 = wave_part_sum(part, nblk, 1);
+  if (B > 1) {
+    mean = a0 + s1 / (float)B;
+    float var = (s2 - s1 * s1 / (float)B) / (float)(B - 1);
+    inv = 1.f / (sqrtf(fmaxf(var, 0.f)) + 1e-8f);
+  } else {
+    mean = 0.f;
+    inv = 1.f;
+  }
+}
+
+__global__ __launch_bounds__(LOSS_TPB) void loss_terms_kernel(const float* __restrict__ logp,
+                                                              const float* __restrict__ v, int B, float clip,
+                                                              float* __restrict__ ws, int nblk) {
+  __shared__ float red[LOSS_TPB / 64];
+  __shared__ float st[2];
+  const float* a_g = ws;
+  const float* old_g = ws + B;
+  const float* ret_g = ws + 2 * (size_t)B;
+  float* part = ws + 3 * (size_t)B;
+  if (threadIdx.x < 64) {
+    float mu, iv;
+    loss_stats(ws, B, nblk, a_g[0], mu, iv);
+    if (threadIdx.x == 0) { st[0] = mu; st[1] = iv; }
+  }
+  __syncthreads();
+  const float mean = st[0], inv = st[1];
+  const int i = blockIdx.x * LOSS_TPB + threadIdx.x;
+  float pg = 0.f, vf = 0.f;
+  if (i < B) {
+    const float an = (a_g[i] - mean) * inv;
+    const float r = expf(logp[i] - old_g[i]);
+    const float rc = fminf(fmaxf(r, 1.f - clip), 1.f + clip);
+    pg = fminf(an * r, an * rc);
+    const float e = ret_g[i] - v[i];
+    vf = e * e;
+  }
+  pg = block_sum256(pg, red);
+  vf = block_sum256(vf, red);
+  if (threadIdx.x == 0) {
+    part[4 * blockIdx.x + 2] = pg;
+    part[4 * blockIdx.x + 3] = vf;
+    if (blockIdx.x == 0) {                    // stats for the backward
+      float* stats = part + 4 * nblk;
+      stats[0] = mean;
+      stats[1] = inv;
+    }
+  }
+}
+
+__global__ void loss_final_kernel(const float* __restrict__ ws, int B, int nblk, float* __restrict__ pg_out,
+                                  float* __restrict__ vf_out) {
+  const float* part = ws + 3 * (size_t)B;
+  const float pg = wave_part_sum(part, nblk, 2), vf = wave_part_sum(part, nblk, 3);
+  if (threadIdx.x != 0) return;
+  pg_out[0] = -pg / (float)B;
+  vf_out[0] = vf / (float)B;
+}
+
+__global__ __launch_bounds__(256) void ppo_loss_bwd_kernel(const float* __restrict__ logp,
+                                                           const float* __restrict__ v, int B, float clip,
+                                                           const float* __restrict__ ws, int nblk,
+                                                           const float* __restrict__ g_pg,
+                                                           const float* __restrict__ g_vf,
+                                                           float* __restrict__ g_logp, float* __restrict__ g_v) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  const float* a_g = ws;
+  const float* old_g = ws + B;
+  const float* ret_g = ws + 2 * (size_t)B;
+  const float* stats = ws + 3 * (size_t)B + 4 * nblk;
+  const float an = (a_g[i] - stats[0]) * stats[1];
+  const float r = expf(logp[i] - old_g[i]);
+  const float lo = 1.f - clip, hi = 1.f + clip;
+  const float rc = fminf(fmaxf(r, lo), hi);
+  const float s1 = an * r, s2 = an * rc;
+  const float d1 = an, d2 = (r >= lo && r <= hi) ? an : 0.f;
+  const float dmin = s1 < s2 ? d1 : (s1 > s2 ? d2 : 0.5f * (d1 + d2));
+  g_logp[i] = g_pg[0] * (-1.f / (float)B) * dmin * r;
+  g_v[i] = g_vf[0] * 2.f * (v[i] - ret_g[i]) / (float)B;
+}
+
 // Column sums of a row-major [rows][cols] float32 matrix: out[c] = sum_r x[r][c].  The PPO
 // update's bias gradients (sum of the output gradient over the minibatch, [32768][256]) and the
 // split-K weight-gradient finish (sum over S slices of [S][out*in]).  A workgroup is a tile of
@@ -319,6 +469,31 @@ hipError_t launch_gauss_logp_grad(const float* mean, int mean_ld, const float* a
   const size_t el = (size_t)N * A;
   hipLaunchKernelGGL(gauss_logp_grad_kernel, dim3((unsigned)((el + 255) / 256)), dim3(256), 0, stream, mean, mean_ld,
                      act, log_std, g_logp, g_mean, gls_rows, N, A);
+  return hipGetLastError();
+}
+
+size_t ppo_loss_workspace(int B) {
+  const size_t nblk = B > 0 ? ((size_t)B + LOSS_TPB - 1) / LOSS_TPB : 0;
+  return 3 * (size_t)B + 4 * nblk + 2;
+}
+
+hipError_t launch_ppo_loss_fwd(const float* logp, const float* v, const int64_t* idx, const float* adv,
+                               const float* ret, const float* old_logp, int B, float clip, float* pg, float* vf,
+                               float* ws, hipStream_t stream) {
+  if (B <= 0) return hipSuccess;
+  const int nblk = (B + LOSS_TPB - 1) / LOSS_TPB;
+  hipLaunchKernelGGL(loss_gather_kernel, dim3(nblk), dim3(LOSS_TPB), 0, stream, idx, adv, ret, old_logp, B, ws);
+  hipLaunchKernelGGL(loss_terms_kernel, dim3(nblk), dim3(LOSS_TPB), 0, stream, logp, v, B, clip, ws, nblk);
+  hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(64), 0, stream, (const float*)ws, B, nblk, pg, vf);
+  return hipGetLastError();
+}
+
+hipError_t launch_ppo_loss_bwd(const float* logp, const float* v, int B, float clip, const float* ws,
+                               const float* g_pg, const float* g_vf, float* g_logp, float* g_v, hipStream_t stream) {
+  if (B <= 0) return hipSuccess;
+  const int nblk = (B + LOSS_TPB - 1) / LOSS_TPB;
+  hipLaunchKernelGGL(ppo_loss_bwd_kernel, dim3(nblk), dim3(256), 0, stream, logp, v, B, clip, ws, nblk, g_pg, g_vf,
+                     g_logp, g_v);
   return hipGetLastError();
 }
 

@@ -84,6 +84,54 @@ class _GaussLogpFn(torch.autograd.Function):
         return g_mean, None, colsum(rows)
 
 
+class _PPOLossFn(torch.autograd.Function):
+    """SB3 PPO.train's minibatch policy/value loss (advantage normalisation, clipped surrogate,
+    value MSE) over indices idx into the rollout arrays: one hs_ppo_loss launch forward, one
+    hs_ppo_loss_grad launch backward (dL/dlog_prob, dL/dvalues)."""
+
+    @staticmethod
+    def forward(ctx, logp, v, idx, adv, ret, old_logp, clip):
+        from . import _lib
+        logp, v = logp.contiguous(), v.contiguous()
+        B = logp.shape[0]
+        dev = logp.device
+        L = _lib.lib()
+        pg = torch.empty((), dtype=torch.float32, device=dev)
+        vf = torch.empty((), dtype=torch.float32, device=dev)
+        ws = torch.empty(int(L.hs_ppo_loss_workspace(B)), dtype=torch.float32, device=dev)
+        st = torch.cuda.current_stream(dev).cuda_stream
+        _lib.check(L.hs_ppo_loss(logp.data_ptr(), v.data_ptr(), idx.data_ptr(), adv.data_ptr(), ret.data_ptr(),
+                                 old_logp.data_ptr(), B, float(clip), pg.data_ptr(), vf.data_ptr(), ws.data_ptr(), st))
+        ctx.save_for_backward(logp, v, ws)
+        ctx.clip = float(clip)
+        return pg, vf
+
+    @staticmethod
+    def backward(ctx, g_pg, g_vf):
+        from . import _lib
+        logp, v, ws = ctx.saved_tensors
+        B = logp.shape[0]
+        dev = logp.device
+        z = torch.zeros((), dtype=torch.float32, device=dev)
+        g_pg = z if g_pg is None else g_pg.to(torch.float32).contiguous()
+        g_vf = z if g_vf is None else g_vf.to(torch.float32).contiguous()
+        g_logp = torch.empty(B, dtype=torch.float32, device=dev)
+        g_v = torch.empty(B, dtype=torch.float32, device=dev)
+        st = torch.cuda.current_stream(dev).cuda_stream
+        _lib.check(_lib.lib().hs_ppo_loss_grad(logp.data_ptr(), v.data_ptr(), B, ctx.clip, ws.data_ptr(),
+                                               g_pg.data_ptr(), g_vf.data_ptr(), g_logp.data_ptr(), g_v.data_ptr(),
+                                               st))
+        return g_logp, g_v, None, None, None, None, None
+
+
+def ppo_loss(logp, v, idx, adv, ret, old_logp, clip):
+    """(policy_loss, value_loss) of one minibatch on a device (hs_ppo_loss / hs_ppo_loss_grad)."""
+    for t in (adv, ret, old_logp):
+        assert t.dtype == torch.float32 and t.is_contiguous() and t.dim() == 1
+    assert idx.dtype == torch.int64 and idx.is_contiguous()
+    return _PPOLossFn.apply(logp, v, idx, adv, ret, old_logp, clip)
+
+
 def colsum(x):
     """Column sums of a contiguous [rows, cols] float32 device matrix through hs_colsum
     (ppo.hip): deterministic, and 3-5x faster than torch's dim-0 reduction at the PPO update's
@@ -503,6 +551,9 @@ class PPO:
         mean, v = self.policy(obs[idx])
         logp = self.policy._logp(mean, act[idx])
         ent_mean = self.policy.entropy()            # = evaluate()'s per-sample entropy, averaged
+        if logp.is_cuda:                            # fused HIP loss (same formulas as below)
+            pg, vf = ppo_loss(logp, v, idx, adv, ret, old_logp, self.clip_range)
+            return pg + self.ent_coef * (-ent_mean) + self.vf_coef * vf, pg, vf
         a = adv[idx]
         if a.numel() > 1:
             a = (a - a.mean()) / (a.std() + 1e-8)

@@ -327,3 +327,37 @@ def test_graphed_rollout_matches_eager_rollout():
         assert pa.ep_returns == pb.ep_returns
     for e in envs:
         e.close()
+
+
+@pytest.mark.parametrize("B", [32768, 777, 1])
+def test_fused_ppo_loss_matches_torch(B):
+    """hs_ppo_loss / hs_ppo_loss_grad == the torch restatement of SB3 PPO.train's minibatch loss
+    (PPO._minibatch_loss's CPU branch) and its autograd gradients, with ratios inside and outside
+    the clip range."""
+    from mujocoposelearning_amd.ppo import ppo_loss
+    g = torch.Generator(device="cuda").manual_seed(B)
+    M, clip = 50000, 0.2
+    adv = torch.randn(M, device="cuda", generator=g) * 3 + 0.5
+    ret = torch.randn(M, device="cuda", generator=g)
+    old = torch.randn(M, device="cuda", generator=g) * 0.1 - 20
+    idx = torch.randperm(M, device="cuda", generator=g)[:B].contiguous()
+    lp0 = old[idx] + 0.3 * torch.randn(B, device="cuda", generator=g)     # ratios ~ exp(N(0, 0.3))
+    v0 = torch.randn(B, device="cuda", generator=g)
+    out = []
+    for fused in (True, False):
+        lp, v = lp0.clone().requires_grad_(), v0.clone().requires_grad_()
+        if fused:
+            pg, vf = ppo_loss(lp, v, idx, adv, ret, old, clip)
+        else:
+            a = adv[idx]
+            if B > 1:
+                a = (a - a.mean()) / (a.std() + 1e-8)
+            r = torch.exp(lp - old[idx])
+            pg = -torch.min(a * r, a * r.clamp(1 - clip, 1 + clip)).mean()
+            vf = torch.nn.functional.mse_loss(ret[idx], v)
+        (pg + 0.5 * vf).backward()
+        out.append((float(pg), float(vf), lp.grad.clone(), v.grad.clone()))
+    (pg, vf, glp, gv), (pg_r, vf_r, glp_r, gv_r) = out
+    assert abs(pg - pg_r) <= 1e-5 * (1 + abs(pg_r)) and abs(vf - vf_r) <= 1e-5 * (1 + abs(vf_r))
+    assert torch.allclose(glp, glp_r, rtol=1e-4, atol=1e-6 * float(glp_r.abs().max()) + 1e-12)
+    assert torch.allclose(gv, gv_r, rtol=1e-5, atol=1e-9)
