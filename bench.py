@@ -105,6 +105,7 @@ def main():
     ap.add_argument("--train-iters", type=int, default=2, help="PPO iterations of the train mode (0: skip)")
     ap.add_argument("--groups", default="1", help="stream groups for the headline run (1 = one launch per step)")
     ap.add_argument("--no-configs", action="store_true", help="skip the configs[3]/[4] legs")
+    ap.add_argument("--no-fp64", action="store_true", help="skip the fp64 (parity-mode) sim-only leg")
     ap.add_argument("--free-groups", type=int, default=4, help="extra sim-only leg: this many free-running stream "
                                                                 "groups (0: skip)")
     ap.add_argument("--dist-backend", default=os.environ.get("HSIM_BENCH_BACKEND", "nccl"),
@@ -236,6 +237,28 @@ def main():
                        note="same workload as value, envs split into free-running stream groups (HsBatch "
                             "join=False): one group's Newton tail overlaps the others' launches")
         envg.close()
+
+    # parity-mode leg: the fp64 engine (the one the oracle parity tests pin at 1e-9 per stage and
+    # that tracks the oracle over 1000 substeps) on the same workload and protocol as value
+    fp64_leg = None
+    if args.precision == "fp32" and not args.no_fp64:
+        e64 = HumanoidVecEnv(cfg, n_envs=n, device=dev_index, precision="fp64", seed=5000 + rank, model=model)
+        e64.reset_tensors()
+        for k in range(min(args.warmup, 5)):
+            e64.step_tensors(tape[k % tape_len])
+        barrier()
+        k64 = max(10, args.steps // 4)
+        t64 = time.perf_counter()
+        for k in range(k64):
+            e64.step_tensors(tape[k % tape_len])
+        barrier()
+        t = torch.tensor([time.perf_counter() - t64], dtype=torch.float64, device=red_dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        fp64_leg = dict(value=n * k64 * world / float(t.item()), unit="env_steps/s", dtype="f64", steps=k64,
+                        note="same workload, fp64 engine (parity mode: <=1e-9 per stage vs the fp64 oracle, "
+                             "tracks it over 1000 substeps; profiles/parity_report.md)")
+        e64.close()
 
     # BASELINE.json configs[3] (kneeling reward, 4096 envs) and configs[4] (full-state obs, 8192
     # envs over 8 GPUs = 1024 per GPU): same sim-only protocol, one launch per step
@@ -389,6 +412,7 @@ def main():
             "rollout": rollout,
             "gae": gae_res,
             "sim_only_stream_groups": grouped,
+            "sim_only_fp64": fp64_leg,
             "other_configs": config_legs,
             "train": train_res,
             "sim_stats": stats,
