@@ -148,15 +148,61 @@ def colsum(x):
     return out
 
 
+class _SplitKLinearReLUFn(torch.autograd.Function):
+    """relu(x W^T + b) with the ReLU in the GEMM's epilogue (hipBLASLt bias+ReLU through
+    torch._addmm_activation: no separate activation pass over [B, out]); backward masks the
+    upstream gradient with y > 0, then takes _SplitKLinearFn's split-K gradients."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, s):
+        y = torch._addmm_activation(b, x, w.t())
+        ctx.save_for_backward(x, w, y)
+        ctx.s = s
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w, y = ctx.saved_tensors
+        s = ctx.s
+        g = torch.where(y > 0, g, torch.zeros((), dtype=g.dtype, device=g.device))
+        gx = g @ w if ctx.needs_input_grad[0] else None
+        part = torch.bmm(g.view(s, -1, g.shape[1]).transpose(1, 2), x.view(s, -1, x.shape[1]))
+        return gx, colsum(part.view(s, -1)).view_as(w), colsum(g), None
+
+
+def _splitk_rows(x):
+    n = x.shape[0] if x.dim() == 2 else 0
+    if SPLIT_K and x.is_cuda and torch.is_grad_enabled() and n >= 2 * _SPLITK_ROWS and n % _SPLITK_ROWS == 0:
+        return n // _SPLITK_ROWS
+    return 0
+
+
 class Linear(nn.Linear):
     """nn.Linear (same parameters and state_dict keys, so SB3 checkpoints map 1:1) with split-K
     weight gradients for large device minibatches; small or CPU batches take nn.Linear's path."""
 
     def forward(self, x):
-        n = x.shape[0] if x.dim() == 2 else 0
-        if SPLIT_K and x.is_cuda and torch.is_grad_enabled() and n >= 2 * _SPLITK_ROWS and n % _SPLITK_ROWS == 0:
-            return _SplitKLinearFn.apply(x, self.weight, self.bias, n // _SPLITK_ROWS)
+        s = _splitk_rows(x)
+        if s:
+            return _SplitKLinearFn.apply(x, self.weight, self.bias, s)
         return super().forward(x)
+
+
+def mlp_forward(seq, x):
+    """nn.Sequential forward that runs each (Linear, ReLU) pair of a large device minibatch as one
+    fused GEMM + epilogue (_SplitKLinearReLUFn); everything else module by module."""
+    mods = list(seq)
+    i = 0
+    while i < len(mods):
+        m = mods[i]
+        if (isinstance(m, Linear) and i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU)
+                and _splitk_rows(x)):
+            x = _SplitKLinearReLUFn.apply(x, m.weight, m.bias, _splitk_rows(x))
+            i += 2
+            continue
+        x = m(x)
+        i += 1
+    return x
 
 
 def _flat_packed(pk):
@@ -190,7 +236,8 @@ class ActorCritic(nn.Module):
                     nn.init.zeros_(m.bias)
 
     def forward(self, obs):
-        return self.action_net(self.pi_net(obs)), self.value_net(self.vf_net(obs)).squeeze(-1)
+        return (self.action_net(mlp_forward(self.pi_net, obs)),
+                self.value_net(mlp_forward(self.vf_net, obs)).squeeze(-1))
 
     def _logp(self, mean, actions):
         """DiagGaussian log_prob; on a device through hs_gauss_logp (+ its HIP backward)."""

@@ -287,3 +287,23 @@ def test_packed_heads_match_two_nets():
     m2, v2 = pol2.heads(obs)
     r2m, r2v = pol2(obs)
     assert torch.equal(m2, r2m) and torch.equal(v2, r2v)
+
+
+@pytest.mark.gpu
+def test_fused_linear_relu_matches_modules():
+    """mlp_forward's fused Linear+ReLU (GEMM epilogue + masked split-K backward) equals the
+    module-by-module Linear, ReLU forward and gradients."""
+    from mujocoposelearning_amd import ppo as ppo_mod
+    torch.manual_seed(0)
+    seq = torch.nn.Sequential(ppo_mod.Linear(352, 256), torch.nn.ReLU(), ppo_mod.Linear(256, 256),
+                              torch.nn.ReLU()).cuda()
+    x = torch.randn(4 * ppo_mod._SPLITK_ROWS, 352, device="cuda")
+    g = torch.randn(x.shape[0], 256, device="cuda")
+    out = []
+    for fused in (True, False):
+        seq.zero_grad()
+        y = ppo_mod.mlp_forward(seq, x) if fused else seq(x)
+        (y * g).sum().backward()
+        out.append([y.detach()] + [p.grad.clone() for p in seq.parameters()])
+    for a, b in zip(*out):
+        assert torch.allclose(a, b, rtol=1e-4, atol=1e-4 * float(b.abs().max())), float((a - b).abs().max())
