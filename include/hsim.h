@@ -29,6 +29,8 @@
  *                           update (SB3 ActorCriticPolicy.evaluate_actions) and its backward
  *   hs_ppo_loss(_grad)   <- SB3 PPO.train's minibatch loss: advantage normalisation, clipped
  *                           surrogate, value MSE (stable_baselines3 2.3.2 ppo/ppo.py) and its backward
+ *   hs_adam_clip         <- torch.nn.utils.clip_grad_norm_(max_grad_norm) + torch.optim.Adam.step of
+ *                           SB3 PPO.train (ppo.py: max_grad_norm 0.5, Adam eps 1e-5)
  *   hs_colsum            <- the bias-gradient and split-K weight-gradient reductions of the PPO
  *                           update's loss.backward() (SB3 PPO.train, ppo.py; train_sb3.py:229)
  *
@@ -202,6 +204,19 @@ int hs_ppo_loss(const float* log_prob, const float* values, const int64_t* idx, 
                 float* value_loss, float* workspace, void* stream);
 int hs_ppo_loss_grad(const float* log_prob, const float* values, int B, float clip, const float* workspace,
                      const float* g_pg, const float* g_vf, float* g_log_prob, float* g_values, void* stream);
+/* Gradient-norm clipping + one Adam step over nt <= 16 float32 device tensors: params[i],
+ * grads[i], exp_avg[i], exp_avg_sq[i] (numel[i] elements each) and step[i] (a float32 device
+ * scalar per tensor, torch's capturable Adam state; all tensors share one step count).  With
+ * c = min(1, max_norm / (||grads||_2 + 1e-6)) (max_norm <= 0: c = 1) and t = step + 1:
+ * m = b1 m + (1-b1) c g; v = b2 v + (1-b2) (c g)^2; p -= lr / (1 - b1^t) * m / (sqrt(v) /
+ * sqrt(1 - b2^t) + eps); step = t (1 - beta rounded to float from double, as torch's scalar
+ * arguments are).  Grads are read, not modified.  `workspace` holds
+ * hs_adam_workspace(sum numel) floats.  Pointer tables are host arrays (copied into the kernel
+ * arguments); asynchronous on `stream`. */
+uint64_t hs_adam_workspace(uint64_t total_numel);
+int hs_adam_clip(int nt, float* const* params, const float* const* grads, float* const* exp_avg,
+                 float* const* exp_avg_sq, float* const* step, const int64_t* numel, float* workspace, float max_norm,
+                 double lr, double beta1, double beta2, double eps, void* stream);
 uint64_t hs_colsum_workspace(uint64_t rows, uint64_t cols);
 int hs_colsum(const float* x, uint64_t rows, uint64_t cols, float* workspace, float* out, void* stream);
 const char* hs_last_error(void);

@@ -82,6 +82,9 @@ def lib():
         "hs_ppo_loss_workspace": (u64, [i]),
         "hs_ppo_loss": (i, [vp, vp, vp, vp, vp, vp, i, C.c_float, vp, vp, vp, vp]),
         "hs_ppo_loss_grad": (i, [vp, vp, i, C.c_float, vp, vp, vp, vp, vp, vp]),
+        "hs_adam_workspace": (u64, [u64]),
+        "hs_adam_clip": (i, [i, vp, vp, vp, vp, vp, vp, vp, C.c_float, C.c_double, C.c_double, C.c_double, C.c_double,
+                             vp]),
         "hs_colsum_workspace": (u64, [u64, u64]),
         "hs_colsum": (i, [vp, u64, u64, vp, vp, vp]),
         "hs_last_error": (C.c_char_p, []),
@@ -99,7 +102,7 @@ EXPORTED = ("hs_model_load", "hs_model_free", "hs_model_field", "hs_batch_create
             "hs_batch_get_info", "hs_get_buffers", "hs_set_config", "hs_set_seed", "hs_get_config", "hs_reset", "hs_step",
             "hs_physics_step", "hs_state_io", "hs_kinematics", "hs_set_debug", "hs_get_debug", "hs_synchronize", "hs_gae",
             "hs_ppo_act", "hs_ppo_post", "hs_gauss_logp", "hs_gauss_logp_grad",
-            "hs_ppo_loss_workspace", "hs_ppo_loss", "hs_ppo_loss_grad",
+            "hs_ppo_loss_workspace", "hs_ppo_loss", "hs_ppo_loss_grad", "hs_adam_workspace", "hs_adam_clip",
             "hs_colsum_workspace", "hs_colsum", "hs_last_error", "hs_version")
 
 

@@ -499,6 +499,27 @@ int hs_ppo_loss_grad(const float* log_prob, const float* values, int B, float cl
              : -1;
 }
 
+uint64_t hs_adam_workspace(uint64_t total_numel) { return (uint64_t)hs::adam_partials((long long)total_numel); }
+
+int hs_adam_clip(int nt, float* const* params, const float* const* grads, float* const* exp_avg,
+                 float* const* exp_avg_sq, float* const* step, const int64_t* numel, float* workspace, float max_norm,
+                 double lr, double beta1, double beta2, double eps, void* stream) {
+  if (nt < 1 || nt > 16) return fail("hs_adam_clip: need 1 <= nt <= 16 tensors");
+  if (!params || !grads || !exp_avg || !exp_avg_sq || !step || !numel || !workspace)
+    return fail("hs_adam_clip: null argument");
+  std::vector<long long> n(nt);
+  for (int t = 0; t < nt; t++) {
+    if (!params[t] || !grads[t] || !exp_avg[t] || !exp_avg_sq[t] || !step[t] || numel[t] < 0)
+      return fail("hs_adam_clip: null tensor or negative size");
+    n[t] = (long long)numel[t];
+  }
+  return hip_ok(hs::launch_adam_clip(nt, params, grads, exp_avg, exp_avg_sq, step, n.data(), workspace, max_norm, lr,
+                                     beta1, beta2, eps, (hipStream_t)stream),
+                "adam kernels")
+             ? 0
+             : -1;
+}
+
 uint64_t hs_colsum_workspace(uint64_t rows, uint64_t cols) { return hs::colsum_workspace(rows, cols); }
 
 int hs_colsum(const float* x, uint64_t rows, uint64_t cols, float* workspace, float* out, void* stream) {

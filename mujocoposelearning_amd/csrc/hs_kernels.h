@@ -97,6 +97,11 @@ hipError_t launch_ppo_loss_fwd(const float* logp, const float* v, const int64_t*
                                float* ws, hipStream_t stream);
 hipError_t launch_ppo_loss_bwd(const float* logp, const float* v, int B, float clip, const float* ws,
                                const float* g_pg, const float* g_vf, float* g_logp, float* g_v, hipStream_t stream);
+// clip_grad_norm_ + Adam over up to 16 tensors (ppo.hip); part: adam_partials(total numel) floats
+int adam_partials(long long total);
+hipError_t launch_adam_clip(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
+                            float* const* step, const long long* numel, float* part, float max_norm, double lr,
+                            double b1, double b2, double eps, hipStream_t stream);
 // GAE reverse scan over [T][N] float32 rollout arrays (gae.hip)
 hipError_t launch_gae(const float* rew, const float* val, const float* start, const float* last_val,
                       const float* last_done, float* adv, float* ret, int T, int N, float gamma, float lam,

@@ -340,6 +340,88 @@ __global__ __launch_bounds__(256) void ppo_loss_bwd_kernel(const float* __restri
   g_v[i] = g_vf[0] * 2.f * (v[i] - ret_g[i]) / (float)B;
 }
 
+// clip_grad_norm_(max_norm) + Adam (torch.optim.Adam, capturable/fused formula) over up to
+// ADAM_MAXT parameter tensors in three launches (torch: a multi-tensor norm, stack, norm, clamp,
+// foreach mul and the fused Adam kernel):
+//   adam_sqsum   per-block sums of g^2 over the concatenated gradients (fixed order)
+//   adam_update  every block reduces those partials (same order) to the clip coefficient
+//                min(1, max_norm / (||g|| + 1e-6)), then updates its chunk:
+//                  m = b1 m + (1-b1) g c;  v = b2 v + (1-b2) (g c)^2
+//                  p -= lr / (1 - b1^t) * m / (sqrt(v) / sqrt(1 - b2^t) + eps),  t = step + 1
+//   adam_step    step[i] = t for every tensor (after all blocks have read the old step)
+// All tensors take the same number of steps (one optimizer), so tensor 0's step is the clock.
+constexpr int ADAM_MAXT = 16, ADAM_TPB = 256, ADAM_PER = 4;
+
+struct AdamArgs {
+  float* p[ADAM_MAXT];
+  const float* g[ADAM_MAXT];
+  float* m[ADAM_MAXT];
+  float* v[ADAM_MAXT];
+  float* step[ADAM_MAXT];
+  long long start[ADAM_MAXT + 1];   // prefix offsets of the tensors in the concatenation
+  int nt;
+};
+
+__device__ inline int adam_tensor(const AdamArgs& a, long long e) {
+  int t = 0;
+  while (t + 1 < a.nt && e >= a.start[t + 1]) t++;
+  return t;
+}
+
+__global__ __launch_bounds__(ADAM_TPB) void adam_sqsum_kernel(AdamArgs a, float* __restrict__ part) {
+  __shared__ float red[ADAM_TPB / 64];
+  float acc = 0.f;
+  const long long base = (long long)blockIdx.x * ADAM_TPB * ADAM_PER;
+  for (int k = 0; k < ADAM_PER; k++) {
+    const long long e = base + (long long)k * ADAM_TPB + threadIdx.x;
+    if (e < a.start[a.nt]) {
+      const int t = adam_tensor(a, e);
+      const float g = a.g[t][e - a.start[t]];
+      acc += g * g;
+    }
+  }
+  for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(ADAM_TPB) void adam_update_kernel(AdamArgs a, const float* __restrict__ part, int nblk,
+                                                               float max_norm, float lr, float b1, float b2,
+                                                               float omb1, float omb2, float eps) {
+  __shared__ float coef_s;
+  if (threadIdx.x < 64) {
+    float t = 0.f;
+    for (int k = threadIdx.x; k < nblk; k += 64) t += part[k];
+    for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o);
+    if (threadIdx.x == 0) coef_s = max_norm > 0.f ? fminf(1.f, max_norm / (sqrtf(t) + 1e-6f)) : 1.f;
+  }
+  __syncthreads();
+  const float c = coef_s;
+  const float step = a.step[0][0] + 1.f;
+  const float bc1 = 1.f - powf(b1, step), bc2s = sqrtf(1.f - powf(b2, step));
+  const float step_size = lr / bc1;
+  const long long base = (long long)blockIdx.x * ADAM_TPB * ADAM_PER;
+  for (int k = 0; k < ADAM_PER; k++) {
+    const long long e = base + (long long)k * ADAM_TPB + threadIdx.x;
+    if (e >= a.start[a.nt]) break;
+    const int t = adam_tensor(a, e);
+    const long long i = e - a.start[t];
+    const float g = a.g[t][i] * c;
+    const float m = b1 * a.m[t][i] + omb1 * g;        // omb = 1 - beta, rounded once from double
+    const float v = b2 * a.v[t][i] + omb2 * g * g;
+    a.m[t][i] = m;
+    a.v[t][i] = v;
+    a.p[t][i] -= step_size * m / (sqrtf(v) / bc2s + eps);
+  }
+}
+
+__global__ void adam_step_kernel(AdamArgs a) {
+  const float step = a.step[0][0] + 1.f;
+  __syncthreads();
+  if ((int)threadIdx.x < a.nt) a.step[threadIdx.x][0] = step;
+}
+
 // Column sums of a row-major [rows][cols] float32 matrix: out[c] = sum_r x[r][c].  The PPO
 // update's bias gradients (sum of the output gradient over the minibatch, [32768][256]) and the
 // split-K weight-gradient finish (sum over S slices of [S][out*in]).  A workgroup is a tile of
@@ -494,6 +576,34 @@ hipError_t launch_ppo_loss_bwd(const float* logp, const float* v, int B, float c
   const int nblk = (B + LOSS_TPB - 1) / LOSS_TPB;
   hipLaunchKernelGGL(ppo_loss_bwd_kernel, dim3(nblk), dim3(256), 0, stream, logp, v, B, clip, ws, nblk, g_pg, g_vf,
                      g_logp, g_v);
+  return hipGetLastError();
+}
+
+int adam_partials(long long total) {
+  return (int)((total + (long long)ADAM_TPB * ADAM_PER - 1) / ((long long)ADAM_TPB * ADAM_PER));
+}
+
+hipError_t launch_adam_clip(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
+                            float* const* step, const long long* numel, float* part, float max_norm, double lr,
+                            double b1, double b2, double eps, hipStream_t stream) {
+  if (nt <= 0 || nt > ADAM_MAXT) return hipErrorInvalidValue;
+  AdamArgs a{};
+  a.nt = nt;
+  a.start[0] = 0;
+  for (int t = 0; t < nt; t++) {
+    a.p[t] = p[t];
+    a.g[t] = g[t];
+    a.m[t] = m[t];
+    a.v[t] = v[t];
+    a.step[t] = step[t];
+    a.start[t + 1] = a.start[t] + numel[t];
+  }
+  const int nblk = adam_partials(a.start[nt]);
+  if (nblk <= 0) return hipSuccess;
+  hipLaunchKernelGGL(adam_sqsum_kernel, dim3(nblk), dim3(ADAM_TPB), 0, stream, a, part);
+  hipLaunchKernelGGL(adam_update_kernel, dim3(nblk), dim3(ADAM_TPB), 0, stream, a, (const float*)part, nblk,
+                     max_norm, (float)lr, (float)b1, (float)b2, (float)(1.0 - b1), (float)(1.0 - b2), (float)eps);
+  hipLaunchKernelGGL(adam_step_kernel, dim3(1), dim3(64), 0, stream, a);
   return hipGetLastError();
 }
 

@@ -132,6 +132,40 @@ def ppo_loss(logp, v, idx, adv, ret, old_logp, clip):
     return _PPOLossFn.apply(logp, v, idx, adv, ret, old_logp, clip)
 
 
+def adam_clip_step(opt, params, max_norm, workspace=None):
+    """clip_grad_norm_(params, max_norm) + opt.step() for a single-group torch Adam on a device in
+    three HIP launches (hs_adam_clip).  Reads and updates the optimizer's own state tensors
+    (exp_avg, exp_avg_sq, capturable float32 step), so torch's state_dict / SB3 checkpoints see
+    the same state; initialises it the way torch's Adam does on its first step.  Returns the
+    workspace (reuse it: a persistent buffer keeps graph captures valid)."""
+    import ctypes as C
+    from . import _lib
+    grp = opt.param_groups[0]
+    assert len(opt.param_groups) == 1 and not grp.get("amsgrad") and not grp.get("weight_decay")
+    assert not grp.get("maximize") and len(params) <= 16
+    dev = params[0].device
+    for p in params:
+        st = opt.state[p]
+        if len(st) == 0:
+            st["step"] = torch.zeros((), dtype=torch.float32, device=dev)
+            st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+    L = _lib.lib()
+    total = sum(p.numel() for p in params)
+    if workspace is None:
+        workspace = torch.empty(max(1, int(L.hs_adam_workspace(total))), dtype=torch.float32, device=dev)
+    nt = len(params)
+    arr = lambda xs: (C.c_void_p * nt)(*[x.data_ptr() for x in xs])   # noqa: E731
+    sts = [opt.state[p] for p in params]
+    b1, b2 = grp["betas"]
+    _lib.check(L.hs_adam_clip(nt, arr(params), arr([p.grad for p in params]), arr([s["exp_avg"] for s in sts]),
+                              arr([s["exp_avg_sq"] for s in sts]), arr([s["step"] for s in sts]),
+                              (C.c_int64 * nt)(*[p.numel() for p in params]), workspace.data_ptr(),
+                              float(max_norm), float(grp["lr"]), float(b1), float(b2), float(grp["eps"]),
+                              torch.cuda.current_stream(dev).cuda_stream))
+    return workspace
+
+
 def colsum(x):
     """Column sums of a contiguous [rows, cols] float32 device matrix through hs_colsum
     (ppo.hip): deterministic, and 3-5x faster than torch's dim-0 reduction at the PPO update's
@@ -627,12 +661,20 @@ class PPO:
                 self.opt.zero_grad(set_to_none=True)
                 loss.backward()
                 self._allreduce_grads()
-                torch.nn.utils.clip_grad_norm_(self.policy.parameters(), self.max_grad_norm)
-                self.opt.step()
+                self._clip_and_step()
                 stats.append((pg.detach(), vf.detach()))
         pg = torch.stack([s[0] for s in stats]).mean().item()
         vf = torch.stack([s[1] for s in stats]).mean().item()
         return dict(policy_loss=pg, value_loss=vf)
+
+    def _clip_and_step(self):
+        """clip_grad_norm_(max_grad_norm) + Adam step: hs_adam_clip on a device, torch on the CPU."""
+        params = self.flat
+        if params[0].is_cuda:
+            self._adam_ws = adam_clip_step(self.opt, params, self.max_grad_norm, getattr(self, "_adam_ws", None))
+        else:
+            torch.nn.utils.clip_grad_norm_(params, self.max_grad_norm)
+            self.opt.step()
 
     # -- HIP-graph update ----------------------------------------------------------------------
     def _build_graphs(self):
@@ -669,8 +711,7 @@ class PPO:
                     n = p.numel()
                     p.grad.copy_(self._g_flat[o:o + n].view_as(p.grad)).mul_(1.0 / world)
                     o += n
-            torch.nn.utils.clip_grad_norm_(params, self.max_grad_norm)
-            self.opt.step()
+            self._clip_and_step()
 
         saved_p = [p.detach().clone() for p in params]
         saved_s = {id(p): {k: v.clone() for k, v in self.opt.state[p].items()} for p in params if p in self.opt.state}

@@ -361,3 +361,35 @@ def test_fused_ppo_loss_matches_torch(B):
     assert abs(pg - pg_r) <= 1e-5 * (1 + abs(pg_r)) and abs(vf - vf_r) <= 1e-5 * (1 + abs(vf_r))
     assert torch.allclose(glp, glp_r, rtol=1e-4, atol=1e-6 * float(glp_r.abs().max()) + 1e-12)
     assert torch.allclose(gv, gv_r, rtol=1e-5, atol=1e-9)
+
+
+def test_adam_clip_matches_torch_clip_and_adam():
+    """hs_adam_clip (clip_grad_norm_ + Adam in three launches) == torch.nn.utils.clip_grad_norm_ +
+    torch.optim.Adam over several steps, on an MLP's parameter list, clipping active and not."""
+    from mujocoposelearning_amd.ppo import adam_clip_step
+    torch.manual_seed(0)
+    nets = [torch.nn.Sequential(torch.nn.Linear(352, 256), torch.nn.ReLU(), torch.nn.Linear(256, 21)).cuda()
+            for _ in range(2)]
+    nets[1].load_state_dict(nets[0].state_dict())
+    opts = [torch.optim.Adam(n.parameters(), lr=3e-4, eps=1e-5) for n in nets]
+    g = torch.Generator(device="cuda").manual_seed(1)
+    ws = None
+    for step, (scale, max_norm) in enumerate([(10.0, 0.5), (0.01, 0.5), (3.0, 0.5), (1.0, 0.0), (5.0, 0.5)]):
+        grads = [torch.randn(p.shape, device="cuda", generator=g) * scale for p in nets[0].parameters()]
+        for n in nets:
+            for p, gr in zip(n.parameters(), grads):
+                p.grad = gr.clone()
+        ws = adam_clip_step(opts[0], list(nets[0].parameters()), max_norm, ws)
+        if max_norm > 0:
+            torch.nn.utils.clip_grad_norm_(nets[1].parameters(), max_norm)
+        opts[1].step()
+        for a, b in zip(nets[0].parameters(), nets[1].parameters()):
+            assert torch.allclose(a, b, rtol=1e-5, atol=1e-6), (step, float((a - b).abs().max()))
+    sa, sb = opts[0].state_dict()["state"], opts[1].state_dict()["state"]
+    for k in sa:
+        assert float(sa[k]["step"]) == float(sb[k]["step"]) == 5
+        for key in ("exp_avg", "exp_avg_sq"):
+            x, y = sa[k][key], sb[k][key]
+            err = float((x - y).abs().max()) / float(y.abs().max())
+            print(k, key, err, float(y.abs().max()))
+            assert err < 1e-5, (k, key, err)
