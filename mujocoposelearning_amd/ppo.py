@@ -351,7 +351,8 @@ class ActorCritic(nn.Module):
             return mean, value
         w1, b1, mid, w3, b3 = pk
         n = obs.shape[0]
-        h = torch.addmm(b1, obs, w1).relu_()                      # [N, 2H]
+        # [N, 2H]: layer 1 of both nets, ReLU in the GEMM epilogue on a device
+        h = torch._addmm_activation(b1, obs, w1) if obs.is_cuda else torch.addmm(b1, obs, w1).relu_()
         h = h.view(n, 2, -1).transpose(0, 1)                      # [2, N, H] (strided)
         for w, b in mid:
             h = torch.baddbmm(b, h, w).relu_()
