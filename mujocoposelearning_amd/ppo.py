@@ -526,7 +526,7 @@ class PPO:
         T, N = self.n_steps, env.num_envs
         pol.pack_heads()
         if self.graphs and self._rollout_graph is None and getattr(env, "graph_safe", False):
-            self._capture_rollout()
+            self._capture_rollout()                   # on failure: graphs off, eager body below
         if self._rollout_graph is not None:
             self._rollout_graph.replay()
         else:
@@ -573,9 +573,14 @@ class PPO:
                 pol.value(self.obs)
         torch.cuda.current_stream(dev).wait_stream(side)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._rollout_body()
-        self._rollout_graph = g
+        try:
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                self._rollout_body()
+            self._rollout_graph = g
+        except RuntimeError as e:                  # nothing ran during capture: stay eager
+            import warnings
+            warnings.warn(f"rollout graph capture failed ({e}); collecting rollouts eagerly")
+            self.graphs = False
 
     def _collect_rollouts_torch(self):
         """SB3 PPO.collect_rollouts on device.  No host synchronisation inside the loop: the
@@ -728,25 +733,36 @@ class PPO:
         self.opt.zero_grad(set_to_none=True)
         pool = torch.cuda.graph_pool_handle()
         g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g1, pool=pool):
-            g1_body()
-        with torch.cuda.graph(g2, pool=pool):
-            g2_body()
-        with torch.no_grad():                      # undo the warm-up steps in place
-            for p, q in zip(params, saved_p):
-                p.copy_(q)
-            for p in params:
-                st, old = self.opt.state.get(p, {}), saved_s.get(id(p))
-                for k, v in st.items():
-                    if old is not None and k in old:
-                        v.copy_(old[k])
-                    elif torch.is_tensor(v):
-                        v.zero_()
-        self._graphs = (g1, g2)
+        try:
+            # thread_local: RCCL's proxy threads (world > 1) may touch the runtime meanwhile
+            with torch.cuda.graph(g1, pool=pool, capture_error_mode="thread_local"):
+                g1_body()
+            with torch.cuda.graph(g2, pool=pool, capture_error_mode="thread_local"):
+                g2_body()
+            self._graphs = (g1, g2)
+        except RuntimeError as e:                  # capture refused: train eagerly from here on
+            import warnings
+            warnings.warn(f"PPO update graph capture failed ({e}); falling back to the eager update")
+            self.graphs = False
+            self._graphs = None
+            self.opt.zero_grad(set_to_none=True)
+        finally:
+            with torch.no_grad():                  # undo the warm-up steps in place
+                for p, q in zip(params, saved_p):
+                    p.copy_(q)
+                for p in params:
+                    st, old = self.opt.state.get(p, {}), saved_s.get(id(p))
+                    for k, v in st.items():
+                        if old is not None and k in old:
+                            v.copy_(old[k])
+                        elif torch.is_tensor(v):
+                            v.zero_()
 
     def _train_graphed(self, adv, ret):
         if self._graphs is None:
             self._build_graphs()
+            if self._graphs is None:
+                return self.train(adv, ret)       # capture failed: self.graphs is now False
         g1, g2 = self._graphs
         M, bs = self.n_steps * self.env.num_envs, self.batch_size
         self._g_adv.copy_(adv.reshape(-1))
