@@ -359,6 +359,25 @@ class ActorCritic(nn.Module):
         out = torch.baddbmm(b3, h, w3)                            # [2, N, A]
         return out[0], out[1, :, 0]
 
+    @torch.no_grad()
+    def net_forward(self, obs, which):
+        """One of the two nets on its own from the packed weights (which = 0: pi -> mean [N, A],
+        1: vf -> value [N]); hidden layers with the ReLU in the GEMM epilogue on a device.  The
+        device rollout samples with the pi net per step and evaluates the vf net once per rollout
+        over the whole [T*N] buffer (the policy is fixed during a rollout)."""
+        pk = getattr(self, "_packed", None)
+        if pk is None:
+            return self(obs)[which]
+        w1, b1, mid, w3, b3 = pk
+        H = w1.shape[1] // 2
+        act = (lambda b, x, w: torch._addmm_activation(b, x, w)) if obs.is_cuda else (  # noqa: E731
+            lambda b, x, w: torch.addmm(b, x, w).relu_())
+        h = act(b1[which * H:(which + 1) * H], obs, w1[:, which * H:(which + 1) * H])
+        for w, b in mid:
+            h = act(b[which, 0], h, w[which])
+        out = torch.addmm(b3[which, 0], h, w3[which])
+        return out if which == 0 else out[:, 0]
+
 
 def gae(rewards, values, dones, last_values, last_dones, gamma, lam):
     """SB3 RolloutBuffer.compute_returns_and_advantage (stable_baselines3 2.3.2 common/buffers.py):
@@ -505,6 +524,8 @@ class PPO:
         self.flat = [p for p in self.policy.parameters()]
         # device rollout: the clipped actions the env steps with, and the Philox noise stream
         self._act_clip = torch.zeros(N, A, dtype=f, device=dev)
+        self._zero_n = torch.zeros(N, dtype=f, device=dev)        # value input of hs_ppo_act (values are
+        self._val_scratch = torch.zeros(N, dtype=f, device=dev)   # filled once per rollout, see below)
         self._noise_seed = (int(seed) + 7919 * rank) * 0x9E3779B97F4A7C15 % 2 ** 64
         self._noise_ctr = torch.zeros(1, dtype=torch.int64, device=dev)    # Philox step counter (device)
         self._rollout_graph = None
@@ -542,13 +563,13 @@ class PPO:
     def _rollout_body(self):
         """The T env steps of a device rollout (what the rollout graph captures)."""
         b, env, pol = self.buf, self.env, self.policy
-        T = self.n_steps
+        T, N = self.n_steps, env.num_envs
         gamma = float(self.gamma)
         b["obs"][0].copy_(self.obs)
         for t in range(T):
-            mean, value = pol.heads(b["obs"][t])
-            ppo_act(mean, value, pol.log_std.detach(), self.episode_start, self._noise_seed, t, False,
-                    b["act"][t], self._act_clip, b["logp"][t], b["val"][t], b["start"][t],
+            mean = pol.net_forward(b["obs"][t], 0) if pol._packed is not None else pol.heads(b["obs"][t])[0]
+            ppo_act(mean, self._zero_n, pol.log_std.detach(), self.episode_start, self._noise_seed, t, False,
+                    b["act"][t], self._act_clip, b["logp"][t], self._val_scratch, b["start"][t],
                     counter_base=self._noise_ctr)
             obs, rew, term, trunc = env.step_tensors(self._act_clip)
             nxt = b["obs"][t + 1] if t + 1 < T else self.obs
@@ -556,6 +577,10 @@ class PPO:
                      b["rew"][t], b["done"][t], self.ep_acc, b["epret"][t], self.episode_start,
                      terminal_obs=env.terminal_obs.float(), boot_obs_out=b["tobs"][t], boot_out=b["boot"][t])
         self._noise_ctr.add_(T)
+        # values of every buffered obs in one batched vf forward (SB3 stores V(obs_t) per step;
+        # the policy does not change inside a rollout, so this is the same quantity)
+        b["val"].view(-1).copy_(pol.net_forward(b["obs"].view(T * N, -1), 1) if pol._packed is not None
+                                else pol.value(b["obs"].view(T * N, -1)))
 
     def _capture_rollout(self):
         """Capture the whole T-step device rollout as one HIP graph (policy GEMMs, hs_ppo_act, the

@@ -307,3 +307,17 @@ def test_fused_linear_relu_matches_modules():
         out.append([y.detach()] + [p.grad.clone() for p in seq.parameters()])
     for a, b in zip(*out):
         assert torch.allclose(a, b, rtol=1e-4, atol=1e-4 * float(b.abs().max())), float((a - b).abs().max())
+
+
+def test_net_forward_matches_heads():
+    """ActorCritic.net_forward (one net from the packed weights, used by the device rollout) equals
+    the corresponding output of heads() / forward()."""
+    torch.manual_seed(1)
+    pol = ActorCritic(352, 21, (256, 256), (256, 256), torch.nn.ReLU)
+    for p in pol.parameters():
+        torch.nn.init.normal_(p, std=0.05)
+    obs = torch.randn(32, 352)
+    pol.pack_heads()
+    mean, value = pol.heads(obs)
+    assert torch.allclose(pol.net_forward(obs, 0), mean, atol=1e-5)
+    assert torch.allclose(pol.net_forward(obs, 1), value, atol=1e-5)
