@@ -22,221 +22,9 @@ import torch
 import torch.nn as nn
 
 
-_SPLITK_ROWS = 2048      # rows per split-K slice of a weight gradient
-SPLIT_K = True           # module switch (A/B probes)
-
-
-class _SplitKLinearFn(torch.autograd.Function):
-    """y = x W^T + b whose weight gradient is computed as S batched [out x rows] x [rows x in]
-    products summed over S, instead of one GEMM with a K = batch-size reduction.  The library's
-    kernel for a 256 x 32768 x 352 weight gradient runs at a few TFLOP/s (one long reduction on few
-    tiles); split into 16 slices it fills the chip (tests/gpu_mlp_probe.py: minibatch fwd+bwd
-    1.45 -> 0.97 ms at 32768 samples)."""
-
-    @staticmethod
-    def forward(ctx, x, w, b, s):
-        ctx.save_for_backward(x, w)
-        ctx.s = s
-        return torch.addmm(b, x, w.t())
-
-    @staticmethod
-    def backward(ctx, g):
-        x, w = ctx.saved_tensors
-        s = ctx.s
-        g = g.contiguous()
-        gx = g @ w if ctx.needs_input_grad[0] else None
-        part = torch.bmm(g.view(s, -1, g.shape[1]).transpose(1, 2), x.view(s, -1, x.shape[1]))   # [S, out, in]
-        gw = colsum(part.view(s, -1)).view_as(w)
-        return gx, gw, colsum(g), None
-
-
-class _GaussLogpFn(torch.autograd.Function):
-    """DiagGaussianDistribution.log_prob(actions) for mean [N, A] (A <= 32) on a device: one
-    hs_gauss_logp launch forward; backward one hs_gauss_logp_grad launch (dL/dmean and the
-    per-row dL/dlog_std terms) + hs_colsum over the rows."""
-
-    @staticmethod
-    def forward(ctx, mean, actions, log_std):
-        from . import _lib
-        if mean.stride(1) != 1:
-            mean = mean.contiguous()
-        actions = actions.contiguous()
-        N, A = mean.shape
-        logp = torch.empty(N, dtype=torch.float32, device=mean.device)
-        st = torch.cuda.current_stream(mean.device).cuda_stream
-        _lib.check(_lib.lib().hs_gauss_logp(mean.data_ptr(), mean.stride(0), actions.data_ptr(), log_std.data_ptr(),
-                                            logp.data_ptr(), N, A, st))
-        ctx.save_for_backward(mean, actions, log_std)
-        return logp
-
-    @staticmethod
-    def backward(ctx, g):
-        from . import _lib
-        mean, actions, log_std = ctx.saved_tensors
-        N, A = mean.shape
-        g = g.contiguous()
-        g_mean = torch.empty(N, A, dtype=torch.float32, device=mean.device)
-        rows = torch.empty(N, A, dtype=torch.float32, device=mean.device)
-        st = torch.cuda.current_stream(mean.device).cuda_stream
-        _lib.check(_lib.lib().hs_gauss_logp_grad(mean.data_ptr(), mean.stride(0), actions.data_ptr(),
-                                                 log_std.data_ptr(), g.data_ptr(), g_mean.data_ptr(), rows.data_ptr(),
-                                                 N, A, st))
-        return g_mean, None, colsum(rows)
-
-
-class _PPOLossFn(torch.autograd.Function):
-    """SB3 PPO.train's minibatch policy/value loss (advantage normalisation, clipped surrogate,
-    value MSE) over indices idx into the rollout arrays: one hs_ppo_loss launch forward, one
-    hs_ppo_loss_grad launch backward (dL/dlog_prob, dL/dvalues)."""
-
-    @staticmethod
-    def forward(ctx, logp, v, idx, adv, ret, old_logp, clip):
-        from . import _lib
-        logp, v = logp.contiguous(), v.contiguous()
-        B = logp.shape[0]
-        dev = logp.device
-        L = _lib.lib()
-        pg = torch.empty((), dtype=torch.float32, device=dev)
-        vf = torch.empty((), dtype=torch.float32, device=dev)
-        ws = torch.empty(int(L.hs_ppo_loss_workspace(B)), dtype=torch.float32, device=dev)
-        st = torch.cuda.current_stream(dev).cuda_stream
-        _lib.check(L.hs_ppo_loss(logp.data_ptr(), v.data_ptr(), idx.data_ptr(), adv.data_ptr(), ret.data_ptr(),
-                                 old_logp.data_ptr(), B, float(clip), pg.data_ptr(), vf.data_ptr(), ws.data_ptr(), st))
-        ctx.save_for_backward(logp, v, ws)
-        ctx.clip = float(clip)
-        return pg, vf
-
-    @staticmethod
-    def backward(ctx, g_pg, g_vf):
-        from . import _lib
-        logp, v, ws = ctx.saved_tensors
-        B = logp.shape[0]
-        dev = logp.device
-        z = torch.zeros((), dtype=torch.float32, device=dev)
-        g_pg = z if g_pg is None else g_pg.to(torch.float32).contiguous()
-        g_vf = z if g_vf is None else g_vf.to(torch.float32).contiguous()
-        g_logp = torch.empty(B, dtype=torch.float32, device=dev)
-        g_v = torch.empty(B, dtype=torch.float32, device=dev)
-        st = torch.cuda.current_stream(dev).cuda_stream
-        _lib.check(_lib.lib().hs_ppo_loss_grad(logp.data_ptr(), v.data_ptr(), B, ctx.clip, ws.data_ptr(),
-                                               g_pg.data_ptr(), g_vf.data_ptr(), g_logp.data_ptr(), g_v.data_ptr(),
-                                               st))
-        return g_logp, g_v, None, None, None, None, None
-
-
-def ppo_loss(logp, v, idx, adv, ret, old_logp, clip):
-    """(policy_loss, value_loss) of one minibatch on a device (hs_ppo_loss / hs_ppo_loss_grad)."""
-    for t in (adv, ret, old_logp):
-        assert t.dtype == torch.float32 and t.is_contiguous() and t.dim() == 1
-    assert idx.dtype == torch.int64 and idx.is_contiguous()
-    return _PPOLossFn.apply(logp, v, idx, adv, ret, old_logp, clip)
-
-
-def adam_clip_step(opt, params, max_norm, workspace=None):
-    """clip_grad_norm_(params, max_norm) + opt.step() for a single-group torch Adam on a device in
-    three HIP launches (hs_adam_clip).  Reads and updates the optimizer's own state tensors
-    (exp_avg, exp_avg_sq, capturable float32 step), so torch's state_dict / SB3 checkpoints see
-    the same state; initialises it the way torch's Adam does on its first step.  Returns the
-    workspace (reuse it: a persistent buffer keeps graph captures valid)."""
-    import ctypes as C
-    from . import _lib
-    grp = opt.param_groups[0]
-    assert len(opt.param_groups) == 1 and not grp.get("amsgrad") and not grp.get("weight_decay")
-    assert not grp.get("maximize") and len(params) <= 16
-    dev = params[0].device
-    for p in params:
-        st = opt.state[p]
-        if len(st) == 0:
-            st["step"] = torch.zeros((), dtype=torch.float32, device=dev)
-            st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-            st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-    L = _lib.lib()
-    total = sum(p.numel() for p in params)
-    if workspace is None:
-        workspace = torch.empty(max(1, int(L.hs_adam_workspace(total))), dtype=torch.float32, device=dev)
-    nt = len(params)
-    arr = lambda xs: (C.c_void_p * nt)(*[x.data_ptr() for x in xs])   # noqa: E731
-    sts = [opt.state[p] for p in params]
-    b1, b2 = grp["betas"]
-    _lib.check(L.hs_adam_clip(nt, arr(params), arr([p.grad for p in params]), arr([s["exp_avg"] for s in sts]),
-                              arr([s["exp_avg_sq"] for s in sts]), arr([s["step"] for s in sts]),
-                              (C.c_int64 * nt)(*[p.numel() for p in params]), workspace.data_ptr(),
-                              float(max_norm), float(grp["lr"]), float(b1), float(b2), float(grp["eps"]),
-                              torch.cuda.current_stream(dev).cuda_stream))
-    return workspace
-
-
-def colsum(x):
-    """Column sums of a contiguous [rows, cols] float32 device matrix through hs_colsum
-    (ppo.hip): deterministic, and 3-5x faster than torch's dim-0 reduction at the PPO update's
-    shapes ([32768, 256] bias gradients, [16, 90112] split-K finishes)."""
-    from . import _lib
-    assert x.dim() == 2 and x.is_contiguous() and x.dtype == torch.float32 and x.is_cuda
-    rows, cols = x.shape
-    L = _lib.lib()
-    ws_n = int(L.hs_colsum_workspace(rows, cols))
-    ws = torch.empty(ws_n, dtype=torch.float32, device=x.device) if ws_n else None
-    out = torch.empty(cols, dtype=torch.float32, device=x.device)
-    _lib.check(L.hs_colsum(x.data_ptr(), rows, cols, ws.data_ptr() if ws is not None else None, out.data_ptr(),
-                           torch.cuda.current_stream(x.device).cuda_stream))
-    return out
-
-
-class _SplitKLinearReLUFn(torch.autograd.Function):
-    """relu(x W^T + b) with the ReLU in the GEMM's epilogue (hipBLASLt bias+ReLU through
-    torch._addmm_activation: no separate activation pass over [B, out]); backward masks the
-    upstream gradient with y > 0, then takes _SplitKLinearFn's split-K gradients."""
-
-    @staticmethod
-    def forward(ctx, x, w, b, s):
-        y = torch._addmm_activation(b, x, w.t())
-        ctx.save_for_backward(x, w, y)
-        ctx.s = s
-        return y
-
-    @staticmethod
-    def backward(ctx, g):
-        x, w, y = ctx.saved_tensors
-        s = ctx.s
-        g = torch.where(y > 0, g, torch.zeros((), dtype=g.dtype, device=g.device))
-        gx = g @ w if ctx.needs_input_grad[0] else None
-        part = torch.bmm(g.view(s, -1, g.shape[1]).transpose(1, 2), x.view(s, -1, x.shape[1]))
-        return gx, colsum(part.view(s, -1)).view_as(w), colsum(g), None
-
-
-def _splitk_rows(x):
-    n = x.shape[0] if x.dim() == 2 else 0
-    if SPLIT_K and x.is_cuda and torch.is_grad_enabled() and n >= 2 * _SPLITK_ROWS and n % _SPLITK_ROWS == 0:
-        return n // _SPLITK_ROWS
-    return 0
-
-
-class Linear(nn.Linear):
-    """nn.Linear (same parameters and state_dict keys, so SB3 checkpoints map 1:1) with split-K
-    weight gradients for large device minibatches; small or CPU batches take nn.Linear's path."""
-
-    def forward(self, x):
-        s = _splitk_rows(x)
-        if s:
-            return _SplitKLinearFn.apply(x, self.weight, self.bias, s)
-        return super().forward(x)
-
-
-def mlp_forward(seq, x):
-    """nn.Sequential forward that runs each (Linear, ReLU) pair of a large device minibatch as one
-    fused GEMM + epilogue (_SplitKLinearReLUFn); everything else module by module."""
-    mods = list(seq)
-    i = 0
-    while i < len(mods):
-        m = mods[i]
-        if (isinstance(m, Linear) and i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU)
-                and _splitk_rows(x)):
-            x = _SplitKLinearReLUFn.apply(x, m.weight, m.bias, _splitk_rows(x))
-            i += 2
-            continue
-        x = m(x)
-        i += 1
-    return x
+from .ppo_ops import (Linear, _GaussLogpFn, _PPOLossFn, _SplitKLinearFn, _SplitKLinearReLUFn,  # noqa: F401
+                      _SPLITK_ROWS, adam_clip_step, colsum, gae_device, mlp_forward, ppo_act, ppo_loss,
+                      ppo_post)
 
 
 def _flat_packed(pk):
@@ -402,65 +190,6 @@ def gae(rewards, values, dones, last_values, last_dones, gamma, lam):
         last = delta + gamma * lam * nonterm * last
         adv[t] = last
     return adv, adv + values
-
-
-def gae_device(rewards, values, dones, last_values, last_dones, gamma, lam):
-    """GAE through the C ABI (hs_gae) on the tensors' device and current stream; float32."""
-    from . import _lib
-    T, N = rewards.shape
-    f32 = lambda x: x.to(torch.float32).contiguous()   # noqa: E731
-    r, v, st, lv, ld = f32(rewards), f32(values), f32(dones), f32(last_values), f32(last_dones)
-    adv = torch.empty_like(r)
-    ret = torch.empty_like(r)
-    with torch.cuda.device(r.device):
-        stream = torch.cuda.current_stream(r.device).cuda_stream
-        _lib.check(_lib.lib().hs_gae(r.data_ptr(), v.data_ptr(), st.data_ptr(), lv.data_ptr(), ld.data_ptr(),
-                                     adv.data_ptr(), ret.data_ptr(), T, N, float(gamma), float(lam), stream))
-    return adv, ret
-
-
-def ppo_act(mean, value, log_std, episode_start, seed, counter, deterministic, act_out, act_clip_out, logp_out,
-            val_out, start_out, stream=None, counter_base=None):
-    """hs_ppo_act on device tensors (ppo.hip): Gaussian sample + log-prob + clip + buffer writes.
-    The Philox counter is ``counter`` plus, if given, the int64 device scalar ``counter_base``
-    (read by the kernel, so a captured graph draws fresh noise on every replay)."""
-    from . import _lib
-    N, A = act_out.shape
-    assert mean.stride(1) == 1 and mean.shape == (N, A) and value.shape == (N,), (mean.shape, value.shape)
-    for t in (log_std, episode_start, act_out, act_clip_out, logp_out, val_out, start_out):
-        assert t.dtype == torch.float32 and t.is_contiguous()
-    st = torch.cuda.current_stream(mean.device).cuda_stream if stream is None else stream
-    _lib.check(_lib.lib().hs_ppo_act(mean.data_ptr(), mean.stride(0), value.data_ptr(), value.stride(0),
-                                     log_std.data_ptr(), episode_start.data_ptr(), int(seed) & (2 ** 64 - 1),
-                                     int(counter), None if counter_base is None else counter_base.data_ptr(),
-                                     int(bool(deterministic)), act_out.data_ptr(),
-                                     act_clip_out.data_ptr(), logp_out.data_ptr(), val_out.data_ptr(),
-                                     start_out.data_ptr(), N, A, st))
-
-
-def ppo_post(reward, terminated, truncated, terminal_value, gamma, obs, obs_out, reward_out, done_out, ep_acc,
-             ep_return_out, episode_start, terminal_obs=None, boot_obs_out=None, boot_out=None, stream=None):
-    """hs_ppo_post on device tensors (ppo.hip): reward bootstrap, dones, returns, next obs copy.
-    terminal_value None = deferred bootstrap: boot flags -> boot_out, terminal-obs rows of the
-    boot envs -> boot_obs_out (the caller adds gamma V(row) at the end of the rollout)."""
-    from . import _lib
-    N = reward.shape[0]
-    assert terminated.dtype == torch.uint8 and truncated.dtype == torch.uint8 and done_out.dtype == torch.bool
-    assert ep_acc.dtype == torch.float64 and ep_return_out.dtype == torch.float64
-    assert obs.is_contiguous() and obs_out.is_contiguous() and obs.numel() == obs_out.numel()
-    ptr = lambda t: None if t is None else t.data_ptr()     # noqa: E731
-    D = 0
-    if terminal_value is None:
-        assert terminal_obs.is_contiguous() and boot_obs_out.is_contiguous() and boot_out.dtype in (torch.bool,
-                                                                                                torch.uint8)
-        D = terminal_obs.shape[1]
-        assert boot_obs_out.shape == terminal_obs.shape == (N, D)
-    st = torch.cuda.current_stream(reward.device).cuda_stream if stream is None else stream
-    _lib.check(_lib.lib().hs_ppo_post(reward.data_ptr(), terminated.data_ptr(), truncated.data_ptr(),
-                                      ptr(terminal_value), ptr(terminal_obs), ptr(boot_obs_out), ptr(boot_out), D,
-                                      float(gamma), obs.data_ptr(), obs_out.data_ptr(), obs.numel(),
-                                      reward_out.data_ptr(), done_out.data_ptr(), ep_acc.data_ptr(),
-                                      ep_return_out.data_ptr(), episode_start.data_ptr(), N, st))
 
 
 class PPO:

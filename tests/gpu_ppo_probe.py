@@ -15,8 +15,8 @@ XML = os.path.join(ROOT, "tests", "golden", "humanoid.xml")
 
 
 def run(n=4096, iters=3, blas=None, fused=True, splitk=True):
-    from mujocoposelearning_amd import ppo as ppo_mod
-    ppo_mod.SPLIT_K = splitk
+    from mujocoposelearning_amd import ppo_ops
+    ppo_ops.SPLIT_K = splitk
     if blas:
         torch.backends.cuda.preferred_blas_library(blas)
     env = HumanoidVecEnv({"model_path": XML, "duration": 10.0, "reward_config": {"type": "stand"}, "frame_skip": 3},
