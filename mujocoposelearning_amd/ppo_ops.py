@@ -191,7 +191,7 @@ class _SplitKLinearReLUFn(torch.autograd.Function):
     def backward(ctx, g):
         x, w, y = ctx.saved_tensors
         s = ctx.s
-        g = torch.where(y > 0, g, torch.zeros((), dtype=g.dtype, device=g.device))
+        g = torch.ops.aten.threshold_backward(g, y, 0)      # g where y > 0 (ReLU backward, one pass)
         gx = g @ w if ctx.needs_input_grad[0] else None
         part = torch.bmm(g.view(s, -1, g.shape[1]).transpose(1, 2), x.view(s, -1, x.shape[1]))
         return gx, colsum(part.view(s, -1)).view_as(w), colsum(g), None
