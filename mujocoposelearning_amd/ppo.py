@@ -394,7 +394,10 @@ class PPO:
         ent_mean = self.policy.entropy()            # = evaluate()'s per-sample entropy, averaged
         if logp.is_cuda:                            # fused HIP loss (same formulas as below)
             pg, vf = ppo_loss(logp, v, idx, adv, ret, old_logp, self.clip_range)
-            return pg + self.ent_coef * (-ent_mean) + self.vf_coef * vf, pg, vf
+            loss = pg + self.vf_coef * vf
+            if self.ent_coef:                       # SB3's default ent_coef 0: the term has no gradient
+                loss = loss - self.ent_coef * ent_mean
+            return loss, pg, vf
         a = adv[idx]
         if a.numel() > 1:
             a = (a - a.mean()) / (a.std() + 1e-8)
