@@ -652,7 +652,7 @@ __device__ __forceinline__ T jtf_lane(MPtr<T> m, const Scratch<T>& s, int sl, co
 // Built only with -DHS_TIMING (libhsim_timing.so): s_memtime stamps accumulated per phase,
 // summed over waves into dbg[8000 + slot].  The product build compiles them out.
 #ifdef HS_TIMING
-constexpr int NSLOT = 24;
+constexpr int NSLOT = 26;
 struct PhaseClock {
   uint64_t acc[NSLOT] = {0};
   uint64_t prev = 0, t0 = 0;
@@ -1658,17 +1658,14 @@ __device__ __forceinline__ void foot_forces(MPtr<T> m, const Scratch<T>& s, T& l
 
 template <typename T>
 __device__ __forceinline__ T compute_reward(MPtr<T> m, const Scratch<T>& s, KPtr<T> k, T time,
-                            T energy_sum) {
+                            T energy_sum, T ctrl_sq) {
   // quaternion_to_euler (utils.py:3-21): pitch = arcsin(2(wy - zx)), not clamped
   T w = s.qpos[3], x = s.qpos[4], y = s.qpos[5], z = s.qpos[6];
   T roll = atan2(2 * (w * x + y * z), 1 - 2 * (x * x + y * y));
   T pitch = asin(2 * (w * y - z * x));
   T h = s.qpos[2];
-  int nu = m->nu;
   if (k->p.reward_id == REWARD_STAND || k->p.reward_id == REWARD_WALK) {
-    T c2 = 0;
-    for (int u = 0; u < nu; u++) c2 += s.ctrl[u] * s.ctrl[u];
-    T torque = exp(T(-0.05) * c2);
+    T torque = exp(T(-0.05) * ctrl_sq);     // sum(ctrl^2), reduced across the half-wave by the caller
     T post = T(0.5) * exp(T(-2) * (h - T(1.282)) * (h - T(1.282))) + T(0.5) * exp(T(-3) * (roll * roll + pitch * pitch));
     if (k->p.reward_id == REWARD_STAND) {
       // cfrc_ext is never computed by mj_step without sensors -> both "feet" forces are 0 (full_state:
@@ -1862,13 +1859,19 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !PGS) ? 2 : 1) void step_ker
       if (nsub > 0) {
         KPtr<T> k = opaque(ka);
         const int obs_dim = k->p.obs_dim;
+        HS_STAMP(st.clk, 22);
         if (active) write_obs(st.m, s, sl, st.qfa, k->b.obs + (size_t)env * obs_dim, obs_dim);
+        HS_STAMP(st.clk, 23);
         if (k->p.mode == MODE_ENV_STEP) {
           step_count += 1;
           bool trunc = step_count >= k->p.max_steps;
           T e = (sl >= 6 && sl < nv) ? st.qfa * s.qvel[sl] : T(0);
           T esum = hsum(e * e);
-          T r = trunc ? T(0) : compute_reward(st.m, s, k, time, esum);
+          const T cu = sl < st.m->nu ? s.ctrl[sl] : T(0);
+          const T csum = hsum(cu * cu);                 // sum ctrl^2 as one half-wave sum
+          HS_STAMP(st.clk, 24);
+          T r = trunc ? T(0) : compute_reward(st.m, s, k, time, esum, csum);
+          HS_STAMP(st.clk, 25);
           total += r;
           bool term = (double)time >= k->p.duration;
           if (sl == 0 && active) {
