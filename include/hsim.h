@@ -186,9 +186,6 @@ int hs_gauss_logp(const float* mean, int mean_ld, const float* actions, const fl
                   int A, void* stream);
 int hs_gauss_logp_grad(const float* mean, int mean_ld, const float* actions, const float* log_std,
                        const float* g_logp, float* g_mean, float* gls_rows, int N, int A, void* stream);
-/* out[c] = sum_r x[r][c] over a row-major [rows][cols] float32 device matrix, in a fixed
- * summation order (deterministic).  `workspace` must hold hs_colsum_workspace(rows, cols) floats
- * (may be NULL when that is 0).  Asynchronous on `stream`. */
 /* SB3 PPO minibatch loss over B samples gathered by idx [B] (int64) from the rollout arrays
  * advantages / returns / old_log_prob [M]: log_prob [B] and values [B] are the policy's on the
  * minibatch.  a = advantages[idx] normalised (mean, unbiased std + 1e-8; not when B == 1),
@@ -217,8 +214,13 @@ uint64_t hs_adam_workspace(uint64_t total_numel);
 int hs_adam_clip(int nt, float* const* params, const float* const* grads, float* const* exp_avg,
                  float* const* exp_avg_sq, float* const* step, const int64_t* numel, float* workspace, float max_norm,
                  double lr, double beta1, double beta2, double eps, void* stream);
+/* out[c] = sum_r w[r] x[r][c] over a row-major [rows][cols] float32 device matrix (w = row_weight
+ * [rows], or 1 when NULL -- the weighted form is a rank-1 weight gradient g'x), in a fixed
+ * summation order (deterministic).  `workspace` must hold hs_colsum_workspace(rows, cols) floats
+ * (may be NULL when that is 0).  Asynchronous on `stream`. */
 uint64_t hs_colsum_workspace(uint64_t rows, uint64_t cols);
-int hs_colsum(const float* x, uint64_t rows, uint64_t cols, float* workspace, float* out, void* stream);
+int hs_colsum(const float* x, uint64_t rows, uint64_t cols, const float* row_weight, float* workspace, float* out,
+              void* stream);
 const char* hs_last_error(void);
 const char* hs_version(void);
 

@@ -86,7 +86,7 @@ def lib():
         "hs_adam_clip": (i, [i, vp, vp, vp, vp, vp, vp, vp, C.c_float, C.c_double, C.c_double, C.c_double, C.c_double,
                              vp]),
         "hs_colsum_workspace": (u64, [u64, u64]),
-        "hs_colsum": (i, [vp, u64, u64, vp, vp, vp]),
+        "hs_colsum": (i, [vp, u64, u64, vp, vp, vp, vp]),
         "hs_last_error": (C.c_char_p, []),
         "hs_version": (C.c_char_p, []),
     }

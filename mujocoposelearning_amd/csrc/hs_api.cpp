@@ -522,11 +522,14 @@ int hs_adam_clip(int nt, float* const* params, const float* const* grads, float*
 
 uint64_t hs_colsum_workspace(uint64_t rows, uint64_t cols) { return hs::colsum_workspace(rows, cols); }
 
-int hs_colsum(const float* x, uint64_t rows, uint64_t cols, float* workspace, float* out, void* stream) {
+int hs_colsum(const float* x, uint64_t rows, uint64_t cols, const float* row_weight, float* workspace, float* out,
+              void* stream) {
   if (cols == 0) return 0;
   if (!out || (rows && !x)) return fail("hs_colsum: null buffer");
   if (hs::colsum_workspace(rows, cols) && !workspace) return fail("hs_colsum: workspace required");
-  return hip_ok(hs::launch_colsum(x, rows, cols, workspace, out, (hipStream_t)stream), "colsum_kernel") ? 0 : -1;
+  return hip_ok(hs::launch_colsum(x, rows, cols, row_weight, workspace, out, (hipStream_t)stream), "colsum_kernel")
+             ? 0
+             : -1;
 }
 
 int hs_gae(const float* rewards, const float* values, const float* episode_starts, const float* last_values,

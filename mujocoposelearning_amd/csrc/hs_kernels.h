@@ -82,7 +82,8 @@ hipError_t launch_ppo_post(const float* reward, const uint8_t* terminated, const
 // column sums of a row-major [rows][cols] float32 matrix (ppo.hip); workspace of
 // colsum_workspace(rows, cols) floats (0: none needed)
 size_t colsum_workspace(size_t rows, size_t cols);
-hipError_t launch_colsum(const float* x, size_t rows, size_t cols, float* workspace, float* out, hipStream_t stream);
+hipError_t launch_colsum(const float* x, size_t rows, size_t cols, const float* row_weight, float* workspace,
+                         float* out, hipStream_t stream);
 // diagonal-Gaussian log-prob of given actions and its backward (ppo.hip)
 hipError_t launch_gauss_logp(const float* mean, int mean_ld, const float* act, const float* log_std, float* logp, int N,
                              int A, hipStream_t stream);

@@ -434,6 +434,7 @@ constexpr int CS_COLS = 64, CS_PHASES = 16;
 
 __global__ __launch_bounds__(CS_COLS* CS_PHASES) void colsum_kernel(const float* __restrict__ x, size_t rows,
                                                                      size_t cols, size_t rows_per_chunk,
+                                                                     const float* __restrict__ rw,
                                                                      float* __restrict__ out) {
   __shared__ float part[CS_PHASES][CS_COLS];
   const int lane = threadIdx.x, ph = threadIdx.y;
@@ -445,14 +446,25 @@ __global__ __launch_bounds__(CS_COLS* CS_PHASES) void colsum_kernel(const float*
     const float* __restrict__ p = x + c;
     const size_t step = (size_t)CS_PHASES * cols;
     size_t r = r0 + ph;
-    for (; r + 3 * CS_PHASES < r1; r += 4 * CS_PHASES) {
-      const float* q = p + r * cols;
-      a0 += q[0];
-      a1 += q[step];
-      a2 += q[2 * step];
-      a3 += q[3 * step];
+    if (rw) {     // weighted rows: out[c] = sum_r rw[r] x[r][c] (a rank-1 weight gradient g' x)
+      for (; r + 3 * CS_PHASES < r1; r += 4 * CS_PHASES) {
+        const float* q = p + r * cols;
+        a0 += rw[r] * q[0];
+        a1 += rw[r + CS_PHASES] * q[step];
+        a2 += rw[r + 2 * CS_PHASES] * q[2 * step];
+        a3 += rw[r + 3 * CS_PHASES] * q[3 * step];
+      }
+      for (; r < r1; r += CS_PHASES) a0 += rw[r] * p[r * cols];
+    } else {
+      for (; r + 3 * CS_PHASES < r1; r += 4 * CS_PHASES) {
+        const float* q = p + r * cols;
+        a0 += q[0];
+        a1 += q[step];
+        a2 += q[2 * step];
+        a3 += q[3 * step];
+      }
+      for (; r < r1; r += CS_PHASES) a0 += p[r * cols];
     }
-    for (; r < r1; r += CS_PHASES) a0 += p[r * cols];
   }
   part[ph][lane] = (a0 + a1) + (a2 + a3);
   __syncthreads();
@@ -517,21 +529,22 @@ size_t colsum_workspace(size_t rows, size_t cols) {
   return chunks > 1 ? chunks * cols : 0;
 }
 
-hipError_t launch_colsum(const float* x, size_t rows, size_t cols, float* workspace, float* out, hipStream_t stream) {
+hipError_t launch_colsum(const float* x, size_t rows, size_t cols, const float* row_weight, float* workspace,
+                         float* out, hipStream_t stream) {
   if (cols == 0) return hipSuccess;
   const dim3 block(CS_COLS, CS_PHASES);
   const unsigned ctiles = (unsigned)((cols + CS_COLS - 1) / CS_COLS);
   const size_t chunks = colsum_chunks(rows, cols);
   if (rows == 0) return hipMemsetAsync(out, 0, cols * sizeof(float), stream);
   if (chunks <= 1) {
-    hipLaunchKernelGGL(colsum_kernel, dim3(ctiles, 1), block, 0, stream, x, rows, cols, rows, out);
+    hipLaunchKernelGGL(colsum_kernel, dim3(ctiles, 1), block, 0, stream, x, rows, cols, rows, row_weight, out);
     return hipGetLastError();
   }
   const size_t rpc = (rows + chunks - 1) / chunks;
   hipLaunchKernelGGL(colsum_kernel, dim3(ctiles, (unsigned)chunks), block, 0, stream, x, rows, cols, rpc,
-                     workspace);
+                     row_weight, workspace);
   hipLaunchKernelGGL(colsum_kernel, dim3(ctiles, 1), block, 0, stream, (const float*)workspace, chunks, cols,
-                     chunks, out);
+                     chunks, (const float*)nullptr, out);
   return hipGetLastError();
 }
 

@@ -37,6 +37,9 @@ class _SplitKLinearFn(torch.autograd.Function):
         x, w = ctx.saved_tensors
         s = ctx.s
         g = g.contiguous()
+        if g.shape[1] == 1:      # value head: rank-1 gradients without a K = 1 / N = 1 GEMM
+            gx = g * w if ctx.needs_input_grad[0] else None
+            return gx, colsum(x, g.view(-1)).view_as(w), g.sum(0), None
         gx = g @ w if ctx.needs_input_grad[0] else None
         part = torch.bmm(g.view(s, -1, g.shape[1]).transpose(1, 2), x.view(s, -1, x.shape[1]))   # [S, out, in]
         gw = colsum(part.view(s, -1)).view_as(w)
@@ -159,7 +162,7 @@ def adam_clip_step(opt, params, max_norm, workspace=None):
     return workspace
 
 
-def colsum(x):
+def colsum(x, row_weight=None):
     """Column sums of a contiguous [rows, cols] float32 device matrix through hs_colsum
     (ppo.hip): deterministic, and 3-5x faster than torch's dim-0 reduction at the PPO update's
     shapes ([32768, 256] bias gradients, [16, 90112] split-K finishes)."""
@@ -170,7 +173,10 @@ def colsum(x):
     ws_n = int(L.hs_colsum_workspace(rows, cols))
     ws = torch.empty(ws_n, dtype=torch.float32, device=x.device) if ws_n else None
     out = torch.empty(cols, dtype=torch.float32, device=x.device)
-    _lib.check(L.hs_colsum(x.data_ptr(), rows, cols, ws.data_ptr() if ws is not None else None, out.data_ptr(),
+    if row_weight is not None:
+        assert row_weight.is_contiguous() and row_weight.numel() == rows and row_weight.dtype == torch.float32
+    _lib.check(L.hs_colsum(x.data_ptr(), rows, cols, None if row_weight is None else row_weight.data_ptr(),
+                           ws.data_ptr() if ws is not None else None, out.data_ptr(),
                            torch.cuda.current_stream(x.device).cuda_stream))
     return out
 

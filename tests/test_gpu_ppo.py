@@ -161,6 +161,10 @@ def test_colsum_matches_fp64_sum(rows, cols):
     ref = x.double().sum(0).float()
     assert torch.equal(out, out2)                                   # fixed summation order
     assert torch.allclose(out, ref, rtol=1e-5, atol=1e-5 * max(1.0, rows ** 0.5)), float((out - ref).abs().max())
+    w = torch.randn(rows, device="cuda", generator=g)               # weighted rows (rank-1 weight gradient)
+    outw = colsum(x, w)
+    refw = (x.double() * w.double()[:, None]).sum(0).float()
+    assert torch.allclose(outw, refw, rtol=1e-5, atol=1e-5 * max(1.0, rows ** 0.5)), float((outw - refw).abs().max())
 
 
 def test_gauss_logp_forward_backward_match_torch():

@@ -256,12 +256,13 @@ def test_splitk_linear_grads_match_dense_linear():
     from mujocoposelearning_amd import ppo as ppo_mod
     torch.manual_seed(0)
     dev = "cuda"
-    for rows in (2 * ppo_mod._SPLITK_ROWS, 16 * ppo_mod._SPLITK_ROWS):
-        lin = ppo_mod.Linear(352, 256).to(dev)
-        ref = torch.nn.Linear(352, 256).to(dev)
+    for rows, out in ((2 * ppo_mod._SPLITK_ROWS, 256), (16 * ppo_mod._SPLITK_ROWS, 256),
+                      (16 * ppo_mod._SPLITK_ROWS, 1)):
+        lin = ppo_mod.Linear(352, out).to(dev)
+        ref = torch.nn.Linear(352, out).to(dev)
         ref.load_state_dict(lin.state_dict())
         x = torch.randn(rows, 352, device=dev, requires_grad=True)
-        g = torch.randn(rows, 256, device=dev)
+        g = torch.randn(rows, out, device=dev)
         (lin(x) * g).sum().backward()
         gx, gw, gb = x.grad.clone(), lin.weight.grad, lin.bias.grad
         x.grad = None
