@@ -31,6 +31,8 @@
  *                           surrogate, value MSE (stable_baselines3 2.3.2 ppo/ppo.py) and its backward
  *   hs_adam_clip         <- torch.nn.utils.clip_grad_norm_(max_grad_norm) + torch.optim.Adam.step of
  *                           SB3 PPO.train (ppo.py: max_grad_norm 0.5, Adam eps 1e-5)
+ *   hs_relu_grad_colsum, hs_colsum_pair <- the ReLU backward + bias / weight-gradient sums of the
+ *                           same loss.backward() (fewer passes and launches)
  *   hs_colsum            <- the bias-gradient and split-K weight-gradient reductions of the PPO
  *                           update's loss.backward() (SB3 PPO.train, ppo.py; train_sb3.py:229)
  *
@@ -218,6 +220,16 @@ int hs_adam_clip(int nt, float* const* params, const float* const* grads, float*
  * [rows], or 1 when NULL -- the weighted form is a rank-1 weight gradient g'x), in a fixed
  * summation order (deterministic).  `workspace` must hold hs_colsum_workspace(rows, cols) floats
  * (may be NULL when that is 0).  Asynchronous on `stream`. */
+/* ReLU backward fused with the bias gradient's first reduction pass, for a [rows][cols] float32
+ * upstream gradient g and the layer's ReLU output y: writes gm = (y > 0) ? g : 0 and per-chunk
+ * column sums of gm to partial [hs_colsum_partial_rows(rows, cols)][cols]. */
+uint64_t hs_colsum_partial_rows(uint64_t rows, uint64_t cols);
+int hs_relu_grad_colsum(const float* g, const float* y, uint64_t rows, uint64_t cols, float* gm, float* partial,
+                        void* stream);
+/* Two single-pass column sums in one launch: out0[c] = sum_r x0[r][c] ([rows0][cols0]) and
+ * out1[c] = sum_r x1[r][c] ([rows1][cols1]) -- for short matrices (split-K slices, partials). */
+int hs_colsum_pair(const float* x0, uint64_t rows0, uint64_t cols0, float* out0, const float* x1, uint64_t rows1,
+                   uint64_t cols1, float* out1, void* stream);
 uint64_t hs_colsum_workspace(uint64_t rows, uint64_t cols);
 int hs_colsum(const float* x, uint64_t rows, uint64_t cols, const float* row_weight, float* workspace, float* out,
               void* stream);

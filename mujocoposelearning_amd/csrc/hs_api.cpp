@@ -520,6 +520,25 @@ int hs_adam_clip(int nt, float* const* params, const float* const* grads, float*
              : -1;
 }
 
+uint64_t hs_colsum_partial_rows(uint64_t rows, uint64_t cols) { return hs::colsum_partial_rows(rows, cols); }
+
+int hs_relu_grad_colsum(const float* g, const float* y, uint64_t rows, uint64_t cols, float* gm, float* partial,
+                        void* stream) {
+  if (!rows || !cols) return 0;
+  if (!g || !y || !gm || !partial) return fail("hs_relu_grad_colsum: null buffer");
+  return hip_ok(hs::launch_relu_colsum(g, y, rows, cols, gm, partial, (hipStream_t)stream), "relu_colsum_kernel") ? 0
+                                                                                                                 : -1;
+}
+
+int hs_colsum_pair(const float* x0, uint64_t rows0, uint64_t cols0, float* out0, const float* x1, uint64_t rows1,
+                   uint64_t cols1, float* out1, void* stream) {
+  if ((cols0 && (!x0 || !out0)) || (cols1 && (!x1 || !out1))) return fail("hs_colsum_pair: null buffer");
+  return hip_ok(hs::launch_colsum_pair(x0, rows0, cols0, out0, x1, rows1, cols1, out1, (hipStream_t)stream),
+                "colsum_pair_kernel")
+             ? 0
+             : -1;
+}
+
 uint64_t hs_colsum_workspace(uint64_t rows, uint64_t cols) { return hs::colsum_workspace(rows, cols); }
 
 int hs_colsum(const float* x, uint64_t rows, uint64_t cols, const float* row_weight, float* workspace, float* out,

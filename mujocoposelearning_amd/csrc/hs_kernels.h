@@ -103,6 +103,12 @@ int adam_partials(long long total);
 hipError_t launch_adam_clip(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
                             float* const* step, const long long* numel, float* part, float max_norm, double lr,
                             double b1, double b2, double eps, hipStream_t stream);
+// ReLU-backward + bias-gradient first pass, and a paired single-pass column sum (ppo.hip)
+size_t colsum_partial_rows(size_t rows, size_t cols);
+hipError_t launch_relu_colsum(const float* g, const float* y, size_t rows, size_t cols, float* gm, float* partial,
+                              hipStream_t stream);
+hipError_t launch_colsum_pair(const float* x0, size_t rows0, size_t cols0, float* out0, const float* x1, size_t rows1,
+                              size_t cols1, float* out1, hipStream_t stream);
 // GAE reverse scan over [T][N] float32 rollout arrays (gae.hip)
 hipError_t launch_gae(const float* rew, const float* val, const float* start, const float* last_val,
                       const float* last_done, float* adv, float* ret, int T, int N, float gamma, float lam,

@@ -476,6 +476,77 @@ __global__ __launch_bounds__(CS_COLS* CS_PHASES) void colsum_kernel(const float*
   }
 }
 
+// ReLU backward fused with the bias gradient's first reduction pass: gm = (y > 0) ? g : 0 is
+// written for the GEMMs that follow, and its per-chunk column sums go to `partial`
+// ([gridDim.y][cols], the same tiling as colsum_kernel), finished by colsum_pair_kernel together
+// with the split-K weight-gradient slices -- one pass over g instead of threshold_backward + a
+// separate colsum read.
+__global__ __launch_bounds__(CS_COLS* CS_PHASES) void relu_colsum_kernel(const float* __restrict__ g,
+                                                                          const float* __restrict__ y,
+                                                                          size_t rows, size_t cols,
+                                                                          size_t rows_per_chunk,
+                                                                          float* __restrict__ gm,
+                                                                          float* __restrict__ partial) {
+  __shared__ float part[CS_PHASES][CS_COLS];
+  const int lane = threadIdx.x, ph = threadIdx.y;
+  const size_t c = (size_t)blockIdx.x * CS_COLS + lane;
+  const size_t r0 = (size_t)blockIdx.y * rows_per_chunk;
+  const size_t r1 = r0 + rows_per_chunk < rows ? r0 + rows_per_chunk : rows;
+  float a0 = 0.f, a1 = 0.f;
+  if (c < cols) {
+    size_t r = r0 + ph;
+    for (; r + CS_PHASES < r1; r += 2 * CS_PHASES) {
+      const size_t i0 = r * cols + c, i1 = (r + CS_PHASES) * cols + c;
+      const float v0 = y[i0] > 0.f ? g[i0] : 0.f, v1 = y[i1] > 0.f ? g[i1] : 0.f;
+      gm[i0] = v0;
+      gm[i1] = v1;
+      a0 += v0;
+      a1 += v1;
+    }
+    for (; r < r1; r += CS_PHASES) {
+      const size_t i = r * cols + c;
+      const float v = y[i] > 0.f ? g[i] : 0.f;
+      gm[i] = v;
+      a0 += v;
+    }
+  }
+  part[ph][lane] = a0 + a1;
+  __syncthreads();
+  if (ph == 0 && c < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < CS_PHASES; k++) t += part[k][lane];
+    partial[(size_t)blockIdx.y * cols + c] = t;
+  }
+}
+
+// Two single-pass column sums in one launch (blocks [0, tiles0) do x0, the rest x1): a layer's
+// split-K weight-gradient finish (S rows) and its bias-gradient finish (chunk rows).
+__global__ __launch_bounds__(CS_COLS* CS_PHASES) void colsum_pair_kernel(const float* __restrict__ x0, size_t rows0,
+                                                                          size_t cols0, float* __restrict__ out0,
+                                                                          const float* __restrict__ x1, size_t rows1,
+                                                                          size_t cols1, float* __restrict__ out1,
+                                                                          unsigned tiles0) {
+  __shared__ float part[CS_PHASES][CS_COLS];
+  const bool second = blockIdx.x >= tiles0;
+  const float* __restrict__ x = second ? x1 : x0;
+  const size_t rows = second ? rows1 : rows0, cols = second ? cols1 : cols0;
+  float* __restrict__ out = second ? out1 : out0;
+  const int lane = threadIdx.x, ph = threadIdx.y;
+  const size_t c = (size_t)(second ? blockIdx.x - tiles0 : blockIdx.x) * CS_COLS + lane;
+  float a = 0.f;
+  if (c < cols)
+    for (size_t r = ph; r < rows; r += CS_PHASES) a += x[r * cols + c];
+  part[ph][lane] = a;
+  __syncthreads();
+  if (ph == 0 && c < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < CS_PHASES; k++) t += part[k][lane];
+    out[c] = t;
+  }
+}
+
 }  // namespace
 
 // row chunks for colsum: enough workgroups to fill the chip (~1024) with >= 32 rows each;
@@ -617,6 +688,28 @@ hipError_t launch_adam_clip(int nt, float* const* p, const float* const* g, floa
   hipLaunchKernelGGL(adam_update_kernel, dim3(nblk), dim3(ADAM_TPB), 0, stream, a, (const float*)part, nblk,
                      max_norm, (float)lr, (float)b1, (float)b2, (float)(1.0 - b1), (float)(1.0 - b2), (float)eps);
   hipLaunchKernelGGL(adam_step_kernel, dim3(1), dim3(64), 0, stream, a);
+  return hipGetLastError();
+}
+
+size_t colsum_partial_rows(size_t rows, size_t cols) { return colsum_chunks(rows, cols); }
+
+hipError_t launch_relu_colsum(const float* g, const float* y, size_t rows, size_t cols, float* gm, float* partial,
+                              hipStream_t stream) {
+  if (cols == 0 || rows == 0) return hipSuccess;
+  const size_t chunks = colsum_chunks(rows, cols);
+  const size_t rpc = (rows + chunks - 1) / chunks;
+  const unsigned ctiles = (unsigned)((cols + CS_COLS - 1) / CS_COLS);
+  hipLaunchKernelGGL(relu_colsum_kernel, dim3(ctiles, (unsigned)chunks), dim3(CS_COLS, CS_PHASES), 0, stream, g, y,
+                     rows, cols, rpc, gm, partial);
+  return hipGetLastError();
+}
+
+hipError_t launch_colsum_pair(const float* x0, size_t rows0, size_t cols0, float* out0, const float* x1, size_t rows1,
+                              size_t cols1, float* out1, hipStream_t stream) {
+  const unsigned t0 = (unsigned)((cols0 + CS_COLS - 1) / CS_COLS), t1 = (unsigned)((cols1 + CS_COLS - 1) / CS_COLS);
+  if (t0 + t1 == 0) return hipSuccess;
+  hipLaunchKernelGGL(colsum_pair_kernel, dim3(t0 + t1), dim3(CS_COLS, CS_PHASES), 0, stream, x0, rows0, cols0, out0, x1,
+                     rows1, cols1, out1, t0);
   return hipGetLastError();
 }
 

@@ -162,6 +162,31 @@ def adam_clip_step(opt, params, max_norm, workspace=None):
     return workspace
 
 
+def relu_grad_colsum(g, y):
+    """(g masked by y > 0, per-chunk column sums of it) through hs_relu_grad_colsum."""
+    from . import _lib
+    assert g.is_contiguous() and y.is_contiguous() and g.shape == y.shape and g.dim() == 2
+    rows, cols = g.shape
+    L = _lib.lib()
+    gm = torch.empty_like(g)
+    part = torch.empty(int(L.hs_colsum_partial_rows(rows, cols)), cols, dtype=torch.float32, device=g.device)
+    _lib.check(L.hs_relu_grad_colsum(g.data_ptr(), y.data_ptr(), rows, cols, gm.data_ptr(), part.data_ptr(),
+                                     torch.cuda.current_stream(g.device).cuda_stream))
+    return gm, part
+
+
+def colsum_pair(x0, x1):
+    """(column sums of x0, column sums of x1) for two short contiguous matrices, one launch."""
+    from . import _lib
+    assert x0.is_contiguous() and x1.is_contiguous() and x0.dim() == 2 and x1.dim() == 2
+    o0 = torch.empty(x0.shape[1], dtype=torch.float32, device=x0.device)
+    o1 = torch.empty(x1.shape[1], dtype=torch.float32, device=x1.device)
+    _lib.check(_lib.lib().hs_colsum_pair(x0.data_ptr(), x0.shape[0], x0.shape[1], o0.data_ptr(), x1.data_ptr(),
+                                         x1.shape[0], x1.shape[1], o1.data_ptr(),
+                                         torch.cuda.current_stream(x0.device).cuda_stream))
+    return o0, o1
+
+
 def colsum(x, row_weight=None):
     """Column sums of a contiguous [rows, cols] float32 device matrix through hs_colsum
     (ppo.hip): deterministic, and 3-5x faster than torch's dim-0 reduction at the PPO update's
@@ -197,10 +222,11 @@ class _SplitKLinearReLUFn(torch.autograd.Function):
     def backward(ctx, g):
         x, w, y = ctx.saved_tensors
         s = ctx.s
-        g = torch.ops.aten.threshold_backward(g, y, 0)      # g where y > 0 (ReLU backward, one pass)
+        g, bias_part = relu_grad_colsum(g.contiguous(), y)  # ReLU mask + the bias sum's first pass
         gx = g @ w if ctx.needs_input_grad[0] else None
         part = torch.bmm(g.view(s, -1, g.shape[1]).transpose(1, 2), x.view(s, -1, x.shape[1]))
-        return gx, colsum(part.view(s, -1)).view_as(w), colsum(g), None
+        gw, gb = colsum_pair(part.view(s, -1), bias_part)    # both finishes in one launch
+        return gx, gw.view_as(w), gb, None
 
 
 def _splitk_rows(x):

@@ -397,3 +397,20 @@ def test_adam_clip_matches_torch_clip_and_adam():
             err = float((x - y).abs().max()) / float(y.abs().max())
             print(k, key, err, float(y.abs().max()))
             assert err < 1e-5, (k, key, err)
+
+
+def test_relu_grad_colsum_and_pair():
+    """hs_relu_grad_colsum (ReLU mask + first bias-sum pass) and hs_colsum_pair (two finishes in
+    one launch) == threshold_backward and fp64 column sums."""
+    from mujocoposelearning_amd.ppo_ops import colsum_pair, relu_grad_colsum
+    gen = torch.Generator(device="cuda").manual_seed(9)
+    for rows, cols in ((32768, 256), (32768, 21), (100, 7)):
+        g = torch.randn(rows, cols, device="cuda", generator=gen)
+        y = torch.relu(torch.randn(rows, cols, device="cuda", generator=gen))
+        gm, part = relu_grad_colsum(g, y)
+        ref = torch.ops.aten.threshold_backward(g, y, 0)
+        assert torch.equal(gm, ref)
+        p2 = torch.randn(16, 3 * cols, device="cuda", generator=gen)
+        s0, s1 = colsum_pair(p2, part)
+        assert torch.allclose(s0, p2.double().sum(0).float(), rtol=1e-5, atol=1e-5)
+        assert torch.allclose(s1, ref.double().sum(0).float(), rtol=1e-5, atol=1e-5 * rows ** 0.5)
