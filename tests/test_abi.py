@@ -70,3 +70,35 @@ def test_config_struct_layout():
     assert [n for n, _ in _lib.hs_buffers._fields_] == names
     assert C.sizeof(_lib.hs_buffers) == len(names) * 8
     assert _lib.HS_FULL_STATE == int(re.search(r"HS_FULL_STATE = (0x[0-9a-fA-F]+)", hdr).group(1), 16)
+
+
+def test_trainer_entry_points_validate_arguments():
+    """The PPO kernels' entry points reject bad sizes / null buffers with a message before touching
+    the device (runs on the CPU: nothing is launched), and report their workspace sizes."""
+    from mujocoposelearning_amd import _lib
+    L = _lib.lib()
+
+    def err(rc):
+        assert rc < 0
+        return L.hs_last_error().decode()
+
+    assert "A <= 32" in err(L.hs_ppo_act(None, 40, None, 1, None, None, 0, 0, None, 0, None, None, None, None, None,
+                                         8, 33, None))
+    assert "null" in err(L.hs_ppo_post(None, None, None, None, None, None, None, 0, 0.9, None, None, 0, None, None,
+                                       None, None, None, 4, None))
+    assert "null" in err(L.hs_ppo_loss(None, None, None, None, None, None, 8, 0.2, None, None, None, None))
+    assert "null" in err(L.hs_ppo_loss_grad(None, None, 8, 0.2, None, None, None, None, None, None))
+    assert "nt" in err(L.hs_adam_clip(17, None, None, None, None, None, None, None, 0.5, 3e-4, 0.9, 0.999, 1e-5,
+                                      None))
+    assert "null" in err(L.hs_colsum(None, 4, 4, None, None, None, None))
+    assert "null" in err(L.hs_relu_grad_colsum(None, None, 4, 4, None, None, None))
+    assert "null" in err(L.hs_colsum_pair(None, 4, 4, None, None, 4, 4, None, None))
+    assert "negative" in err(L.hs_gae(None, None, None, None, None, None, None, -1, 4, 0.99, 0.95, None))
+    # empty problems are no-ops, not errors
+    assert L.hs_ppo_loss(None, None, None, None, None, None, 0, 0.2, None, None, None, None) == 0
+    assert L.hs_colsum(None, 0, 0, None, None, None, None) == 0
+    # workspace sizes: loss 3B + 4 blocks + 2; colsum partial rows bounded; Adam one partial per 1024 elements
+    assert L.hs_ppo_loss_workspace(32768) == 3 * 32768 + 4 * 128 + 2
+    assert 1 <= L.hs_colsum_partial_rows(32768, 256) <= 32768 // 64
+    assert L.hs_colsum_workspace(16, 90112) == 0          # single pass for short matrices
+    assert L.hs_adam_workspace(317995) == (317995 + 1023) // 1024
