@@ -395,7 +395,6 @@ def test_adam_clip_matches_torch_clip_and_adam():
         for key in ("exp_avg", "exp_avg_sq"):
             x, y = sa[k][key], sb[k][key]
             err = float((x - y).abs().max()) / float(y.abs().max())
-            print(k, key, err, float(y.abs().max()))
             assert err < 1e-5, (k, key, err)
 
 
