@@ -102,3 +102,15 @@ def test_trainer_entry_points_validate_arguments():
     assert 1 <= L.hs_colsum_partial_rows(32768, 256) <= 32768 // 64
     assert L.hs_colsum_workspace(16, 90112) == 0          # single pass for short matrices
     assert L.hs_adam_workspace(317995) == (317995 + 1023) // 1024
+
+
+def test_header_is_plain_c():
+    """include/hsim.h is a C-ABI header: it compiles as C and as C++ with no torch/HIP types."""
+    import shutil
+    import subprocess
+    hdr = os.path.join(ROOT, "include", "hsim.h")
+    src = open(hdr).read()
+    assert "torch" not in src and "hip_runtime" not in src
+    for cc, lang in (("gcc", "c"), ("g++", "c++")):
+        if shutil.which(cc):
+            subprocess.run([cc, "-fsyntax-only", "-Wall", "-Werror", "-x", lang, hdr], check=True)
