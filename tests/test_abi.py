@@ -109,8 +109,8 @@ def test_header_is_plain_c():
     import shutil
     import subprocess
     hdr = os.path.join(ROOT, "include", "hsim.h")
-    src = open(hdr).read()
-    assert "torch" not in src and "hip_runtime" not in src
+    code = re.sub(r"/\*.*?\*/", "", open(hdr).read(), flags=re.S)       # declarations only
+    assert "torch" not in code and "hip" not in code.replace("hsim", "")
     for cc, lang in (("gcc", "c"), ("g++", "c++")):
         if shutil.which(cc):
             subprocess.run([cc, "-fsyntax-only", "-Wall", "-Werror", "-x", lang, hdr], check=True)
