@@ -40,4 +40,4 @@ def main(iters=400, reward="stand"):
 
 
 if __name__ == "__main__":
-    main(int(sys.argv[1]) if len(sys.argv) > 1 else 400)
+    main(int(sys.argv[1]) if len(sys.argv) > 1 else 400, sys.argv[2] if len(sys.argv) > 2 else "stand")
