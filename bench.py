@@ -2,23 +2,35 @@
 """Headline benchmark: humanoid env steps/sec (whole node), 'stand' task -- BASELINE.json metric.
 
 One "step" = one batched env step of every env on the rank: frame_skip=3 physics substeps
-(full mj_step pipeline incl. contacts + Newton solve), the 352-float observation, the device
-stand reward, termination/truncation and auto-reset -- one launch of the fused step kernel.
-Workload (BASELINE.json configs[1]): 4096 humanoid.xml envs per GPU, stand reward,
-frame_skip 3, duration 10; actions come from a pre-generated U(-1,1) action tape already
-resident in HBM (sim-only mode).  N GPUs run N independent env shards (weak scaling, no
-data-path collective).  rank 0 prints one JSON line.
+(full mj_step pipeline incl. contacts + Newton solve), the 352-value observation, the device
+stand reward, termination/truncation and auto-reset -- one launch of the fused step kernel (plus
+the wide-contact-tier launch, which re-runs the rare envs whose contacts overflow the resident
+tier and otherwise exits at once).  Workload (BASELINE.json configs[1]): 4096 humanoid.xml envs
+per GPU, stand reward, frame_skip 3, duration 10, computed in float64 like the reference's
+MuJoCo (mjtNum); actions come from a pre-generated U(-1,1) action tape already resident in HBM
+(sim-only mode).
 
-Also reported (extra keys): the rollout mode (MLP[256,256] policy forward + Gaussian sampling
-+ env step, all on device), the step-kernel roofline (HBM bytes vs 8 TB/s, measured live with
-HIP events on the launch stream) and the CPU baseline (the reference's n_envs=8
-SubprocVecEnv-style path, run on the oracle's fp64 C restatement of mj_step because MuJoCo is
-not installable: kind "port").
+Representative window: before the warm-up, env i's clock is set to i/N of the episode and the
+batch runs one full episode (667 env steps, untimed), so every env is at a different point of
+its episode (auto-resets included) and ANY timed window averages over standing, falling and
+lying humanoids -- the whole-episode mix of training, not the first 20 steps after a reset.
+
+N GPUs run N independent env shards (weak scaling, no data-path collective).  ``--gpus N``
+without a launcher spawns the N ranks itself (torch.distributed.run, 127.0.0.1); under an
+external launcher WORLD_SIZE must equal N.  Rank 0 prints one JSON line.
+
+Extra keys: fp32 sim-only, full-episode legs on tapes T0/T1/T2, rollout / train /
+GAE, configs[3]/[4], the step-kernel roofline (HBM bytes vs 8 TB/s, live HIP events on the
+launch stream) and the CPU baseline (the reference's n_envs=8 SubprocVecEnv path, on the
+oracle's fp64 C restatement of mj_step because MuJoCo is not installable: kind "port").
 """
 import argparse
 import json
+import math
 import multiprocessing as mp
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -26,17 +38,23 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-XML = os.path.join(ROOT, "tests", "golden", "humanoid.xml")
+XML = os.path.join(ROOT, "mujocoposelearning_amd", "assets", "humanoid.xml")
 
 N_ENVS_PER_GPU = 4096
 FRAME_SKIP = 3
 DURATION = 10.0
-# algorithmic HBM bytes per env step of the fused kernel: read qpos 28 + qvel 27
-# + qacc_warmstart 27 + time 1 + action 21 floats; write qpos/qvel/warmstart/time 83 + obs 352
-# + reward 1 floats; + 2 B done flags
-ALGO_BYTES_PER_ENV_STEP = (104 + 436) * 4 + 2
+TIMESTEP = 0.005
+EPISODE = math.ceil(DURATION / (FRAME_SKIP * TIMESTEP) - 1e-9)   # 667 env steps (custom_env.py:213)
 HBM_PEAK_GBS = 8000.0
 PROFILE_TRAFFIC = os.path.join(ROOT, "profiles", "traffic_step_kernel.json")
+
+
+def algo_bytes_per_env_step(es):
+    """Algorithmic HBM bytes of one env step of the fused kernel, state and obs of
+    element size ``es``: read qpos 28 + qvel 27 + qacc_warmstart 27 + time 1 (state) and the f32
+    action 21; write qpos/qvel/warmstart/time 83 + obs 352 + reward 1; + 2 B of done flags.
+    fp32: 2162 B; fp64: 4238 B."""
+    return 83 * es + 21 * 4 + 436 * es + 2
 
 
 # ----------------------------------------------------------------------------- CPU baseline
@@ -57,6 +75,17 @@ def _cpu_worker(conn, seed):
         elif cmd == "close":
             conn.close()
             return
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def cpu_baseline(n_envs=8, vec_steps=1500):
@@ -86,9 +115,51 @@ def cpu_baseline(n_envs=8, vec_steps=1500):
     for p in procs:
         p.join(timeout=10)
     return dict(value=n_envs * vec_steps / dt, unit="env_steps/s", cores=n_envs, kind="port",
+                cpu_model=_cpu_model(), nproc=os.cpu_count(),
                 sample=f"{n_envs} worker processes x {vec_steps} env steps (stand, frame_skip 3, U(-1,1) actions, "
-                       f"pipe IPC per step as SB3 SubprocVecEnv) on the fp64 oracle restatement of mj_step; "
-                       f"{dt:.1f} s wall; host nproc={os.cpu_count()}")
+                       f"pipe IPC per step as SB3 SubprocVecEnv) on the fp64 oracle restatement of mj_step "
+                       f"(numpy/ctypes host glue, one process per env, single-threaded each); {dt:.1f} s wall")
+
+
+# ----------------------------------------------------------------------------- launcher
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(nproc):
+    """Spawn ``nproc`` ranks of this script (one process per GPU) with torch.distributed.run on
+    127.0.0.1; this parent never touches the GPU.  Returns the launcher's exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def selftest_launch(args, world, rank):
+    """--selftest-launch: the multi-rank plumbing of the bench (rendezvous, barrier, max-over-ranks
+    timing, the JSON line) with a trivial CPU loop instead of the GPU work (CPU test of --gpus N)."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    ws = dist.get_world_size() if world > 1 else 1
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    x = np.zeros(1000)
+    for k in range(args.steps):
+        x += k
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": "selftest", "value": args.steps * ws / max(float(el.item()), 1e-9),
+                          "unit": "steps/s", "n_gpus": ws, "steps": args.steps, "warmup": args.warmup}))
+    if world > 1:
+        dist.destroy_process_group()
 
 
 # ----------------------------------------------------------------------------- GPU
@@ -98,30 +169,45 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--envs", type=int, default=N_ENVS_PER_GPU, help="envs per GPU")
-    ap.add_argument("--precision", default="fp32", choices=["fp32", "fp64"])
+    ap.add_argument("--precision", default="fp64", choices=["fp32", "fp64"],
+                    help="headline arithmetic (fp64 = the reference's mjtNum; fp32 is an extra leg)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-rollout", action="store_true")
     ap.add_argument("--no-gae", action="store_true")
     ap.add_argument("--train-iters", type=int, default=2, help="PPO iterations of the train mode (0: skip)")
-    ap.add_argument("--groups", default="1", help="stream groups for the headline run (1 = one launch per step)")
     ap.add_argument("--no-configs", action="store_true", help="skip the configs[3]/[4] legs")
-    ap.add_argument("--no-fp64", action="store_true", help="skip the fp64 (parity-mode) sim-only leg")
-    ap.add_argument("--free-groups", type=int, default=4, help="extra sim-only leg: this many free-running stream "
+    ap.add_argument("--no-fp32", action="store_true", help="skip the fp32 sim-only leg")
+    ap.add_argument("--no-episodes", action="store_true", help="skip the full-episode T0/T1/T2 legs")
+    ap.add_argument("--no-precondition", action="store_true",
+                    help="time from a synchronized reset (standing humanoids only) instead of the staggered mix")
+    ap.add_argument("--free-groups", type=int, default=0, help="extra sim-only leg: this many free-running stream "
                                                                 "groups (0: skip)")
+    ap.add_argument("--protocol", action="store_true",
+                    help="SURVEY 8d protocol instead of the default run: 1000 warm-up + 10000 timed env steps "
+                         "per tape T0/T1/T2 and base seed {0,1,2} (~2 min per precision)")
     ap.add_argument("--dist-backend", default=os.environ.get("HSIM_BENCH_BACKEND", "nccl"),
                     help="nccl (= RCCL over xGMI; the real multi-GPU run) or gloo (multi-rank rehearsal on one GPU)")
     ap.add_argument("--cpu-steps", type=int, default=60000, help="vec steps of the CPU baseline (~13 s)")
+    ap.add_argument("--selftest-launch", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(self_launch(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (one rank per GPU)")
+    if args.selftest_launch:
+        return selftest_launch(args, world, rank)
     cpu_res = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu_res = cpu_baseline(vec_steps=args.cpu_steps)   # before any GPU/torch init (fork-safe)
 
     import torch
     import torch.distributed as dist
+    if cpu_res is not None:
+        cpu_res["torch_threads"] = torch.get_num_threads()
     gloo = args.dist_backend == "gloo"
     # gloo rehearsal: ranks may share a GPU; nccl: one process per GPU (LOCAL_RANK = device)
     dev_index = local_rank % max(1, torch.cuda.device_count()) if gloo else local_rank
@@ -133,21 +219,17 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
     red_dev = torch.device("cpu") if gloo else dev      # device of the timing reductions
+    ranks = dist.get_world_size() if world > 1 else 1
 
     from mujocoposelearning_amd.model import HsModel
     from mujocoposelearning_amd.vec_env import HumanoidVecEnv
     cfg = {"model_path": XML, "duration": DURATION, "reward_config": {"type": "stand"}, "frame_skip": FRAME_SKIP}
     model = HsModel(XML)
     n = args.envs
-    groups = args.groups if args.groups == "auto" else int(args.groups)
-    env = HumanoidVecEnv(cfg, n_envs=n, device=dev_index, precision=args.precision, seed=1000 + rank,
-                         model=model, groups=groups)
-    n_groups = len(env.batch._groups)
-    env.reset_tensors()
-    g = torch.Generator(device=dev).manual_seed(rank)
-    tape_len = min(args.steps + args.warmup, 256)
-    tape = (torch.rand(tape_len, n, model.nu, device=dev, generator=g) * 2 - 1).contiguous()
+    stream = torch.cuda.current_stream(dev)
 
     def barrier():
         torch.cuda.synchronize(dev)
@@ -155,48 +237,140 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    for k in range(args.warmup):
-        env.step_tensors(tape[k % tape_len])
-    barrier()
-    stream = torch.cuda.current_stream(dev)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for k in range(args.steps):
-        env.step_tensors(tape[(args.warmup + k) % tape_len])
-    ev1.record(stream)
-    barrier()
-    elapsed = time.perf_counter() - t0
-    step_ms = ev0.elapsed_time(ev1) / args.steps
-    t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
-    total_env_steps = n * args.steps * world
-    value = total_env_steps / elapsed
-    warn = env.batch.warning.sum(0).tolist()
-    aux = env.batch.aux
-    stats = dict(mean_contacts=float(aux[:, 35].float().mean()), mean_rows=float(aux[:, 36].float().mean()),
-                 mean_newton_iters=float(aux[:, 37].float().mean()), warnings=warn)
+    def max_over_ranks(x):
+        t = torch.tensor([x], dtype=torch.float64, device=red_dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
 
-    # rollout mode: policy MLP[256,256] forward + sampling + env step (on device)
+    def make_tape(kind, length, n_x, seed):
+        g = torch.Generator(device=dev).manual_seed(seed)
+        if kind == "T0":
+            return torch.zeros(length, n_x, model.nu, device=dev)
+        if kind == "T2":
+            return (torch.randn(length, n_x, model.nu, device=dev, generator=g) * 0.1).clamp_(-1, 1)
+        return (torch.rand(length, n_x, model.nu, device=dev, generator=g) * 2 - 1).contiguous()
+
+    def make_env(precision, seed, cfg_x=cfg, n_x=n, stats=False):
+        e = HumanoidVecEnv(cfg_x, n_envs=n_x, device=dev_index, precision=precision, seed=seed + 7919 * rank,
+                           model=model)
+        # sim-only timing writes what a trainer needs; the aux row / ctrl copy only when stats are read
+        e.batch.configure(aux=stats, ctrl=False)
+        e.reset_tensors()
+        return e
+
+    def precondition(e, tape):
+        """Staggered episode phases: env i's clock starts at i/N of the episode, then one full
+        episode runs, so env i ends up ~i/N of the way into a genuine episode (after its first
+        auto-reset); untimed."""
+        if args.no_precondition:
+            return
+        nx = e.num_envs
+        t0 = np.floor(np.arange(nx) * EPISODE / nx) * FRAME_SKIP * TIMESTEP + TIMESTEP
+        e.batch.set_state(time=t0)
+        for k in range(EPISODE):
+            e.step_tensors(tape[k % tape.shape[0]])
+
+    def timed(e, tape, steps, warmup, offset=0):
+        """warm-up, then ``steps`` env steps bracketed by barrier + synchronize; returns
+        (wall seconds max over ranks, HIP-event ms per step on the launch stream)."""
+        for k in range(warmup):
+            e.step_tensors(tape[(offset + k) % tape.shape[0]])
+        barrier()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for k in range(steps):
+            e.step_tensors(tape[(offset + warmup + k) % tape.shape[0]])
+        ev1.record(stream)
+        barrier()
+        return max_over_ranks(time.perf_counter() - t0), ev0.elapsed_time(ev1) / steps
+
+    def stats_of(e, tape, k0, steps=3):
+        """aux-row statistics of a few further (untimed) steps of the same batch."""
+        e.batch.configure(aux=True)
+        for k in range(steps):
+            e.step_tensors(tape[(k0 + k) % tape.shape[0]])
+        a = e.batch.aux.double()
+        e.batch.configure(aux=False)
+        return dict(mean_contacts=float(a[:, 35].mean()), max_contacts=int(a[:, 35].max()),
+                    mean_rows=float(a[:, 36].mean()), max_rows=int(a[:, 36].max()),
+                    mean_newton_iters=float(a[:, 37].mean()),
+                    fallen_frac=float((e.batch.qpos[:, 2] < 0.8).double().mean()),
+                    warnings=e.batch.warning.sum(0).tolist(), wide_tier_reruns=e.batch.wide_reruns())
+
+    if args.protocol:
+        return run_protocol(args, rank, world, ranks, make_env, make_tape, precondition, timed, stats_of)
+
+    # ---- headline: configs[1], fp64, staggered whole-episode mix
+    tape = make_tape("T1", 1024, n, 1 + rank)
+    env = make_env(args.precision, 1000)
+    precondition(env, tape)
+    elapsed, step_ms = timed(env, tape, args.steps, args.warmup, offset=EPISODE)
+    value = n * args.steps * ranks / elapsed
+    stats = stats_of(env, tape, EPISODE + args.warmup + args.steps)
+    kernel_ms = step_ms
+    env.close()
+
+    # ---- fp32 sim-only leg (the throughput engine; tolerance-based parity, not the headline)
+    fp32_leg = None
+    if args.precision == "fp64" and not args.no_fp32:
+        e = make_env("fp32", 5000)
+        precondition(e, tape)
+        el, ms = timed(e, tape, args.steps, args.warmup, offset=EPISODE)
+        fp32_leg = dict(value=n * args.steps * ranks / el, unit="env_steps/s", dtype="f32", steps=args.steps,
+                        kernel_ms_per_launch=ms, stats=stats_of(e, tape, EPISODE + args.warmup + args.steps),
+                        note="same workload and staggered episode mix, fp32 engine (parity within fp32 tolerances, "
+                             "not the reference's fp64: see DESIGN.md 4)")
+        e.close()
+
+    # ---- full episodes from a synchronized reset on tapes T0 / T1 / T2 (SURVEY 8d), per phase
+    episodes = None
+    if not args.no_episodes:
+        episodes = {}
+        phases = [(0, 50), (50, 100), (100, 200), (200, 300), (300, 400), (400, 500), (500, 600), (600, EPISODE)]
+        for kind in ("T0", "T1", "T2"):
+            tp = make_tape(kind, EPISODE, n, 11 + rank)
+            e = make_env(args.precision, 6000, stats=True)
+            per, tot_t = [], 0.0
+            for a, b in phases:
+                barrier()
+                t0 = time.perf_counter()
+                for k in range(a, b):
+                    e.step_tensors(tp[k])
+                barrier()
+                dt = max_over_ranks(time.perf_counter() - t0)
+                tot_t += dt
+                ax = e.batch.aux.double()
+                per.append(dict(steps=[a, b], env_steps_per_s=n * (b - a) * ranks / dt,
+                                mean_contacts=float(ax[:, 35].mean()), mean_rows=float(ax[:, 36].mean()),
+                                mean_newton_iters=float(ax[:, 37].mean()),
+                                fallen_frac=float((e.batch.qpos[:, 2] < 0.8).double().mean())))
+            episodes[kind] = dict(value=n * EPISODE * ranks / tot_t, unit="env_steps/s", steps=EPISODE,
+                                  phases=per, warnings=e.batch.warning.sum(0).tolist(),
+                                  wide_tier_reruns=e.batch.wide_reruns())
+            e.close()
+
+    # ---- rollout mode: policy MLP[256,256] forward + sampling + env step (on device)
     rollout = None
     if not args.no_rollout:
         from mujocoposelearning_amd.ppo import ActorCritic, ppo_act
-        pol = ActorCritic(env.batch.obs_dim, model.nu, (256, 256), activation=torch.nn.ReLU).to(dev)
+        e = make_env(args.precision, 7000)
+        precondition(e, tape)
+        pol = ActorCritic(e.batch.obs_dim, model.nu, (256, 256), activation=torch.nn.ReLU).to(dev)
         pol.pack_heads()
         ls = pol.log_std.detach()
         start = torch.zeros(n, device=dev)
         act, clip = torch.empty(n, model.nu, device=dev), torch.empty(n, model.nu, device=dev)
         logp, val, st_out = (torch.empty(n, device=dev) for _ in range(3))
-        obs = env.batch.obs
+        obs = e.batch.obs
 
         def policy_step(obs, k):
             # the PPO rollout's policy half (ppo.PPO._collect_rollouts_device): packed pi/vf GEMM
-            # chain + hs_ppo_act (Gaussian sample, log-prob, clip, buffer writes), then the env
-            mean, value = pol.heads(obs)
-            ppo_act(mean, value, ls, start, 1 + rank, k, False, act, clip, logp, val, st_out)
-            return env.step_tensors(clip)[0]
+            # chain (fp32, as SB3's policy) + hs_ppo_act (Gaussian sample, log-prob, clip), then the env
+            mean, value_ = pol.heads(obs.float())
+            ppo_act(mean, value_, ls, start, 1 + rank, k, False, act, clip, logp, val, st_out)
+            return e.step_tensors(clip)[0]
 
         with torch.no_grad():
             for k in range(5):
@@ -207,137 +381,79 @@ def main():
             for k in range(rs):
                 obs = policy_step(obs, 5 + k)
             barrier()
-            rel = time.perf_counter() - tr0
-        t = torch.tensor([rel], dtype=torch.float64, device=red_dev)
-        if world > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        rollout = dict(value=n * rs * world / float(t.item()), unit="env_steps/s",
-                       note="policy MLP[256,256] (pi+vf, packed GEMM chain) forward + hs_ppo_act (diag-Gaussian sample, log-prob, clip) + env step")
+            rel = max_over_ranks(time.perf_counter() - tr0)
+        rollout = dict(value=n * rs * ranks / rel, unit="env_steps/s",
+                       note="policy MLP[256,256] (pi+vf, packed GEMM chain, fp32) forward + hs_ppo_act "
+                            "(diag-Gaussian sample, log-prob, clip) + env step")
+        e.close()
 
-    # extra sim-only leg: the same n envs as free-running stream groups (no per-step join; the
-    # action tape is open-loop, so every env still takes exactly the same steps)
+    # ---- extra sim-only leg: free-running stream groups (opt-in)
     grouped = None
     if args.free_groups > 1:
-        envg = HumanoidVecEnv(cfg, n_envs=n, device=dev_index, precision=args.precision, seed=3000 + rank,
-                              model=model, groups=args.free_groups)
-        envg.reset_tensors()
+        eg = HumanoidVecEnv(cfg, n_envs=n, device=dev_index, precision=args.precision, seed=3000 + rank,
+                            model=model, groups=args.free_groups)
+        eg.batch.configure(aux=False, ctrl=False)
+        eg.reset_tensors()
         for k in range(args.warmup):
-            envg.batch.step(tape[k % tape_len], join=False)
-        envg.batch.join()
+            eg.batch.step(tape[k], join=False)
+        eg.batch.join()
         barrier()
         tg = time.perf_counter()
         for k in range(args.steps):
-            envg.batch.step(tape[(args.warmup + k) % tape_len], join=False)
-        envg.batch.join()
+            eg.batch.step(tape[(args.warmup + k) % tape.shape[0]], join=False)
+        eg.batch.join()
         barrier()
-        t = torch.tensor([time.perf_counter() - tg], dtype=torch.float64, device=red_dev)
-        if world > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        grouped = dict(value=n * args.steps * world / float(t.item()), unit="env_steps/s", groups=args.free_groups,
-                       note="same workload as value, envs split into free-running stream groups (HsBatch "
-                            "join=False): one group's Newton tail overlaps the others' launches")
-        envg.close()
+        grouped = dict(value=n * args.steps * ranks / max_over_ranks(time.perf_counter() - tg), unit="env_steps/s",
+                       groups=args.free_groups,
+                       note="envs split into free-running stream groups (HsBatch join=False), from a reset")
+        eg.close()
 
-    # parity-mode leg: the fp64 engine (the one the oracle parity tests pin at 1e-9 per stage and
-    # that tracks the oracle over 1000 substeps) on the same workload and protocol as value
-    fp64_leg = None
-    if args.precision == "fp32" and not args.no_fp64:
-        e64 = HumanoidVecEnv(cfg, n_envs=n, device=dev_index, precision="fp64", seed=5000 + rank, model=model)
-        e64.reset_tensors()
-        for k in range(min(args.warmup, 5)):
-            e64.step_tensors(tape[k % tape_len])
-        barrier()
-        k64 = max(10, args.steps // 4)
-        t64 = time.perf_counter()
-        for k in range(k64):
-            e64.step_tensors(tape[k % tape_len])
-        barrier()
-        t = torch.tensor([time.perf_counter() - t64], dtype=torch.float64, device=red_dev)
-        if world > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        fp64_leg = dict(value=n * k64 * world / float(t.item()), unit="env_steps/s", dtype="f64", steps=k64,
-                        note="same workload, fp64 engine (parity mode: <=1e-9 per stage vs the fp64 oracle, "
-                             "tracks it over 1000 substeps; profiles/parity_report.md)")
-        e64.close()
-
-    # BASELINE.json configs[3] (kneeling reward, 4096 envs) and configs[4] (full-state obs, 8192
-    # envs over 8 GPUs = 1024 per GPU): same sim-only protocol, one launch per step
+    # ---- BASELINE.json configs[3] (kneeling reward, 4096 envs) and configs[4] (full-state obs,
+    # 8192 envs over 8 GPUs = 1024 per GPU): same staggered sim-only protocol
     config_legs = None
     if not args.no_configs:
         def leg(cfg_x, n_x, label):
-            e = HumanoidVecEnv(cfg_x, n_envs=n_x, device=dev_index, precision=args.precision, seed=4000 + rank,
-                               model=model)
-            e.reset_tensors()
-            tp = tape[:, :n_x] if n_x <= n else (torch.rand(tape_len, n_x, model.nu, device=dev) * 2 - 1)
-            for k in range(args.warmup):
-                e.step_tensors(tp[k % tape_len])
-            barrier()
-            tl = time.perf_counter()
+            e = make_env(args.precision, 4000, cfg_x=cfg_x, n_x=n_x)
+            tp = tape[:, :n_x] if n_x <= n else make_tape("T1", 1024, n_x, 5)
+            precondition(e, tp)
             ks = min(args.steps, 50)
-            for k in range(ks):
-                e.step_tensors(tp[(args.warmup + k) % tape_len])
-            barrier()
-            tt = torch.tensor([time.perf_counter() - tl], dtype=torch.float64, device=red_dev)
-            if world > 1:
-                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            r = dict(value=n_x * ks * world / float(tt.item()), unit="env_steps/s", n_envs_per_gpu=n_x,
-                     obs_dim=e.obs_dim, workload=label)
+            el, _ = timed(e, tp, ks, args.warmup, offset=EPISODE)
+            r = dict(value=n_x * ks * ranks / el, unit="env_steps/s", n_envs_per_gpu=n_x, obs_dim=e.obs_dim,
+                     workload=label)
             e.close()
             return r
         config_legs = {
             "configs[3]": leg({**cfg, "reward_config": {"type": "kneeling"}}, n,
                               "kneeling (robust_kneeling_reward) device reward, humanoid.xml x 4096 envs per GPU"),
             "configs[4]": leg({**cfg, "full_state_obs": True}, 1024,
-                              "full-state obs (+cfrc_ext[1:], 448 floats; subtree_linvel), 1024 envs per GPU "
+                              "full-state obs (+cfrc_ext[1:], 448 values; subtree_linvel), 1024 envs per GPU "
                               "(8192 over 8 GPUs)"),
         }
 
-    # roofline pass: the step kernel with all n envs in ONE launch per step (groups=1), HIP events on
-    # the stream it is launched on -- the per-launch figure rocprofv3 reports for profiles/collect.sh
-    if n_groups == 1:
-        kernel_ms = step_ms
-    else:
-        env1 = HumanoidVecEnv(cfg, n_envs=n, device=dev_index, precision=args.precision, seed=2000 + rank,
-                              model=model, groups=1)
-        env1.reset_tensors()
-        for k in range(args.warmup):
-            env1.step_tensors(tape[k % tape_len])
-        torch.cuda.synchronize(dev)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        rsteps = min(args.steps, 50)
-        for k in range(rsteps):
-            env1.step_tensors(tape[(args.warmup + k) % tape_len])
-        e1.record(stream)
-        torch.cuda.synchronize(dev)
-        kernel_ms = e0.elapsed_time(e1) / rsteps
-        env1.close()
-
-    # train mode (SURVEY 8d iii): end-to-end on-device PPO iterations (rollout with the
+    # ---- train mode (SURVEY 8d iii): end-to-end on-device PPO iterations (rollout with the
     # MLP[256,256] policy + GAE + clipped-surrogate updates with the per-step gradient all-reduce)
     train_res = None
     if args.train_iters > 0:
         from mujocoposelearning_amd.ppo import PPO
+        e = make_env(args.precision, 8000)
         tk = dict(n_steps=32, batch_size=32768, n_epochs=4, learning_rate=3e-4,
                   policy_kwargs={"net_arch": {"pi": [256, 256], "vf": [256, 256]}, "activation_fn": "ReLU"})
-        ppo = PPO(env, seed=0, world_size=world, rank=rank, **tk)
+        ppo = PPO(e, seed=0, world_size=world, rank=rank, **tk)
         ppo.learn(ppo.num_timesteps + n * tk["n_steps"] * world)          # warm-up iteration
         barrier()
         t_tr = time.perf_counter()
         ppo.learn(ppo.num_timesteps + args.train_iters * n * tk["n_steps"] * world)
         barrier()
-        t = torch.tensor([time.perf_counter() - t_tr], dtype=torch.float64, device=red_dev)
-        if world > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ts = float(t.item())
-        train_res = dict(value=args.train_iters * n * tk["n_steps"] * world / ts, unit="env_steps/s",
+        ts = max_over_ranks(time.perf_counter() - t_tr)
+        train_res = dict(value=args.train_iters * n * tk["n_steps"] * ranks / ts, unit="env_steps/s",
                          iterations=args.train_iters, ms_per_iteration=ts / args.train_iters * 1e3,
+                         env_precision=args.precision,
                          config={k: v for k, v in tk.items() if k != "policy_kwargs"} | {"net_arch": "[256,256] ReLU"},
                          note="rollout (policy forward + env step) + GAE + 4 epochs of minibatch updates, "
                               "one gradient all-reduce per optimizer step")
+        e.close()
 
-    # GAE leg: the rollout-end reverse scan (hs_gae) over an n_steps=2048 x n-env buffer -- an
-    # HBM-bound kernel (12 B read + 8 B written per element), timed with HIP events on its stream
+    # ---- GAE leg: the rollout-end reverse scan (hs_gae) over an n_steps=2048 x n-env buffer
     gae_res = None
     if not args.no_gae:
         from mujocoposelearning_amd.ppo import gae_device
@@ -363,16 +479,17 @@ def main():
                                 "frac": gbs / HBM_PEAK_GBS, "algo_bytes_per_element": 20}}
 
     if rank == 0:
-        achieved = ALGO_BYTES_PER_ENV_STEP * n / (kernel_ms * 1e-3) / 1e9
-        traffic = None
-        issue = None
+        es = 8 if args.precision == "fp64" else 4
+        abytes = algo_bytes_per_env_step(es)
+        achieved = abytes * n / (kernel_ms * 1e-3) / 1e9
+        traffic = issue = None
         if os.path.exists(PROFILE_TRAFFIC):
             try:
-                tr = json.load(open(PROFILE_TRAFFIC))
-                if tr.get("n_envs") == n and tr.get("precision") == args.precision:
+                tr = json.load(open(PROFILE_TRAFFIC)).get(args.precision, {})
+                if tr.get("n_envs") == n:
                     traffic = tr.get("hbm_bytes_per_launch")
-                    # VALU-issue view of the same kernel (what actually bounds it): VALU wave-instructions
-                    # per launch from the profile's PMC pass over the live launch time; a SIMD issues one
+                    # VALU-issue view of the same kernel (what bounds it): VALU wave-instructions per
+                    # launch from the profile's PMC pass over the live launch time; a SIMD issues one
                     # wave64 VALU op per 2 cycles at 2.4 GHz (MI355X_MICROARCH.md, wave scheduling)
                     valu = tr.get("sq", {}).get("SQ_INSTS_VALU")
                     if valu:
@@ -382,43 +499,71 @@ def main():
                                  "source": f"SQ_INSTS_VALU per launch from profiles ({tr.get('tag')})"}
             except Exception:
                 traffic = None
+        kname = "step_kernel<double,27>" if args.precision == "fp64" else "step_kernel<float,27>"
         out = {
             "metric": "env steps/sec (whole node), humanoid 'stand' task, 1/2/4/8 MI355X",
             "value": value,
             "unit": "env_steps/s",
-            "n_gpus": world,
+            "n_gpus": ranks,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32" if args.precision == "fp32" else "f64",
-            "data": "synthetic (reset distribution of custom_env.py:97-121; U(-1,1) action tape in HBM)",
+            "dtype": "f64" if args.precision == "fp64" else "f32",
+            "data": "synthetic (reset distribution of custom_env.py:97-121; U(-1,1) action tape in HBM; "
+                    "staggered episode phases, see config.window)",
             "config": {"workload": "configs[1]: humanoid.xml x 4096 envs per GPU, 'stand' reward, frame_skip 3, "
-                                   "duration 10 (sim-only env steps)",
-                       "n_envs_per_gpu": n, "n_envs_total": n * world, "frame_skip": FRAME_SKIP,
-                       "reward": "stand", "parallelism": f"dp{world} (env shards, no collective)",
-                       "stream_groups": n_groups},
+                                   "duration 10 (sim-only env steps, fp64 physics like the reference's mjtNum)",
+                       "n_envs_per_gpu": n, "n_envs_total": n * ranks, "frame_skip": FRAME_SKIP,
+                       "reward": "stand", "parallelism": f"dp{ranks} (env shards, no collective)",
+                       "window": ("synchronized reset (standing phase only)" if args.no_precondition else
+                                  f"staggered: env i starts at episode step ~{EPISODE}*i/N, then one untimed "
+                                  f"{EPISODE}-step episode; every timed window averages the whole-episode mix")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "step_kernel<float,27>" if args.precision == "fp32" else "step_kernel<double,27>",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
                          "kernel_ms_per_launch": kernel_ms, "envs_per_launch": n,
-                         "algo_bytes_per_env_step": ALGO_BYTES_PER_ENV_STEP, "valu_issue": issue,
-                         "note": "latency-bound kernel (see valu_issue and DESIGN.md 3.1); HBM fraction reported per BASELINE.json; measured "
-                                 "with all envs in one launch per step (the headline value uses "
-                                 f"{n_groups} stream groups; step time {step_ms:.3f} ms)"},
+                         "algo_bytes_per_env_step": abytes, "valu_issue": issue,
+                         "note": "latency-bound kernel (see valu_issue and DESIGN.md 3.1); HBM fraction reported per "
+                                 "BASELINE.json; HIP events over the timed steps on the launch stream (the step "
+                                 "kernel + the wide-tier launch, which exits at once when no env overflowed)"},
             "cpu_baseline": cpu_res,
+            "sim_stats": stats,
+            "sim_only_fp32": fp32_leg,
+            "sim_only_episode": episodes,
             "rollout": rollout,
+            "train": train_res,
             "gae": gae_res,
             "sim_only_stream_groups": grouped,
-            "sim_only_fp64": fp64_leg,
             "other_configs": config_legs,
-            "train": train_res,
-            "sim_stats": stats,
         }
         print(json.dumps(out))
     if world > 1:
+        dist.destroy_process_group()
+
+
+def run_protocol(args, rank, world, ranks, make_env, make_tape, precondition, timed, stats_of):
+    """SURVEY 8d protocol: per tape T0/T1/T2 and base seed {0,1,2}: reset (synchronized, as in
+    training: all envs reset together every 667 steps), 1000 warm-up env steps, then 10000 timed."""
+    res = {}
+    for kind in ("T0", "T1", "T2"):
+        for seed in (0, 1, 2):
+            tp = make_tape(kind, 1024, args.envs, 100 * seed + rank)
+            e = make_env(args.precision, seed)
+            el, ms = timed(e, tp, 10000, 1000)
+            res[f"{kind}/seed{seed}"] = dict(value=args.envs * 10000 * ranks / el, kernel_ms_per_launch=ms,
+                                             stats=stats_of(e, tp, 11000))
+            e.close()
+            if rank == 0:
+                print(json.dumps({kind + "/seed" + str(seed): res[f"{kind}/seed{seed}"]}), flush=True)
+    if rank == 0:
+        vals = [r["value"] for r in res.values()]
+        print(json.dumps({"protocol": "SURVEY 8d: 1000 warm-up + 10000 timed env steps", "precision": args.precision,
+                          "n_envs_per_gpu": args.envs, "n_gpus": ranks, "mean_value": float(np.mean(vals)),
+                          "min_value": float(np.min(vals)), "runs": res}))
+    if world > 1:
+        import torch.distributed as dist
         dist.destroy_process_group()
 
 

@@ -63,6 +63,11 @@ enum { HS_FULL_STATE = 0x100 };
 enum { HS_REWARD_NONE = -1, HS_REWARD_STAND = 0, HS_REWARD_KNEELING = 1, HS_REWARD_WALK = 2 };
 enum { HS_WARN_BADQPOS = 0, HS_WARN_BADQVEL = 1, HS_WARN_BADQACC = 2, HS_WARN_OVERFLOW = 3, HS_NWARN = 4 };
 #define HS_AUXDIM 40   /* per env aux row: qacc[32], com[3], ncon, nefc, newton iterations, pad */
+/* Optional per-env outputs (hs_env_config.outputs).  HS_OUT_AUX: the aux row (qacc, subtree com,
+ * contact / row counts, solver iterations) that data views and statistics read.  HS_OUT_CTRL: the
+ * data.ctrl copy (the action; data views and host reward callables read it,
+ * reward_functions.py:194).  A trainer on the device reward needs neither. */
+enum { HS_OUT_AUX = 1, HS_OUT_CTRL = 2 };
 
 /* Env semantics (custom_env.py defaults in brackets; train_sb3.py overrides in parentheses). */
 typedef struct {
@@ -71,7 +76,7 @@ typedef struct {
   int reward_id;           /* HS_REWARD_*; reward_config['type'] custom_env.py:263-271 */
   int autoreset;           /* 1 = SB3 VecEnv auto-reset (terminal obs kept in terminal_obs) */
   int max_newton;          /* Newton iteration cap [100 = opt.iterations] */
-  int reserved;
+  int outputs;             /* HS_OUT_* bits: optional per-env outputs [all] */
   double duration;         /* [15] (10.0) custom_env.py:23, train_sb3.py:187 */
   double init_height;      /* 1.282   custom_env.py:59 */
   double noise_scale;      /* 0.01    custom_env.py:109-110 */
@@ -100,6 +105,8 @@ typedef struct {
   void* aux;               /* [N][HS_AUXDIM] */
   void* cfrc_ext;          /* [N][nbody][6]  (torque, force) at the root subtree com; HS_FULL_STATE only */
   void* subtree_linvel;    /* [N][nbody][3]  HS_FULL_STATE only */
+  int32_t* terminal_step_count;  /* [N] or NULL: info["step_count"] of envs that auto-reset this step */
+  void* terminal_total_reward;   /* [N] or NULL: their info["total_reward"] (custom_env.py:216-224) */
 } hs_buffers;
 
 typedef struct {
@@ -128,6 +135,13 @@ int hs_get_config(const hs_batch* b, hs_env_config* cfg);
 int hs_reset(hs_batch* b, const uint8_t* mask, const void* qpos_noise, const void* qvel_noise, void* stream);
 /* actions: [N][nu] float32 device. Runs frame_skip substeps, writes obs/reward/terminated/truncated. */
 int hs_step(hs_batch* b, const float* actions, void* stream);
+/* Auto-reset noise source of hs_step: [N][nq] / [N][nv] device arrays of the batch precision with
+ * the raw U(-noise_scale, noise_scale) draws of the NEXT reset of each env (the kernel applies the
+ * x0.1 height factor and zeroes the quaternion part, custom_env.py:109-114); NULL, NULL = the
+ * on-device counter RNG (default).  The caller refreshes an env's row after it auto-resets -- the
+ * SubprocVecEnv-exact mode where worker i continues its own np.random stream seeded with
+ * seed + i (custom_env.py:99-110, SB3 VecEnv.seed).  The arrays stay owned by the caller. */
+int hs_set_autoreset_noise(hs_batch* b, const void* qpos_noise, const void* qvel_noise);
 /* ctrl: [N][nu] float32 device (NULL = keep current ctrl).  nsub raw mj_step's, obs refreshed. */
 int hs_physics_step(hs_batch* b, const float* ctrl, int nsub, void* stream);
 
@@ -146,6 +160,10 @@ int hs_kinematics(hs_batch* b, int env, const double* qpos, double* xpos, double
 int hs_set_debug(hs_batch* b, int enable);
 int hs_get_debug(hs_batch* b, double* out, int n);
 int hs_synchronize(hs_batch* b);
+/* Diagnostics (synchronous): *wide_reruns = cumulative count of env steps whose contacts or
+ * constraint rows overflowed the resident kernel tier (32 contacts / 128 rows) and were re-run by
+ * the wide tier (64 / 256); contacts are only dropped (HS_WARN_OVERFLOW) past the wide tier. */
+int hs_batch_counters(const hs_batch* b, uint64_t* wide_reruns);
 
 /* GAE(gamma, lambda) reverse scan over a device rollout buffer, SB3 semantics: [T][N] float32
  * rewards, values, episode_starts; [N] last_values, last_dones; writes [T][N] advantages and
@@ -203,7 +221,7 @@ int hs_ppo_loss(const float* log_prob, const float* values, const int64_t* idx, 
                 float* value_loss, float* workspace, void* stream);
 int hs_ppo_loss_grad(const float* log_prob, const float* values, int B, float clip, const float* workspace,
                      const float* g_pg, const float* g_vf, float* g_log_prob, float* g_values, void* stream);
-/* Gradient-norm clipping + one Adam step over nt <= 16 float32 device tensors: params[i],
+/* Gradient-norm clipping + one Adam step over nt <= 1024 float32 device tensors: params[i],
  * grads[i], exp_avg[i], exp_avg_sq[i] (numel[i] elements each) and step[i] (a float32 device
  * scalar per tensor, torch's capturable Adam state; all tensors share one step count).  With
  * c = min(1, max_norm / (||grads||_2 + 1e-6)) (max_norm <= 0: c = 1) and t = step + 1:

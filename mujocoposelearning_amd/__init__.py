@@ -5,7 +5,11 @@ Drop-in for the hot path of redradman/MujocoPoseLearning: the per-process
 for gfx950 behind the same ``HumanoidEnv`` / VecEnv / ``REWARD_FUNCTIONS`` surface.
 Heavy modules (torch, the native library) load lazily on first use.
 """
-__version__ = "0.1.0"
+import os as _os
+
+__version__ = "0.2.0"
+# the reference's model (XML/humanoid.xml, custom_env.py:53), shipped as package data
+HUMANOID_XML = _os.path.join(_os.path.dirname(_os.path.abspath(__file__)), "assets", "humanoid.xml")
 
 from .reward_functions import REWARD_FUNCTIONS, robust_kneeling_reward, stand_reward, walk_reward  # noqa: F401
 from .utils import quaternion_to_euler  # noqa: F401

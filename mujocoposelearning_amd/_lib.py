@@ -17,19 +17,21 @@ HS_FULL_STATE = 0x100      # OR-ed into hs_batch_create's precision: cfrc_ext / 
 HS_REWARD_NONE, HS_REWARD_STAND, HS_REWARD_KNEELING, HS_REWARD_WALK = -1, 0, 1, 2
 HS_NWARN = 4
 HS_AUXDIM = 40
+HS_OUT_AUX, HS_OUT_CTRL = 1, 2   # hs_env_config.outputs bits
 DBGDIM = 16384
 
 
 class hs_env_config(C.Structure):
     _fields_ = [("frame_skip", C.c_int), ("max_steps", C.c_int), ("reward_id", C.c_int), ("autoreset", C.c_int),
-                ("max_newton", C.c_int), ("reserved", C.c_int), ("duration", C.c_double),
+                ("max_newton", C.c_int), ("outputs", C.c_int), ("duration", C.c_double),
                 ("init_height", C.c_double), ("noise_scale", C.c_double), ("kneel_params", C.c_double * 9)]
 
 
 class hs_buffers(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ("qpos", "qvel", "qacc_warmstart", "ctrl", "time", "step_count", "episode",
                                           "total_reward", "warning", "obs", "terminal_obs", "reward", "terminated",
-                                          "truncated", "aux", "cfrc_ext", "subtree_linvel")]
+                                          "truncated", "aux", "cfrc_ext", "subtree_linvel", "terminal_step_count",
+                                          "terminal_total_reward")]
 
 
 class hs_batch_info(C.Structure):
@@ -68,12 +70,14 @@ def lib():
         "hs_set_seed": (i, [vp, u64]),
         "hs_reset": (i, [vp, vp, vp, vp, vp]),
         "hs_step": (i, [vp, vp, vp]),
+        "hs_set_autoreset_noise": (i, [vp, vp, vp]),
         "hs_physics_step": (i, [vp, vp, i, vp]),
         "hs_state_io": (i, [vp, i, vp, vp, vp, vp, vp]),
         "hs_kinematics": (i, [vp, i, vp, vp, vp, vp, vp, vp]),
         "hs_set_debug": (i, [vp, i]),
         "hs_get_debug": (i, [vp, vp, i]),
         "hs_synchronize": (i, [vp]),
+        "hs_batch_counters": (i, [vp, vp]),
         "hs_gae": (i, [vp, vp, vp, vp, vp, vp, vp, i, i, C.c_float, C.c_float, vp]),
         "hs_ppo_act": (i, [vp, i, vp, i, vp, vp, u64, u64, vp, i, vp, vp, vp, vp, vp, i, i, vp]),
         "hs_ppo_post": (i, [vp, vp, vp, vp, vp, vp, vp, i, C.c_float, vp, vp, u64, vp, vp, vp, vp, vp, i, vp]),
@@ -102,8 +106,8 @@ def lib():
 
 
 EXPORTED = ("hs_model_load", "hs_model_free", "hs_model_field", "hs_batch_create", "hs_batch_destroy",
-            "hs_batch_get_info", "hs_get_buffers", "hs_set_config", "hs_set_seed", "hs_get_config", "hs_reset", "hs_step",
-            "hs_physics_step", "hs_state_io", "hs_kinematics", "hs_set_debug", "hs_get_debug", "hs_synchronize", "hs_gae",
+            "hs_batch_get_info", "hs_get_buffers", "hs_set_config", "hs_set_seed", "hs_get_config", "hs_reset", "hs_step", "hs_set_autoreset_noise",
+            "hs_physics_step", "hs_state_io", "hs_kinematics", "hs_set_debug", "hs_get_debug", "hs_synchronize", "hs_batch_counters", "hs_gae",
             "hs_ppo_act", "hs_ppo_post", "hs_gauss_logp", "hs_gauss_logp_grad",
             "hs_ppo_loss_workspace", "hs_ppo_loss", "hs_ppo_loss_grad", "hs_adam_workspace", "hs_adam_clip",
             "hs_colsum_partial_rows", "hs_relu_grad_colsum", "hs_colsum_pair",

@@ -51,7 +51,8 @@ class HsBatch:
                       step_count=z(N, dt=i32), episode=z(N, dt=i32), total_reward=z(N),
                       warning=z(N, _lib.HS_NWARN, dt=i32), obs=z(N, self.obs_dim), terminal_obs=z(N, self.obs_dim),
                       reward=z(N), terminated=z(N, dt=u8), truncated=z(N, dt=u8), aux=z(N, _lib.HS_AUXDIM),
-                      cfrc_ext=z(N, nb, 6), subtree_linvel=z(N, nb, 3))
+                      cfrc_ext=z(N, nb, 6), subtree_linvel=z(N, nb, 3), terminal_step_count=z(N, dt=i32),
+                      terminal_total_reward=z(N))
         torch.cuda.synchronize(self.device)
         flags = prec | (_lib.HS_FULL_STATE if self.full_state else 0)
         G = max(1, min(int(groups), self.n))
@@ -88,8 +89,15 @@ class HsBatch:
 
     # -- configuration ---------------------------------------------------------------------
     def configure(self, frame_skip=None, duration=None, reward_id=None, max_steps=None, autoreset=None,
-                  max_newton=None, init_height=None, noise_scale=None, kneel_params=None):
+                  max_newton=None, init_height=None, noise_scale=None, kneel_params=None, aux=None, ctrl=None):
+        """``aux`` / ``ctrl``: write the optional aux row (qacc, subtree com, contact / row counts,
+        solver iterations) and the data.ctrl copy at every commit (both on by default; data views,
+        host rewards and statistics read them, the on-device trainer does not)."""
         c = self.cfg
+        if aux is not None:
+            c.outputs = (c.outputs & ~_lib.HS_OUT_AUX) | (_lib.HS_OUT_AUX if aux else 0)
+        if ctrl is not None:
+            c.outputs = (c.outputs & ~_lib.HS_OUT_CTRL) | (_lib.HS_OUT_CTRL if ctrl else 0)
         if frame_skip is not None:
             c.frame_skip = int(frame_skip)
         if duration is not None:
@@ -171,6 +179,25 @@ class HsBatch:
                      mk, qn, vn)
         return self.t["obs"]
 
+    def set_autoreset_noise(self, qpos_noise=None, qvel_noise=None):
+        """Bind [N, nq] / [N, nv] device tensors (batch dtype) holding each env's NEXT reset noise
+        for the auto-reset inside ``step`` (None: the on-device counter RNG).  The tensors are
+        kept referenced; refresh the rows of envs that reset (hs_set_autoreset_noise)."""
+        torch = _torch()
+        if qpos_noise is None:
+            self._ar_noise = None
+            for h, _, _ in self._groups:
+                check(lib().hs_set_autoreset_noise(h, None, None))
+            return
+        qn = torch.as_tensor(qpos_noise, device=self.device).to(self.dtype).contiguous()
+        vn = torch.as_tensor(qvel_noise, device=self.device).to(self.dtype).contiguous()
+        assert qn.shape == (self.n, self.model.nq) and vn.shape == (self.n, self.model.nv)
+        self._ar_noise = (qn, vn)
+        for h, lo, hi in self._groups:
+            check(lib().hs_set_autoreset_noise(h, qn.data_ptr() + lo * qn.stride(0) * qn.element_size(),
+                                               vn.data_ptr() + lo * vn.stride(0) * vn.element_size()))
+        return qn, vn
+
     def step(self, actions, join=True):
         """custom_env.py:152-230 batched; ``actions`` [N, nu] float32 on device.  With stream
         groups and join=False the groups run free; call ``join()`` before reading outputs."""
@@ -243,6 +270,16 @@ class HsBatch:
         out = np.zeros(_lib.DBGDIM)
         check(lib().hs_get_debug(self._h, out.ctypes.data, _lib.DBGDIM))
         return out
+
+    def wide_reruns(self):
+        """Env steps re-run by the wide contact tier so far (resident tier overflowed; see
+        hs_model.h).  Synchronous."""
+        tot = 0
+        for h, _, _ in self._groups:
+            v = C.c_uint64(0)
+            check(lib().hs_batch_counters(h, C.byref(v)))
+            tot += int(v.value)
+        return tot
 
     def synchronize(self):
         for h, _, _ in self._groups:

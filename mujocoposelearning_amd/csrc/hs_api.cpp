@@ -23,6 +23,10 @@ struct hs_batch {
   bool owns = false;
   void* dbg = nullptr;
   bool debug = false;
+  const void* ar_qpos_noise = nullptr;       // bound auto-reset noise [n][nq] / [n][nv] (null: device RNG)
+  const void* ar_qvel_noise = nullptr;
+  int* redo = nullptr;                       // wide-tier work list [2 + n] (kernel-managed)
+  unsigned long long* redo_total = nullptr;  // cumulative wide-tier re-runs
   hs_env_config cfg{};
 };
 
@@ -73,6 +77,10 @@ hs::EnvBuffers<T> env_buffers(const hs_batch* b) {
   e.aux = (T*)b->buf.aux;
   e.cfrc_ext = (T*)b->buf.cfrc_ext;
   e.subtree_linvel = (T*)b->buf.subtree_linvel;
+  e.term_step_count = b->buf.terminal_step_count;
+  e.term_total_reward = (T*)b->buf.terminal_total_reward;
+  e.redo = b->redo;
+  e.redo_total = b->redo_total;
   e.dbg = b->debug ? (T*)b->dbg : nullptr;
   return e;
 }
@@ -93,6 +101,7 @@ hs::StepParams params_of(const hs_batch* b, int mode, int nsub) {
   p.seed = b->seed;
   for (int k = 0; k < 9; k++) p.kneel[k] = b->cfg.kneel_params[k];
   p.solver = b->model->host.solver == 1 ? hs::SOLVER_PGS : hs::SOLVER_NEWTON;
+  p.outputs = b->cfg.outputs;
   return p;
 }
 
@@ -148,7 +157,11 @@ bool init_state(hs_batch* b) {
          hip_ok(hipMemset(b->buf.truncated, 0, (size_t)N), "init") &&
          hip_ok(hipMemset(b->buf.aux, 0, (size_t)N * hs::AUXDIM * es), "init") &&
          (!b->buf.cfrc_ext || hip_ok(hipMemset(b->buf.cfrc_ext, 0, (size_t)N * m.nbody * 6 * es), "init")) &&
-         (!b->buf.subtree_linvel || hip_ok(hipMemset(b->buf.subtree_linvel, 0, (size_t)N * m.nbody * 3 * es), "init"));
+         (!b->buf.subtree_linvel || hip_ok(hipMemset(b->buf.subtree_linvel, 0, (size_t)N * m.nbody * 3 * es), "init")) &&
+         (!b->buf.terminal_step_count || hip_ok(hipMemset(b->buf.terminal_step_count, 0, (size_t)N * 4), "init")) &&
+         (!b->buf.terminal_total_reward || hip_ok(hipMemset(b->buf.terminal_total_reward, 0, (size_t)N * es), "init")) &&
+         hip_ok(hipMemset(b->redo, 0, (size_t)(N + 2) * sizeof(int)), "init") &&
+         hip_ok(hipMemset(b->redo_total, 0, sizeof(unsigned long long)), "init");
 }
 
 template <typename T>
@@ -269,6 +282,7 @@ hs_batch* hs_batch_create(const hs_model* m, int n_envs, int device, uint64_t se
   b->cfg.reward_id = HS_REWARD_STAND;
   b->cfg.autoreset = 1;
   b->cfg.max_newton = m->host.iterations;     // <option iterations>
+  b->cfg.outputs = HS_OUT_AUX | HS_OUT_CTRL;
   b->cfg.duration = 15.0;
   b->cfg.init_height = 1.282;
   b->cfg.noise_scale = 0.01;
@@ -292,10 +306,16 @@ hs_batch* hs_batch_create(const hs_model* m, int n_envs, int device, uint64_t se
          al(&b->buf.obs, N * b->obs_dim * es) && al(&b->buf.terminal_obs, N * b->obs_dim * es) &&
          al(&b->buf.reward, N * es) && al((void**)&b->buf.terminated, N) && al((void**)&b->buf.truncated, N) &&
          al(&b->buf.aux, N * hs::AUXDIM * es) && al(&b->buf.cfrc_ext, N * h.nbody * 6 * es) &&
-         al(&b->buf.subtree_linvel, N * h.nbody * 3 * es);
+         al(&b->buf.subtree_linvel, N * h.nbody * 3 * es) && al((void**)&b->buf.terminal_step_count, N * 4) &&
+         al(&b->buf.terminal_total_reward, N * es);
     if (!ok) { hs_batch_destroy(b); return nullptr; }
   }
-  if (!hip_ok(hipMalloc(&b->dbg, hs::DBGDIM * 8), "hipMalloc(dbg)")) { hs_batch_destroy(b); return nullptr; }
+  if (!hip_ok(hipMalloc(&b->dbg, hs::DBGDIM * 8), "hipMalloc(dbg)") ||
+      !hip_ok(hipMalloc((void**)&b->redo, (N + 2) * sizeof(int)), "hipMalloc(redo)") ||
+      !hip_ok(hipMalloc((void**)&b->redo_total, sizeof(unsigned long long)), "hipMalloc(redo_total)")) {
+    hs_batch_destroy(b);
+    return nullptr;
+  }
   ok = precision == HS_FP64 ? init_state<double>(b) : init_state<float>(b);
   if (!ok) { hs_batch_destroy(b); return nullptr; }
   return b;
@@ -308,12 +328,14 @@ void hs_batch_destroy(hs_batch* b) {
     void* ptrs[] = {b->buf.qpos, b->buf.qvel, b->buf.qacc_warmstart, b->buf.ctrl, b->buf.time, b->buf.step_count,
                     b->buf.episode, b->buf.total_reward, b->buf.warning, b->buf.obs, b->buf.terminal_obs,
                     b->buf.reward, b->buf.terminated, b->buf.truncated, b->buf.aux, b->buf.cfrc_ext,
-                    b->buf.subtree_linvel};
+                    b->buf.subtree_linvel, b->buf.terminal_step_count, b->buf.terminal_total_reward};
     for (void* p : ptrs)
       if (p) (void)hipFree(p);
   }
   if (b->dmodel) (void)hipFree(b->dmodel);
   if (b->dbg) (void)hipFree(b->dbg);
+  if (b->redo) (void)hipFree(b->redo);
+  if (b->redo_total) (void)hipFree(b->redo_total);
   delete b;
 }
 
@@ -339,6 +361,7 @@ int hs_set_config(hs_batch* b, const hs_env_config* cfg) {
   if (cfg->frame_skip < 1) return fail("frame_skip must be >= 1");
   if (cfg->max_newton < 1) return fail("max_newton must be >= 1");
   if (cfg->reward_id < HS_REWARD_NONE || cfg->reward_id > HS_REWARD_WALK) return fail("unknown reward id");
+  if (cfg->outputs & ~(HS_OUT_AUX | HS_OUT_CTRL)) return fail("unknown output bits");
   b->cfg = *cfg;
   return 0;
 }
@@ -361,7 +384,16 @@ int hs_reset(hs_batch* b, const uint8_t* mask, const void* qpos_noise, const voi
 
 int hs_step(hs_batch* b, const float* actions, void* stream) {
   if (!actions) return fail("hs_step: actions must not be NULL");
-  return launch(b, hs::MODE_ENV_STEP, actions, nullptr, nullptr, nullptr, b ? b->cfg.frame_skip : 1, stream);
+  if (!b) return fail("null batch");
+  return launch(b, hs::MODE_ENV_STEP, actions, nullptr, b->ar_qpos_noise, b->ar_qvel_noise, b->cfg.frame_skip, stream);
+}
+
+int hs_set_autoreset_noise(hs_batch* b, const void* qpos_noise, const void* qvel_noise) {
+  if (!b) return fail("null batch");
+  if ((qpos_noise == nullptr) != (qvel_noise == nullptr)) return fail("bind both noise arrays or neither");
+  b->ar_qpos_noise = qpos_noise;
+  b->ar_qvel_noise = qvel_noise;
+  return 0;
 }
 
 int hs_physics_step(hs_batch* b, const float* ctrl, int nsub, void* stream) {
@@ -504,7 +536,7 @@ uint64_t hs_adam_workspace(uint64_t total_numel) { return (uint64_t)hs::adam_par
 int hs_adam_clip(int nt, float* const* params, const float* const* grads, float* const* exp_avg,
                  float* const* exp_avg_sq, float* const* step, const int64_t* numel, float* workspace, float max_norm,
                  double lr, double beta1, double beta2, double eps, void* stream) {
-  if (nt < 1 || nt > 16) return fail("hs_adam_clip: need 1 <= nt <= 16 tensors");
+  if (nt < 1 || nt > 1024) return fail("hs_adam_clip: need 1 <= nt <= 1024 tensors");
   if (!params || !grads || !exp_avg || !exp_avg_sq || !step || !numel || !workspace)
     return fail("hs_adam_clip: null argument");
   std::vector<long long> n(nt);
@@ -563,6 +595,17 @@ int hs_gae(const float* rewards, const float* values, const float* episode_start
                 "gae_kernel")
              ? 0
              : -1;
+}
+
+int hs_batch_counters(const hs_batch* b, uint64_t* wide_reruns) {
+  if (!b || !wide_reruns) return fail("null argument");
+  DeviceGuard g(b->device);
+  unsigned long long v = 0;
+  if (!hip_ok(hipDeviceSynchronize(), "sync") ||
+      !hip_ok(hipMemcpy(&v, b->redo_total, sizeof v, hipMemcpyDeviceToHost), "counters"))
+    return -1;
+  *wide_reruns = v;
+  return 0;
 }
 
 int hs_synchronize(hs_batch* b) {

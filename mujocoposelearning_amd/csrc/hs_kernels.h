@@ -34,6 +34,10 @@ struct EnvBuffers {
   T* aux;                // [N][AUXDIM]
   T* cfrc_ext;           // [N][nbody][6]  (full_state)
   T* subtree_linvel;     // [N][nbody][3]  (full_state)
+  int* term_step_count;  // [N] or null: step_count of envs that auto-reset this step (SB3 final info)
+  T* term_total_reward;  // [N] or null: their episode return
+  int* redo;             // [2 + N] wide-tier work list: count, done counter, env ids (hs_batch owned)
+  unsigned long long* redo_total;   // cumulative number of wide-tier re-runs (diagnostics)
   T* dbg;                // [DBGDIM] or nullptr
 };
 
@@ -53,7 +57,11 @@ struct StepParams {
   double kneel[9];       // target_height, min_height, max_roll_pitch, com_radius, energy_w, posture_w,
                          // com_w, foot_w, alive_w (reward_functions.py:71-81)
   int solver;            // SOLVER_NEWTON (MuJoCo default) or SOLVER_PGS: selects the kernel instance
+  int outputs;           // OUT_* bits: optional per-env outputs written at commit
 };
+// optional outputs (hs_env_config.outputs): the aux row (qacc, subtree com, ncon, nefc, solver
+// iterations -- data views and stats) and the data.ctrl copy (data views / host rewards)
+enum Outputs { OUT_AUX = 1, OUT_CTRL = 2 };
 enum Solver { SOLVER_NEWTON = 0, SOLVER_PGS = 1 };
 
 // actions: [N][nu] float32 (may be null in MODE_RESET); reset_mask: [N] (null = all);
@@ -98,7 +106,7 @@ hipError_t launch_ppo_loss_fwd(const float* logp, const float* v, const int64_t*
                                float* ws, hipStream_t stream);
 hipError_t launch_ppo_loss_bwd(const float* logp, const float* v, int B, float clip, const float* ws,
                                const float* g_pg, const float* g_vf, float* g_logp, float* g_v, hipStream_t stream);
-// clip_grad_norm_ + Adam over up to 16 tensors (ppo.hip); part: adam_partials(total numel) floats
+// clip_grad_norm_ + Adam over up to 1024 tensors (ppo.hip); part: adam_partials(total numel) floats
 int adam_partials(long long total);
 hipError_t launch_adam_clip(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
                             float* const* step, const long long* numel, float* part, float max_norm, double lr,

@@ -22,6 +22,7 @@
 // HBM traffic is only the per-env state in/out; the model is read through L1/L2.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <type_traits>
@@ -34,8 +35,19 @@ namespace {
 
 constexpr int WAVE = 64;
 constexpr int HL = 32;            // lanes per env
-constexpr int RPL = MAXEFC / HL;  // constraint rows per lane
 static_assert(MAXDOF == HL, "one dof per sub-lane (lim_row slots, dof masks)");
+
+// Per-env contact / constraint-row capacity of a kernel instance (hs_model.h): the resident tier
+// every launch runs with and the wide tier that re-runs the (rare) envs overflowing it.
+template <int NCON, int NEFC>
+struct Cap {
+  static constexpr int CON = NCON;        // contacts (CON / HL per lane)
+  static constexpr int EFC = NEFC;        // constraint rows
+  static constexpr int RPL = NEFC / HL;   // rows per lane (kept in registers by the row's lane)
+  static_assert(NCON % HL == 0 && NEFC % HL == 0, "capacity in whole half-waves");
+};
+using Resident = Cap<MAXCON, MAXEFC>;
+using Wide = Cap<MAXCON_WIDE, MAXEFC_WIDE>;
 
 // scheduling fence: keeps the machine scheduler from hoisting loads across iterations of fully
 // unrolled loops (which otherwise inflates VGPR pressure far past the occupancy target)
@@ -337,7 +349,7 @@ enum RowKind { RK_JLO = 0, RK_JHI = 1, RK_TLO = 2, RK_THI = 3, RK_CN = 4, RK_P0 
 __device__ __forceinline__ int rk_kind(int kid) { return kid >> 16; }
 __device__ __forceinline__ int rk_id(int kid) { return kid & 0xffff; }
 
-template <typename T>
+template <typename T, typename C>
 struct Scratch {
   T qpos[MAXQ];
   T qvel[MAXDOF];
@@ -347,24 +359,24 @@ struct Scratch {
   T cinert[MAXBODY][10];
   T cdof[MAXDOF][6];
   T cvel[MAXBODY][6];
-  T con_pos[MAXCON][3];
-  T con_n[MAXCON][3];
-  T con_t1[MAXCON][3];
-  T con_dist[MAXCON];
-  T con_v[MAXCON][3];
-  T con_U[MAXCON][6];
-  T con_F[MAXCON][3];
-  int con_pair[MAXCON];
-  int con_adr[MAXCON];
-  uint32_t con_bb[MAXCON];    // b1 | b2 << 8 | condim << 16 of the contact's pair (no model lookups per use)
-  uint32_t con_m1[MAXCON];    // dof chain masks of the contact's bodies (m1 = 0: world)
-  uint32_t con_m2[MAXCON];
-  T con_mu[MAXCON];
+  T con_pos[C::CON][3];
+  T con_n[C::CON][3];
+  T con_t1[C::CON][3];
+  T con_dist[C::CON];
+  T con_v[C::CON][3];
+  T con_U[C::CON][6];
+  T con_F[C::CON][3];
+  int con_pair[C::CON];
+  int con_adr[C::CON];
+  uint32_t con_bb[C::CON];    // b1 | b2 << 8 | condim << 16 of the contact's pair (no model lookups per use)
+  uint32_t con_m1[C::CON];    // dof chain masks of the contact's bodies (m1 = 0: world)
+  uint32_t con_m2[C::CON];
+  T con_mu[C::CON];
   uint16_t lim_row[MAXDOF];   // joint-limit rows of a dof: (lo row + 1) | (hi row + 1) << 8
-  uint32_t dense_mask[MAXEFC / HL];   // rows added as dense rank-1 Hessian terms (tendons, body-body)
-  int row_kid[MAXEFC];
-  T row_D[MAXEFC];
-  T row_f[MAXEFC];
+  uint32_t dense_mask[C::RPL];   // rows added as dense rank-1 Hessian terms (tendons, body-body)
+  int row_kid[C::EFC];
+  T row_D[C::EFC];
+  T row_f[C::EFC];
   int ncon, nefc, nlim, njl;   // njl: joint-limit rows (tendon rows are [njl, nlim))
   union {   // phase-local arrays (aliased)
     struct { T xpos[MAXBODY][3]; T xmat[MAXBODY][9]; T xquat[MAXBODY][4]; T xanchor[MAXJNT][3];
@@ -380,12 +392,12 @@ struct Scratch {
 // PGS solver scratch (the <option solver="PGS"> kernel instance only; the Newton instance never
 // allocates it): rows [0, PGS_CACHE) keep J_r and M^-1 J_r' per dof, every row its AR_rr and aref
 constexpr int PGS_CACHE = 32;
-template <typename T>
+template <typename T, typename C>
 struct PgsCache {
   T J[PGS_CACHE][MAXDOF];
   T MJ[PGS_CACHE][MAXDOF];
-  T AR[MAXEFC];
-  T ar[MAXEFC];
+  T AR[C::EFC];
+  T ar[C::EFC];
 };
 
 // ------------------------------------------------------------------ narrow phase
@@ -429,8 +441,8 @@ __device__ __forceinline__ void make_frame(Con<T>& c) {
 }
 
 // number of contacts (0..2) for static pair p (mjc_* primitives)
-template <typename T>
-__device__ __forceinline__ int collide_pair(const Scratch<T>& s, const int4 info, const T (&sz)[4], Con<T>& c0,
+template <typename T, typename C>
+__device__ __forceinline__ int collide_pair(const Scratch<T, C>& s, const int4 info, const T (&sz)[4], Con<T>& c0,
                                            Con<T>& c1) {
   const int g1 = info.x, g2 = info.y, fn = info.z;
   const T* p1 = s.u.k.gpos[g1];
@@ -489,9 +501,9 @@ __device__ __forceinline__ int collide_pair(const Scratch<T>& s, const int4 info
   return n;
 }
 
-template <typename T>
-__device__ __forceinline__ void store_contact(MPtr<T> m, Scratch<T>& s, int slot, const Con<T>& c, int p) {
-  if (slot >= MAXCON) return;
+template <typename T, typename C>
+__device__ __forceinline__ void store_contact(MPtr<T> m, Scratch<T, C>& s, int slot, const Con<T>& c, int p) {
+  if (slot >= C::CON) return;
   for (int k = 0; k < 3; k++) { s.con_pos[slot][k] = c.pos[k]; s.con_n[slot][k] = c.n[k]; s.con_t1[slot][k] = c.t1[k]; }
   s.con_dist[slot] = c.dist;
   s.con_pair[slot] = p;
@@ -531,8 +543,8 @@ template <typename T>
 __device__ __forceinline__ uint32_t chain_mask(MPtr<T> m, int sl, int nb) {
   return (sl > 0 && sl < nb) ? m->body_chainmask[sl] : 0u;
 }
-template <int NV, typename T>
-__device__ __forceinline__ void map_vx(Scratch<T>& s, int sl, int nb, uint32_t ch) {
+template <int NV, typename T, typename C>
+__device__ __forceinline__ void map_vx(Scratch<T, C>& s, int sl, int nb, uint32_t ch) {
   if (sl < nb) {   // body spatial velocity = sum over the body's dof chain of cdof_j x_j
     T v[6] = {0, 0, 0, 0, 0, 0};
     static_for<0, NV>([&](auto jc) {      // unrolled + predicated: no per-dof branch, loads pipelined
@@ -544,21 +556,25 @@ __device__ __forceinline__ void map_vx(Scratch<T>& s, int sl, int nb, uint32_t c
     for (int k = 0; k < 6; k++) s.u.n.bvel[sl][k] = v[k];
   }
   WSYNC();
-  if (sl < s.ncon) {
-    const uint32_t bb = s.con_bb[sl];
-    const int b1 = bb & 0xff, b2 = (bb >> 8) & 0xff;
-    T r[3] = {s.con_pos[sl][0] - s.com[0], s.con_pos[sl][1] - s.com[1], s.con_pos[sl][2] - s.com[2]};
-    T w[3], v1[3], v2[3];
-    cross3(s.u.n.bvel[b2], r, w);
-    for (int k = 0; k < 3; k++) v2[k] = s.u.n.bvel[b2][3 + k] + w[k];
-    cross3(s.u.n.bvel[b1], r, w);
-    for (int k = 0; k < 3; k++) v1[k] = s.u.n.bvel[b1][3 + k] + w[k];
-    T dv[3] = {v2[0] - v1[0], v2[1] - v1[1], v2[2] - v1[2]};
-    T t2[3];
-    cross3(s.con_n[sl], s.con_t1[sl], t2);
-    s.con_v[sl][0] = dot3(s.con_n[sl], dv);
-    s.con_v[sl][1] = dot3(s.con_t1[sl], dv);
-    s.con_v[sl][2] = dot3(t2, dv);
+#pragma unroll
+  for (int cs = 0; cs < C::CON; cs += HL) {   // contact slots of this lane (one per lane in the resident tier)
+    const int c = cs + sl;
+    if (c < s.ncon) {
+      const uint32_t bb = s.con_bb[c];
+      const int b1 = bb & 0xff, b2 = (bb >> 8) & 0xff;
+      T r[3] = {s.con_pos[c][0] - s.com[0], s.con_pos[c][1] - s.com[1], s.con_pos[c][2] - s.com[2]};
+      T w[3], v1[3], v2[3];
+      cross3(s.u.n.bvel[b2], r, w);
+      for (int k = 0; k < 3; k++) v2[k] = s.u.n.bvel[b2][3 + k] + w[k];
+      cross3(s.u.n.bvel[b1], r, w);
+      for (int k = 0; k < 3; k++) v1[k] = s.u.n.bvel[b1][3 + k] + w[k];
+      T dv[3] = {v2[0] - v1[0], v2[1] - v1[1], v2[2] - v1[2]};
+      T t2[3];
+      cross3(s.con_n[c], s.con_t1[c], t2);
+      s.con_v[c][0] = dot3(s.con_n[c], dv);
+      s.con_v[c][1] = dot3(s.con_t1[c], dv);
+      s.con_v[c][2] = dot3(t2, dv);
+    }
   }
   WSYNC();
 }
@@ -566,8 +582,8 @@ __device__ __forceinline__ void map_vx(Scratch<T>& s, int sl, int nb, uint32_t c
 // Row descriptor kept in registers by the row's lane for the whole solve (no LDS / model
 // lookups per use): desc = kind << 16 | j with j = dof (joint limits), tendon id or contact id;
 // coef = +-1 (limits), +-mu (pyramid rows), 0 (frictionless contact normal).
-template <typename T>
-__device__ __forceinline__ T row_Jx(MPtr<T> m, const Scratch<T>& s, int desc, T coef) {
+template <typename T, typename C>
+__device__ __forceinline__ T row_Jx(MPtr<T> m, const Scratch<T, C>& s, int desc, T coef) {
   int kind = rk_kind(desc), j = rk_id(desc);
   if (kind <= RK_JHI) return coef * s.vx[j];
   if (kind <= RK_THI) {
@@ -580,8 +596,8 @@ __device__ __forceinline__ T row_Jx(MPtr<T> m, const Scratch<T>& s, int desc, T 
 }
 
 // world-frame force direction u of a contact row
-template <typename T>
-__device__ __forceinline__ void row_u(MPtr<T> m, const Scratch<T>& s, int kind, int c, T* u) {
+template <typename T, typename C>
+__device__ __forceinline__ void row_u(MPtr<T> m, const Scratch<T, C>& s, int kind, int c, T* u) {
   if (kind == RK_CN) { for (int k = 0; k < 3; k++) u[k] = s.con_n[c][k]; return; }
   int sub = kind - RK_P0;
   T mu = s.con_mu[c];
@@ -593,34 +609,38 @@ __device__ __forceinline__ void row_u(MPtr<T> m, const Scratch<T>& s, int kind, 
 }
 
 // per-contact aggregates from current row forces: U = sum D u u' (active rows), F = sum f u
-template <typename T>
-__device__ __forceinline__ void contact_aggregates(MPtr<T> m, Scratch<T>& s, int sl) {
-  if (sl < s.ncon) {
-    int adr = s.con_adr[sl];
-    int nr = (s.con_bb[sl] >> 16) == 1 ? 1 : 4;
-    T U[6] = {0, 0, 0, 0, 0, 0}, F[3] = {0, 0, 0};
-    for (int q = 0; q < nr; q++) {
-      int r = adr + q;
-      T f = s.row_f[r];
-      if (f != T(0)) {
-        T u[3];
-        row_u(m, s, rk_kind(s.row_kid[r]), sl, u);
-        T D = s.row_D[r];
-        U[0] += D * u[0] * u[0]; U[1] += D * u[1] * u[1]; U[2] += D * u[2] * u[2];
-        U[3] += D * u[0] * u[1]; U[4] += D * u[0] * u[2]; U[5] += D * u[1] * u[2];
-        for (int k = 0; k < 3; k++) F[k] += f * u[k];
+template <typename T, typename C>
+__device__ __forceinline__ void contact_aggregates(MPtr<T> m, Scratch<T, C>& s, int sl) {
+#pragma unroll
+  for (int cs = 0; cs < C::CON; cs += HL) {
+    const int c = cs + sl;
+    if (c < s.ncon) {
+      int adr = s.con_adr[c];
+      int nr = (s.con_bb[c] >> 16) == 1 ? 1 : 4;
+      T U[6] = {0, 0, 0, 0, 0, 0}, F[3] = {0, 0, 0};
+      for (int q = 0; q < nr; q++) {
+        int r = adr + q;
+        T f = s.row_f[r];
+        if (f != T(0)) {
+          T u[3];
+          row_u(m, s, rk_kind(s.row_kid[r]), c, u);
+          T D = s.row_D[r];
+          U[0] += D * u[0] * u[0]; U[1] += D * u[1] * u[1]; U[2] += D * u[2] * u[2];
+          U[3] += D * u[0] * u[1]; U[4] += D * u[0] * u[2]; U[5] += D * u[1] * u[2];
+          for (int k = 0; k < 3; k++) F[k] += f * u[k];
+        }
       }
+      for (int k = 0; k < 6; k++) s.con_U[c][k] = U[k];
+      for (int k = 0; k < 3; k++) s.con_F[c][k] = F[k];
     }
-    for (int k = 0; k < 6; k++) s.con_U[sl][k] = U[k];
-    for (int k = 0; k < 3; k++) s.con_F[sl][k] = F[k];
   }
   WSYNC();
 }
 
 // (J' f)_i for dof sub-lane i (contacts via point Jacobians, joint limits via the dof's
 // limit-row slots, tendon limits via rows [njl, nlim))
-template <typename T>
-__device__ __forceinline__ T jtf_lane(MPtr<T> m, const Scratch<T>& s, int sl, const T* cd) {
+template <typename T, typename C>
+__device__ __forceinline__ T jtf_lane(MPtr<T> m, const Scratch<T, C>& s, int sl, const T* cd) {
   T acc = 0;
   for (int c = 0; c < s.ncon; c++) {
     int in2 = bit(s.con_m2[c], sl), in1 = bit(s.con_m1[c], sl);
@@ -673,11 +693,11 @@ struct PhaseClock {
 #endif
 
 // ------------------------------------------------------------------ one mj_step (per half-wave)
-template <typename T, int NV>
+template <typename T, int NV, typename C>
 struct Stepper {
   PhaseClock clk;
   MPtr<T> m;
-  Scratch<T>& s;
+  Scratch<T, C>& s;
   int sl, nb;
   bool up;        // upper half-wave (second env of the wave)
   T cd[6];        // cdof of this sub-lane's dof (registers)
@@ -690,7 +710,7 @@ struct Stepper {
   int niter;
   T* dbg = nullptr;   // stage-dump target (env 0 in debug mode only)
 
-  __device__ Stepper(MPtr<T> mm, Scratch<T>& ss, int lane)
+  __device__ Stepper(MPtr<T> mm, Scratch<T, C>& ss, int lane)
       : m(mm), s(ss), sl(lane & (HL - 1)), nb(mm->nbody), up(lane >= HL) {}
 
   // start of a pipeline phase: nothing lane-invariant is carried over from the previous phase
@@ -895,8 +915,8 @@ struct Stepper {
       if (n >= 2) store_contact(m, s, ncon + pre + 1, c1, p);
       ncon += __popc(m1) + __popc(m2);
     }
-    int overflow = ncon > MAXCON;
-    if (overflow) ncon = MAXCON;
+    int overflow = ncon > C::CON;
+    if (overflow) ncon = C::CON;
     if (sl == 0) s.ncon = ncon;
     WSYNC();
     return overflow;
@@ -1012,7 +1032,7 @@ struct Stepper {
   }
 
   // mj_makeConstraint + mj_makeImpedance + reference (aref); row q of this lane: r = sl + 32 q
-  __device__ __forceinline__ int rows(T (&D)[RPL], T (&ar)[RPL], int (&rd)[RPL], T (&rc)[RPL]) {
+  __device__ __forceinline__ int rows(T (&D)[C::RPL], T (&ar)[C::RPL], int (&rd)[C::RPL], T (&rc)[C::RPL]) {
     phase_begin();
     damp = sl < NV ? m->dof_damping[sl] : T(0);
     int overflow = 0;
@@ -1050,38 +1070,47 @@ struct Stepper {
       nrow += __popc(ml) + __popc(mh);
     }
     int nlim = nrow;
-    {   // contacts: 1 row (condim 1) or 4 pyramid rows (condim 3)
-      bool isc = sl < ncon;
-      bool pyr = isc && (s.con_bb[sl] >> 16) == 3;
-      uint32_t mc = hballot(isc, up), mp = hballot(pyr, up);
-      int pre = nrow + below(mc, sl) + 3 * below(mp, sl);
-      int tot = __popc(mc) + 3 * __popc(mp);
-      if (nrow + tot > MAXEFC) {   // drop whole contacts that do not fit (counted as overflow)
+    {   // contacts: 1 row (condim 1) or 4 pyramid rows (condim 3), in contact order
+      int tot = 0;
+#pragma unroll
+      for (int cs = 0; cs < C::CON; cs += HL) {
+        const int c = cs + sl;
+        const bool isc = c < ncon;
+        const bool pyr = isc && (s.con_bb[c] >> 16) == 3;
+        tot += __popc(hballot(isc, up)) + 3 * __popc(hballot(pyr, up));
+      }
+      if (nrow + tot > C::EFC) {   // drop whole contacts that do not fit (counted as overflow)
         overflow = 1;
         int fit = 0, nr = nrow;
         for (int c = 0; c < ncon; c++) {
           int need = (s.con_bb[c] >> 16) == 3 ? 4 : 1;
-          if (nr + need > MAXEFC) break;
+          if (nr + need > C::EFC) break;
           nr += need;
           fit++;
         }
         ncon = fit;
-        isc = sl < ncon;
-        tot = nr - nrow;
       }
-      if (isc) {
-        s.con_adr[sl] = pre;
-        if (!pyr) s.row_kid[pre] = (RK_CN << 16) | sl;
-        else for (int q = 0; q < 4; q++) s.row_kid[pre + q] = ((RK_P0 + q) << 16) | sl;
+#pragma unroll
+      for (int cs = 0; cs < C::CON; cs += HL) {
+        const int c = cs + sl;
+        const bool isc = c < ncon;
+        const bool pyr = isc && (s.con_bb[c] >> 16) == 3;
+        const uint32_t mc = hballot(isc, up), mp = hballot(pyr, up);
+        const int pre = nrow + below(mc, sl) + 3 * below(mp, sl);
+        if (isc) {
+          s.con_adr[c] = pre;
+          if (!pyr) s.row_kid[pre] = (RK_CN << 16) | c;
+          else for (int q = 0; q < 4; q++) s.row_kid[pre + q] = ((RK_P0 + q) << 16) | c;
+        }
+        nrow += __popc(mc) + 3 * __popc(mp);
       }
-      nrow += tot;
     }
     if (sl == 0) { s.ncon = ncon; s.nefc = nrow; s.nlim = nlim; s.njl = njl; }
     if (sl < NV) s.vx[sl] = s.qvel[sl];
     WSYNC();
     map_vx<NV>(s, sl, nb, chain_mask(m, sl, nb));     // row velocities J qvel for aref
 #pragma unroll
-    for (int q = 0; q < RPL; q++) {
+    for (int q = 0; q < C::RPL; q++) {
       int r = sl + HL * q;
       D[q] = 0;
       ar[q] = 0;
@@ -1153,14 +1182,14 @@ struct Stepper {
   }
 
   // primal Newton (mj_solNewton semantics), warm-started; x = qacc
-  __device__ __forceinline__ void solve(T xws, int maxit, T tol, const T (&D)[RPL], const T (&ar)[RPL],
-                                        const int (&rd)[RPL], const T (&rc)[RPL]) {
+  __device__ __forceinline__ void solve(T xws, int maxit, T tol, const T (&D)[C::RPL], const T (&ar)[C::RPL],
+                                        const int (&rd)[C::RPL], const T (&rc)[C::RPL]) {
     phase_begin();
     const int nefc = s.nefc, ncon = s.ncon;
     T x = sl < NV ? xws : T(0);
-    bool vr[RPL];
+    bool vr[C::RPL];
 #pragma unroll
-    for (int q = 0; q < RPL; q++) vr[q] = sl + HL * q < nefc;
+    for (int q = 0; q < C::RPL; q++) vr[q] = sl + HL * q < nefc;
     const uint32_t anci = sl < NV ? m->dof_ancmask[sl] : 0u;
     const uint32_t bch = chain_mask(m, sl, nb);     // loaded once per solve (map_vx per iteration)
     const T scale = m->newton_scale;
@@ -1168,18 +1197,18 @@ struct Stepper {
     WSYNC();
     T Mx = matvec_lds(Mr, s.vx);     // kept current below (Mx += alpha M s)
     map_vx<NV>(s, sl, nb, bch);
-    T jar[RPL], Js[RPL];
+    T jar[C::RPL], Js[C::RPL];
 #pragma unroll
-    for (int q = 0; q < RPL; q++) jar[q] = vr[q] ? row_Jx(m, s, rd[q], rc[q]) - ar[q] : T(0);
+    for (int q = 0; q < C::RPL; q++) jar[q] = vr[q] ? row_Jx(m, s, rd[q], rc[q]) - ar[q] : T(0);
     HS_STAMP(clk, 6);
     bool done = false;      // this half-wave's solver has converged
     int it = 0;
     for (; it < maxit; it++) {
       m = opaque(m);
       sl = opaque_v(sl);
-      bool act[RPL];
+      bool act[C::RPL];
 #pragma unroll
-      for (int q = 0; q < RPL; q++) {
+      for (int q = 0; q < C::RPL; q++) {
         act[q] = vr[q] && jar[q] < 0;
         if (vr[q]) s.row_f[sl + HL * q] = act[q] ? -D[q] * jar[q] : T(0);
       }
@@ -1226,13 +1255,13 @@ struct Stepper {
         }
         // dense rank-1 rows (tendon limits, body-body contacts): only the rows flagged in
         // dense_mask; the loop runs max(#rows of either half) times (wave-uniform control)
-        uint32_t dm[RPL];
+        uint32_t dm[C::RPL];
 #pragma unroll
-        for (int q = 0; q < RPL; q++) dm[q] = s.dense_mask[q];
+        for (int q = 0; q < C::RPL; q++) dm[q] = s.dense_mask[q];
         for (;;) {
           int r = -1;
 #pragma unroll
-          for (int q = RPL - 1; q >= 0; q--)
+          for (int q = C::RPL - 1; q >= 0; q--)
             if (dm[q]) r = HL * q + __builtin_ctz(dm[q]);
           if (__ballot(r >= 0) == 0) break;
           T jr = 0, Dr = 0;
@@ -1284,19 +1313,19 @@ struct Stepper {
       map_vx<NV>(s, sl, nb, bch);
       HS_STAMP(clk, 19);
 #pragma unroll
-      for (int q = 0; q < RPL; q++) Js[q] = vr[q] ? row_Jx(m, s, rd[q], rc[q]) : T(0);
+      for (int q = 0; q < C::RPL; q++) Js[q] = vr[q] ? row_Jx(m, s, rd[q], rc[q]) : T(0);
       HS_STAMP(clk, 16);
       // alpha = 1 is exact when no row changes state on [0, 1] (jar is linear in alpha)
       bool same1 = true;
 #pragma unroll
-      for (int q = 0; q < RPL; q++) same1 = same1 && (!vr[q] || ((jar[q] + Js[q] < 0) == act[q]));
+      for (int q = 0; q < C::RPL; q++) same1 = same1 && (!vr[q] || ((jar[q] + Js[q] < 0) == act[q]));
       bool lsdone = done || (hballot(!same1, up) == 0);
       T alpha = 1, lo = 0, hi = T(1e30);
       T d0 = 0;
       {
         T c = 0;
 #pragma unroll
-        for (int q = 0; q < RPL; q++) c += act[q] ? D[q] * jar[q] * Js[q] : T(0);
+        for (int q = 0; q < C::RPL; q++) c += act[q] ? D[q] * jar[q] * Js[q] : T(0);
         d0 = B0 + hsum(c);
       }
       const T ltol = (sizeof(T) == 8 ? T(1e-10) : T(1e-5)) * fabs(d0);
@@ -1304,7 +1333,7 @@ struct Stepper {
         if (__ballot(!lsdone) == 0) break;
         T c1 = 0, c2 = 0;
 #pragma unroll
-        for (int q = 0; q < RPL; q++) {
+        for (int q = 0; q < C::RPL; q++) {
           T jq = jar[q] + alpha * Js[q];
           bool a = vr[q] && jq < 0;
           c1 += a ? D[q] * jq * Js[q] : T(0);
@@ -1330,7 +1359,7 @@ struct Stepper {
         Mx += alpha * Ms;
         bool changed = false;
 #pragma unroll
-        for (int q = 0; q < RPL; q++) {
+        for (int q = 0; q < C::RPL; q++) {
           T nj = jar[q] + alpha * Js[q];
           changed = changed || (vr[q] && ((nj < 0) != act[q]));
           jar[q] = nj;
@@ -1342,7 +1371,7 @@ struct Stepper {
     niter = it;
     // final forces -> qfrc_constraint
 #pragma unroll
-    for (int q = 0; q < RPL; q++)
+    for (int q = 0; q < C::RPL; q++)
       if (vr[q]) s.row_f[sl + HL * q] = jar[q] < 0 ? -D[q] * jar[q] : T(0);
     WSYNC();
     contact_aggregates(m, s, sl);
@@ -1384,14 +1413,14 @@ struct Stepper {
   // M^-1 J_r' of the first PGS_CACHE rows are kept in LDS, later rows are rebuilt per sweep.
   // Warm start: the forces of qacc_warmstart under the primal map, kept if their dual cost is
   // negative.  Stops when a sweep's improvement * scale < tolerance, or after maxit sweeps.
-  __device__ __forceinline__ void solve_pgs(T xws, int maxit, const T (&D)[RPL], const T (&ar)[RPL],
-                                            const int (&rd)[RPL], const T (&rc)[RPL], PgsCache<T>& pc) {
+  __device__ __forceinline__ void solve_pgs(T xws, int maxit, const T (&D)[C::RPL], const T (&ar)[C::RPL],
+                                            const int (&rd)[C::RPL], const T (&rc)[C::RPL], PgsCache<T, C>& pc) {
     phase_begin();
     const int nefc = s.nefc;
     const uint32_t bch = chain_mask(m, sl, nb);
-    bool vr[RPL];
+    bool vr[C::RPL];
 #pragma unroll
-    for (int q = 0; q < RPL; q++) {
+    for (int q = 0; q < C::RPL; q++) {
       vr[q] = sl + HL * q < nefc;
       if (vr[q]) pc.ar[sl + HL * q] = ar[q];
     }
@@ -1405,9 +1434,9 @@ struct Stepper {
     if (sl < NV) s.vx[sl] = xws;
     WSYNC();
     map_vx<NV>(s, sl, nb, bch);
-    T f[RPL];
+    T f[C::RPL];
 #pragma unroll
-    for (int q = 0; q < RPL; q++) {
+    for (int q = 0; q < C::RPL; q++) {
       T jar = vr[q] ? row_Jx(m, s, rd[q], rc[q]) - ar[q] : T(0);
       f[q] = jar < 0 ? -D[q] * jar : T(0);
       if (vr[q]) s.row_f[sl + HL * q] = f[q];
@@ -1420,21 +1449,21 @@ struct Stepper {
     if (sl < NV) s.vx[sl] = z;
     WSYNC();
     map_vx<NV>(s, sl, nb, bch);
-    T c = 0, jz[RPL];
+    T c = 0, jz[C::RPL];
 #pragma unroll
-    for (int q = 0; q < RPL; q++) jz[q] = vr[q] ? row_Jx(m, s, rd[q], rc[q]) : T(0);
+    for (int q = 0; q < C::RPL; q++) jz[q] = vr[q] ? row_Jx(m, s, rd[q], rc[q]) : T(0);
     WSYNC();
     if (sl < NV) s.vx[sl] = qs;
     WSYNC();
     map_vx<NV>(s, sl, nb, bch);
 #pragma unroll
-    for (int q = 0; q < RPL; q++)
+    for (int q = 0; q < C::RPL; q++)
       if (vr[q]) c += f[q] * (T(0.5) * jz[q] + T(0.5) * f[q] / D[q] + row_Jx(m, s, rd[q], rc[q]) - ar[q]);
     const bool keep = hsum(c) <= T(0);
     T x = sl < NV ? (keep ? qs + z : qs) : T(0);
     if (!keep) {
 #pragma unroll
-      for (int q = 0; q < RPL; q++)
+      for (int q = 0; q < C::RPL; q++)
         if (vr[q]) s.row_f[sl + HL * q] = 0;
     }
     // rows that exist in either half of the wave (wave-uniform loop bound)
@@ -1592,8 +1621,8 @@ __device__ __forceinline__ T uniform_pm(uint64_t seed, int env, uint32_t episode
   return (T)(-scale + 2.0 * scale * u);
 }
 
-template <typename T>
-__device__ __forceinline__ void reset_state(MPtr<T> m, Scratch<T>& s, int sl, T& time, T& xws) {
+template <typename T, typename C>
+__device__ __forceinline__ void reset_state(MPtr<T> m, Scratch<T, C>& s, int sl, T& time, T& xws) {
   if (sl < m->nq) s.qpos[sl] = m->qpos0[sl];
   if (sl + HL < m->nq) s.qpos[sl + HL] = m->qpos0[sl + HL];
   if (sl < m->nv) s.qvel[sl] = 0;
@@ -1603,11 +1632,11 @@ __device__ __forceinline__ void reset_state(MPtr<T> m, Scratch<T>& s, int sl, T&
   WSYNC();
 }
 
-template <typename T, int NV, bool PGS>
-__device__ __forceinline__ void physics_step(Stepper<T, NV>& st, KPtr<T> k, T& time, T& xws, int* warn,
-                                             PgsCache<T>* pc) {
+template <typename T, int NV, bool PGS, typename C>
+__device__ __forceinline__ void physics_step(Stepper<T, NV, C>& st, KPtr<T> k, T& time, T& xws, int* warn,
+                                             PgsCache<T, C>* pc) {
   MPtr<T> m = st.m;
-  Scratch<T>& s = st.s;
+  Scratch<T, C>& s = st.s;
   const int sl = st.sl;
   const bool up = st.up;
   // mj_checkPos / mj_checkVel (auto-reset to qpos0, time 0)
@@ -1615,8 +1644,8 @@ __device__ __forceinline__ void physics_step(Stepper<T, NV>& st, KPtr<T> k, T& t
   bool bv = sl < m->nv && isbad(s.qvel[sl]);
   if (hballot(bq, up)) { warn[WARN_BADQPOS]++; reset_state(m, s, sl, time, xws); }
   else if (hballot(bv, up)) { warn[WARN_BADQVEL]++; reset_state(m, s, sl, time, xws); }
-  T D[RPL], ar[RPL], rc[RPL];
-  int rd[RPL];
+  T D[C::RPL], ar[C::RPL], rc[C::RPL];
+  int rd[C::RPL];
   for (int attempt = 0; attempt < 2; attempt++) {
     HS_STAMP(st.clk, 0);
     st.kinematics();
@@ -1648,16 +1677,16 @@ __device__ __forceinline__ void physics_step(Stepper<T, NV>& st, KPtr<T> k, T& t
 }
 
 // sum |cfrc_ext| of the last two bodies ("feet", reward_functions.py:121-122,176-177)
-template <typename T>
-__device__ __forceinline__ void foot_forces(MPtr<T> m, const Scratch<T>& s, T& lf, T& rf) {
+template <typename T, typename C>
+__device__ __forceinline__ void foot_forces(MPtr<T> m, const Scratch<T, C>& s, T& lf, T& rf) {
   const int nb = m->nbody;
   lf = 0;
   rf = 0;
   for (int k = 0; k < 6; k++) { lf += fabs(s.u.n.cfrc[nb - 2][k]); rf += fabs(s.u.n.cfrc[nb - 1][k]); }
 }
 
-template <typename T>
-__device__ __forceinline__ T compute_reward(MPtr<T> m, const Scratch<T>& s, KPtr<T> k, T time,
+template <typename T, typename C>
+__device__ __forceinline__ T compute_reward(MPtr<T> m, const Scratch<T, C>& s, KPtr<T> k, T time,
                             T energy_sum, T ctrl_sq) {
   // quaternion_to_euler (utils.py:3-21): pitch = arcsin(2(wy - zx)), not clamped
   T w = s.qpos[3], x = s.qpos[4], y = s.qpos[5], z = s.qpos[6];
@@ -1704,8 +1733,8 @@ __device__ __forceinline__ T compute_reward(MPtr<T> m, const Scratch<T>& s, KPtr
 }
 
 // custom_env.py:232-261 layout; qfrc_actuator comes from registers (sub-lane i holds dof i)
-template <typename T>
-__device__ __forceinline__ void write_obs(MPtr<T> m, const Scratch<T>& s, int sl, T qfa, T* out,
+template <typename T, typename C>
+__device__ __forceinline__ void write_obs(MPtr<T> m, const Scratch<T, C>& s, int sl, T qfa, T* out,
                           int obs_dim) {
   int nq = m->nq, nv = m->nv;
   int o1 = nq - 2, o2 = o1 + nv, o3 = o2 + 10 * m->nbody, o4 = o3 + 6 * m->nbody;
@@ -1723,9 +1752,9 @@ __device__ __forceinline__ void write_obs(MPtr<T> m, const Scratch<T>& s, int sl
     for (int k = sl; k < nf; k += HL) out[o5 + k] = s.u.n.cfrc[1 + k / 6][k % 6];
 }
 
-template <typename T, int NV>
-__device__ __forceinline__ void dump_debug(const Stepper<T, NV>& st, T* dbg) {
-  const Scratch<T>& s = st.s;
+template <typename T, int NV, typename C>
+__device__ __forceinline__ void dump_debug(const Stepper<T, NV, C>& st, T* dbg) {
+  const Scratch<T, C>& s = st.s;
   int sl = st.sl;
   for (int k = sl; k < MAXBODY * 10; k += HL) dbg[200 + k] = s.cinert[k / 10][k % 10];
   for (int k = sl; k < MAXDOF * 6; k += HL) dbg[500 + k] = s.cdof[k / 6][k % 6];
@@ -1749,34 +1778,37 @@ __device__ __forceinline__ void dump_debug(const Stepper<T, NV>& st, T* dbg) {
     o[10] = s.con_pair[c];
   }
   for (int r = sl; r < s.nefc; r += HL) {
-    T* o = dbg + 3200 + 6 * r;
+    T* o = dbg + 4000 + 6 * r;     // contacts above end at 2600 + 11 * 64
     o[0] = rk_kind(s.row_kid[r]); o[1] = rk_id(s.row_kid[r]); o[2] = s.row_D[r]; o[4] = s.row_f[r];
   }
 }
 
-// per-env commit of state + aux (one half-wave)
-template <typename T, int NV>
-__device__ __forceinline__ void commit(MPtr<T> m, KPtr<T> k, const Stepper<T, NV>& st,
+// per-env commit of state (+ the optional aux row / ctrl copy) for one half-wave
+template <typename T, int NV, typename C>
+__device__ __forceinline__ void commit(MPtr<T> m, KPtr<T> k, const Stepper<T, NV, C>& st,
                        int env, T time, T xws, int step_count, uint32_t episode, T total, const int* warn,
                        bool full) {
-  const Scratch<T>& s = st.s;
+  const Scratch<T, C>& s = st.s;
   const int sl = st.sl, nq = m->nq, nv = m->nv, nu = m->nu;
+  const int outputs = k->p.outputs;
   if (sl < nq) k->b.qpos[(size_t)env * nq + sl] = s.qpos[sl];
   if (sl + HL < nq) k->b.qpos[(size_t)env * nq + sl + HL] = s.qpos[sl + HL];
   if (sl < nv) {
     k->b.qvel[(size_t)env * nv + sl] = s.qvel[sl];
     k->b.qacc_ws[(size_t)env * nv + sl] = xws;
-    k->b.aux[(size_t)env * AUXDIM + sl] = st.qacc;
+    if (outputs & OUT_AUX) k->b.aux[(size_t)env * AUXDIM + sl] = st.qacc;
   }
-  if (sl < nu) k->b.ctrl[(size_t)env * nu + sl] = s.ctrl[sl];
+  if (sl < nu && (outputs & OUT_CTRL)) k->b.ctrl[(size_t)env * nu + sl] = s.ctrl[sl];
   if (sl == 0) {
     k->b.time[env] = time;
     k->b.step_count[env] = step_count;
     k->b.episode[env] = episode;
     k->b.total_reward[env] = total;
-    T* a = k->b.aux + (size_t)env * AUXDIM;
-    a[MAXDOF + 0] = s.com[0]; a[MAXDOF + 1] = s.com[1]; a[MAXDOF + 2] = s.com[2];
-    a[MAXDOF + 3] = (T)s.ncon; a[MAXDOF + 4] = (T)s.nefc; a[MAXDOF + 5] = (T)st.niter;
+    if (outputs & OUT_AUX) {
+      T* a = k->b.aux + (size_t)env * AUXDIM;
+      a[MAXDOF + 0] = s.com[0]; a[MAXDOF + 1] = s.com[1]; a[MAXDOF + 2] = s.com[2];
+      a[MAXDOF + 3] = (T)s.ncon; a[MAXDOF + 4] = (T)s.nefc; a[MAXDOF + 5] = (T)st.niter;
+    }
     for (int w = 0; w < NWARN; w++)   // read-modify-write only when set (a load here would wait for
       if (warn[w]) k->b.warning[(size_t)env * NWARN + w] += warn[w];   // every store issued above)
   }
@@ -1788,56 +1820,69 @@ __device__ __forceinline__ void commit(MPtr<T> m, KPtr<T> k, const Stepper<T, NV
 }
 
 // ------------------------------------------------------------------ the kernel
-template <typename T, int NV, bool PGS = false>
-// 2 waves/SIMD (the VGPR budget of 256) for the fp32 engine; the fp64 parity engine needs more
-// registers and runs at 1.  PGS: the <option solver="PGS"> instance (its own LDS cache).
-__global__ __launch_bounds__(64, (sizeof(T) == 4 && !PGS) ? 2 : 1) void step_kernel(KArgs<T> /* read via kernarg ptr */) {
-  __shared__ Scratch<T> smem[2];
-  PgsCache<T>* pcache = nullptr;
-  if constexpr (PGS) {
-    __shared__ PgsCache<T> pgs_smem[2];
-    pcache = &pgs_smem[threadIdx.x >= HL ? 1 : 0];
-  }
-  const KPtr<T> ka = (KPtr<T>)__builtin_amdgcn_kernarg_segment_ptr();
+// One env step (or reset / raw physics call) of the env pair (index, index + 1) of one wave.
+// `list` (wide tier): indices map to env ids through it; resident tier: indices are env ids.
+// In the resident tier an env whose contacts / rows overflowed the resident capacity in any
+// substep is NOT committed: it is appended to the wide tier's work list instead, and the wide
+// launch that follows re-runs its whole step from the same (untouched) inputs.
+template <typename T, int NV, bool PGS, typename C>
+__device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCache<T, C>* pcache, int idx,
+                                          int nidx, const int* list) {
+  constexpr bool WIDE = C::CON > MAXCON;
   const int lane = threadIdx.x;
   const bool up = lane >= HL;
   const int sl = lane & (HL - 1);
-  const int nenv = ka->nenv;
-  const int env_raw = 2 * blockIdx.x + (up ? 1 : 0);
-  bool active = env_raw < nenv;                       // ghost half for odd N
-  const int env = active ? env_raw : nenv - 1;
+  bool active = idx < nidx;                           // ghost half for an odd count
+  const int ei = active ? idx : nidx - 1;
+  const int env_id = list ? list[ei] : ei;
   const int mode = ka->p.mode;
-  if (mode == MODE_RESET && ka->reset_mask && !ka->reset_mask[env]) active = false;
+  if (mode == MODE_RESET && ka->reset_mask && !ka->reset_mask[env_id]) active = false;
   if (__ballot(active) == 0) return;                  // wave-uniform exit
-  Scratch<T>& s = smem[up ? 1 : 0];
+  Scratch<T, C>& s = smem[up ? 1 : 0];
   MPtr<T> m = ka->m;
   const int nq = m->nq, nv = m->nv, nu = m->nu;
-  Stepper<T, NV> st(m, s, lane);
-  if (ka->b.dbg && env == 0 && active) st.dbg = ka->b.dbg;
+  Stepper<T, NV, C> st(m, s, lane);
+  if (ka->b.dbg && env_id == 0 && active) st.dbg = ka->b.dbg;
   int warn[NWARN] = {0, 0, 0, 0};
   T time, xws;
   int step_count;
   uint32_t episode;
   T total, act;
   {
-    time = ka->b.time[env];
-    xws = (sl < nv) ? ka->b.qacc_ws[(size_t)env * nv + sl] : T(0);
-    if (sl < nq) s.qpos[sl] = ka->b.qpos[(size_t)env * nq + sl];
-    if (sl + HL < nq) s.qpos[sl + HL] = ka->b.qpos[(size_t)env * nq + sl + HL];
-    if (sl < nv) s.qvel[sl] = ka->b.qvel[(size_t)env * nv + sl];
-    if (sl < nu) s.ctrl[sl] = ka->b.ctrl[(size_t)env * nu + sl];
-    step_count = ka->b.step_count[env];
-    episode = ka->b.episode[env];
-    total = ka->b.total_reward[env];
-    // the action is the same for all substeps: one load, issued with the state loads
+    time = ka->b.time[env_id];
+    xws = (sl < nv) ? ka->b.qacc_ws[(size_t)env_id * nv + sl] : T(0);
+    if (sl < nq) s.qpos[sl] = ka->b.qpos[(size_t)env_id * nq + sl];
+    if (sl + HL < nq) s.qpos[sl + HL] = ka->b.qpos[(size_t)env_id * nq + sl + HL];
+    if (sl < nv) s.qvel[sl] = ka->b.qvel[(size_t)env_id * nv + sl];
+    // data.ctrl is an input only to a raw physics call that keeps the current ctrl; env steps set
+    // it from the action, resets zero it
     const float* actions = ka->actions;
-    act = (actions && sl < nu) ? (T)actions[(size_t)env * nu + sl] : T(0);
+    if (sl < nu) s.ctrl[sl] = (mode == MODE_PHYSICS && !actions) ? ka->b.ctrl[(size_t)env_id * nu + sl] : T(0);
+    step_count = ka->b.step_count[env_id];
+    episode = ka->b.episode[env_id];
+    total = ka->b.total_reward[env_id];
+    // the action is the same for all substeps: one load, issued with the state loads
+    act = (actions && sl < nu) ? (T)actions[(size_t)env_id * nu + sl] : T(0);
   }
   WSYNC();
   st.clk.start();
   st.qfa = 0;
   st.qacc = 0;
   st.niter = 0;
+  // resident tier: an overflowing env is deferred to the wide tier instead of committed
+  auto defer = [&](KPtr<T> k) -> bool {
+    if constexpr (WIDE) {
+      return false;
+    } else {
+      if (!k->b.redo || warn[WARN_OVERFLOW] == 0) return false;
+      if (sl == 0) {
+        const int slot = atomicAdd(&k->b.redo[0], 1);
+        k->b.redo[2 + slot] = env_id;
+        atomicAdd(k->b.redo_total, 1ull);
+      }
+      return true;
+    }
+  };
 
   // Both halves always run the same instruction stream; a half that is inactive (ghost env,
   // masked reset) or not resetting while its partner resets computes on scratch but commits
@@ -1855,6 +1900,7 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !PGS) ? 2 : 1) void step_ker
   for (int sub = 0;; sub++) {
     st.m = opaque(st.m);
     st.sl = opaque_v(st.sl);
+    const int env = opaque_v(env_id);   // per-env addresses recomputed at each use, not kept live
     if (sub == nsub && !in_reset) {
       if (nsub > 0) {
         KPtr<T> k = opaque(ka);
@@ -1881,12 +1927,16 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !PGS) ? 2 : 1) void step_ker
           }
           if ((term || trunc) && k->p.autoreset && active) {
             write_obs(st.m, s, sl, st.qfa, k->b.terminal_obs + (size_t)env * obs_dim, obs_dim);
+            // the final step's info (SubprocVecEnv returns the finished episode's step_count /
+            // total_reward before resetting, custom_env.py:216-224)
+            if (sl == 0 && k->b.term_step_count) k->b.term_step_count[env] = step_count;
+            if (sl == 0 && k->b.term_total_reward) k->b.term_total_reward[env] = total;
             do_reset = true;
           }
         }
         if (active && !do_reset) {
-          commit(st.m, k, st, env, time, xws, step_count, episode, total, warn, k->p.full_state != 0);
-          active = false;   // committed; a reset pass below is scratch work for this half
+          if (!defer(k)) commit(st.m, k, st, env, time, xws, step_count, episode, total, warn, k->p.full_state != 0);
+          active = false;   // committed (or deferred); a reset pass below is scratch work for this half
         }
       }
       if (__ballot(do_reset) == 0) break;
@@ -1921,7 +1971,7 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !PGS) ? 2 : 1) void step_ker
         if (k->b.dbg && env == 0) dump_debug(st, k->b.dbg);
         const int obs_dim = k->p.obs_dim;
         write_obs(st.m, s, sl, st.qfa, k->b.obs + (size_t)env * obs_dim, obs_dim);
-        commit(st.m, k, st, env, time, xws, 0, episode, T(0), warn, k->p.full_state != 0);
+        if (!defer(k)) commit(st.m, k, st, env, time, xws, 0, episode, T(0), warn, k->p.full_state != 0);
       }
       break;
     } else {
@@ -1949,19 +1999,56 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !PGS) ? 2 : 1) void step_ker
 #endif
 }
 
+// Resident tier: one wave per env pair, all pairs of the batch in one grid.
+// 2 waves/SIMD (the VGPR budget of 256) for the fp32 engine; the fp64 parity engine needs more
+// registers and runs at 1.  PGS: the <option solver="PGS"> instance (its own LDS cache).
+template <typename T, int NV, bool PGS>
+__global__ __launch_bounds__(64, (sizeof(T) == 4 && !PGS) ? 2 : 1) void step_kernel(KArgs<T> /* read via kernarg ptr */) {
+  __shared__ Scratch<T, Resident> smem[2];
+  PgsCache<T, Resident>* pcache = nullptr;
+  if constexpr (PGS) {
+    __shared__ PgsCache<T, Resident> pgs_smem[2];
+    pcache = &pgs_smem[threadIdx.x >= HL ? 1 : 0];
+  }
+  const KPtr<T> ka = (KPtr<T>)__builtin_amdgcn_kernarg_segment_ptr();
+  step_pair<T, NV, PGS, Resident>(ka, smem, pcache, 2 * blockIdx.x + (threadIdx.x >= HL ? 1 : 0), ka->nenv, nullptr);
+}
+
+// Wide tier: a small grid that strides over the envs the resident launch deferred (usually none:
+// every wave reads the count and leaves), then the last wave out clears the list for the next step.
+template <typename T, int NV, bool PGS>
+__global__ __launch_bounds__(64, 1) void step_kernel_wide(KArgs<T> /* read via kernarg ptr */) {
+  __shared__ Scratch<T, Wide> smem[2];
+  PgsCache<T, Wide>* pcache = nullptr;
+  if constexpr (PGS) {
+    __shared__ PgsCache<T, Wide> pgs_smem[2];
+    pcache = &pgs_smem[threadIdx.x >= HL ? 1 : 0];
+  }
+  const KPtr<T> ka = (KPtr<T>)__builtin_amdgcn_kernarg_segment_ptr();
+  int* redo = ka->b.redo;
+  const int count = redo[0];
+  for (int base = 2 * blockIdx.x; base < count; base += 2 * gridDim.x)
+    step_pair<T, NV, PGS, Wide>(ka, smem, pcache, base + (threadIdx.x >= HL ? 1 : 0), count, redo + 2);
+  __threadfence();
+  if (threadIdx.x == 0 && atomicAdd(&redo[1], 1) == (int)gridDim.x - 1) {   // every wave has read the list
+    redo[0] = 0;
+    redo[1] = 0;
+  }
+}
+
 // mj_kinematics + mj_comPos of ONE state (visualisation / data view, never the step path): one
 // wave, the lower half-wave computes, the upper half duplicates it.  out = [xpos MAXBODY*3]
 // [xmat MAXBODY*9][geom_xpos MAXGEOM*3][geom z-axis MAXGEOM*3][subtree_com[0] 3].
 template <typename T, int NV>
 __global__ __launch_bounds__(64) void kin_kernel(MPtr<T> m, const T* __restrict__ qpos, T* __restrict__ out) {
-  __shared__ Scratch<T> smem[2];
+  __shared__ Scratch<T, Resident> smem[2];
   const int lane = threadIdx.x;
   const bool up = lane >= HL;
   const int sl = lane & (HL - 1);
-  Scratch<T>& s = smem[up ? 1 : 0];
+  Scratch<T, Resident>& s = smem[up ? 1 : 0];
   for (int k = sl; k < m->nq; k += HL) s.qpos[k] = qpos[k];
   WSYNC();
-  Stepper<T, NV> st(m, s, lane);
+  Stepper<T, NV, Resident> st(m, s, lane);
   st.kinematics();
   if (up) return;
   const int nb = m->nbody, ng = m->ngeom;
@@ -1983,28 +2070,32 @@ hipError_t launch_step(const DevModel<T>* dmodel, int nv, const EnvBuffers<T>& b
                        const uint8_t* reset_mask, const T* noise_qpos, const T* noise_qvel,
                        const StepParams& p, int nenv, hipStream_t stream) {
   if (nenv <= 0) return hipSuccess;
-  dim3 grid((nenv + 1) / 2), block(WAVE);
-  switch (nv) {
-    case 27:
-      if (p.solver == SOLVER_PGS)
-        hipLaunchKernelGGL((step_kernel<T, 27, true>), grid, block, 0, stream,
-                           KArgs<T>{(MPtr<T>)dmodel, b, actions, reset_mask, noise_qpos, noise_qvel, p, nenv});
-      else
-        hipLaunchKernelGGL((step_kernel<T, 27>), grid, block, 0, stream,
-                           KArgs<T>{(MPtr<T>)dmodel, b, actions, reset_mask, noise_qpos, noise_qvel, p, nenv});
-      break;
-    default:
-      return hipErrorInvalidValue;
+  if (nv != 27) return hipErrorInvalidValue;
+  const KArgs<T> args{(MPtr<T>)dmodel, b, actions, reset_mask, noise_qpos, noise_qvel, p, nenv};
+  const dim3 grid((nenv + 1) / 2), block(WAVE);
+  // the wide tier's grid: enough waves for a few deferred envs at once, few enough that the
+  // common no-overflow launch (every wave reads the count and exits) costs a few microseconds
+  const dim3 wgrid(std::min((nenv + 1) / 2, 32));
+#ifndef HS_DEV_NEWTON_ONLY   // development builds: resource-usage checks of the Newton instances only
+  if (p.solver == SOLVER_PGS) {
+    hipLaunchKernelGGL((step_kernel<T, 27, true>), grid, block, 0, stream, args);
+    if (b.redo) hipLaunchKernelGGL((step_kernel_wide<T, 27, true>), wgrid, block, 0, stream, args);
+    return hipGetLastError();
   }
+#endif
+  hipLaunchKernelGGL((step_kernel<T, 27, false>), grid, block, 0, stream, args);
+  if (b.redo) hipLaunchKernelGGL((step_kernel_wide<T, 27, false>), wgrid, block, 0, stream, args);
   return hipGetLastError();
 }
 
 template hipError_t launch_step<float>(const DevModel<float>*, int, const EnvBuffers<float>&, const float*,
                                        const uint8_t*, const float*, const float*, const StepParams&, int,
                                        hipStream_t);
+#ifndef HS_DEV_F32_ONLY
 template hipError_t launch_step<double>(const DevModel<double>*, int, const EnvBuffers<double>&, const float*,
                                         const uint8_t*, const double*, const double*, const StepParams&, int,
                                         hipStream_t);
+#endif
 
 template <typename T>
 hipError_t launch_kinematics(const DevModel<T>* dmodel, int nv, const T* qpos, T* out, hipStream_t stream) {

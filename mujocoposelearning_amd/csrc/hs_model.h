@@ -21,8 +21,17 @@ constexpr int MAXTEN = 4;
 constexpr int MAXWRAP = 4;    // joints per fixed tendon
 constexpr int MAXU = 24;
 constexpr int MAXPAIR = 192;  // static candidate geom pairs
-constexpr int MAXCON = 32;    // contacts per env (one half-wave lane each; overflow -> warning word)
-constexpr int MAXEFC = 128;   // constraint rows per env (4 per half-wave lane)
+// Contact / constraint-row capacity per env comes in two tiers (hs_kernels.hip):
+//  * resident tier: what every launch runs with, sized so all 4096 envs of configs[1] stay
+//    resident (LDS) -- 2.3x / 2.5x the worst full-episode counts measured on the oracle
+//    (14 contacts, 52 rows over 48 episodes x tapes T0/T1/T2);
+//  * wide tier: an env whose contacts or rows overflow the resident tier in any substep is not
+//    committed; a second (small-grid) launch re-runs that env's whole step from the same inputs
+//    with this capacity.  Only overflow of the wide tier drops contacts (warning word).
+constexpr int MAXCON = 32;    // resident tier: contacts per env (one half-wave lane each)
+constexpr int MAXEFC = 128;   // resident tier: constraint rows per env (4 per half-wave lane)
+constexpr int MAXCON_WIDE = 64;    // wide tier (2 contacts per lane)
+constexpr int MAXEFC_WIDE = 256;   // wide tier (8 rows per lane)
 constexpr int MAXLEVEL = 16;
 constexpr int MAXJPB = 3;     // hinge joints per body (kinematics keeps their rotations in registers)
 // solimp on the device: MuJoCo's (d0, dwidth, width, midpoint, power) followed by derived constants

@@ -223,6 +223,20 @@ struct Compiler {
   std::map<std::string, int> jnt_by_name, body_by_name;
   Compiler(HostModel& mm, std::string& e) : m(mm), err(e) {}
 
+  // exactly n numbers in attribute text s (what = the attribute, for the message)
+  bool numsn(const char* s, size_t n, const char* what, std::vector<double>& v) {
+    v = nums(s);
+    if (v.size() == n) return true;
+    err = std::string("attribute '") + what + "' needs " + std::to_string(n) + " number(s), got '" + (s ? s : "") + "'";
+    return false;
+  }
+  bool num1(const char* s, const char* what, double& x) {
+    std::vector<double> v;
+    if (!numsn(s, 1, what, v)) return false;
+    x = v[0];
+    return true;
+  }
+
   void parse_defaults(const XNode* n, const DefClass* parent) {
     DefClass d = parent ? *parent : DefClass();
     for (auto& k : n->kids)
@@ -275,10 +289,15 @@ struct Compiler {
     } else {
       auto p = getv(a, "pos", {0, 0, 0});
       for (int k = 0; k < 3; k++) pos[k] = p[k];
-      if (a.count("zaxis")) { auto z = nums(a["zaxis"].c_str()); quat_z2vec(quat, z.data()); }
+      std::vector<double> z, q;
+      if (a.count("zaxis")) {
+        if (!numsn(a["zaxis"].c_str(), 3, "zaxis", z)) return false;
+        quat_z2vec(quat, z.data());
+      }
       if (a.count("quat")) {
-        auto q = nums(a["quat"].c_str());
+        if (!numsn(a["quat"].c_str(), 4, "quat", q)) return false;
         double nq = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+        if (!(nq > 0)) { err = "zero geom quat"; return false; }
         for (int k = 0; k < 4; k++) quat[k] = q[k] / nq;
       }
     }
@@ -364,13 +383,16 @@ struct Compiler {
       if (k->get("name")) body_by_name[k->get("name")] = id;
       m.body_name.push_back(k->get("name") ? k->get("name") : "");
       m.body_parentid.push_back(parent);
-      auto p = nums(k->get("pos") ? k->get("pos") : "0 0 0");
-      auto q = nums(k->get("quat") ? k->get("quat") : "1 0 0 0");
+      std::vector<double> p, q;
+      if (!numsn(k->get("pos") ? k->get("pos") : "0 0 0", 3, "pos", p) ||
+          !numsn(k->get("quat") ? k->get("quat") : "1 0 0 0", 4, "quat", q))
+        return false;
       if (k->get("euler") || k->get("axisangle") || k->get("xyaxes") || k->get("zaxis")) {
         err = "body orientation specifiers other than quat are not supported";
         return false;
       }
       double qn = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+      if (!(qn > 0)) { err = "zero body quat"; return false; }
       for (int j = 0; j < 3; j++) m.body_pos.push_back(p[j]);
       for (int j = 0; j < 4; j++) m.body_quat.push_back(q[j] / qn);
       std::string ccls = k->get("childclass") ? k->get("childclass") : cls;
@@ -387,14 +409,18 @@ struct Compiler {
   // <option>: timestep, gravity, iterations, tolerance are honoured; anything that changes the
   // dynamics in a way the engine does not implement is rejected (never silently ignored).
   bool parse_option(const XNode* k) {
-    if (k->get("timestep")) m.timestep = nums(k->get("timestep"))[0];
+    if (k->get("timestep") && !num1(k->get("timestep"), "timestep", m.timestep)) return false;
+    if (!(m.timestep > 0)) { err = "<option timestep> must be > 0"; return false; }
     if (k->get("gravity")) {
       auto g = nums(k->get("gravity"));
       if (g.size() != 3) { err = "<option gravity> needs 3 numbers"; return false; }
       for (int j = 0; j < 3; j++) m.gravity[j] = g[j];
     }
-    if (k->get("iterations")) m.iterations = (int)nums(k->get("iterations"))[0];
-    if (k->get("tolerance")) m.tolerance = nums(k->get("tolerance"))[0];
+    double it = m.iterations;
+    if (k->get("iterations") && !num1(k->get("iterations"), "iterations", it)) return false;
+    if (!(it >= 1 && it <= 1e6)) { err = "<option iterations> must be in [1, 1e6]"; return false; }
+    m.iterations = (int)it;
+    if (k->get("tolerance") && !num1(k->get("tolerance"), "tolerance", m.tolerance)) return false;
     auto is = [&](const char* a, const char* dflt) { return !k->get(a) || std::string(k->get(a)) == dflt; };
     auto zero = [&](const char* a) {
       if (!k->get(a)) return true;
@@ -409,7 +435,9 @@ struct Compiler {
     }
     if (!is("integrator", "Euler")) { err = "only integrator=\"Euler\" is supported (reference: MuJoCo default)"; return false; }
     if (!is("cone", "pyramidal")) { err = "only cone=\"pyramidal\" is supported"; return false; }
-    if (k->get("impratio") && nums(k->get("impratio"))[0] != 1.0) { err = "only impratio=1 is supported"; return false; }
+    double impratio = 1.0;
+    if (k->get("impratio") && !num1(k->get("impratio"), "impratio", impratio)) return false;
+    if (impratio != 1.0) { err = "only impratio=1 is supported"; return false; }
     if (!zero("noslip_iterations")) { err = "noslip solver not supported"; return false; }
     if (!zero("density") || !zero("viscosity")) { err = "fluid forces (density/viscosity) not supported"; return false; }
     for (auto& f : k->kids)
@@ -587,7 +615,9 @@ bool Compiler::finish(const XNode* root) {
           auto it = jnt_by_name.find(w->get("joint") ? w->get("joint") : "");
           if (it == jnt_by_name.end()) { err = "tendon joint not found"; return false; }
           m.wrap_jnt.push_back(it->second);
-          m.wrap_coef.push_back(w->get("coef") ? nums(w->get("coef"))[0] : 1.0);
+          double coef = 1.0;
+          if (w->get("coef") && !num1(w->get("coef"), "coef", coef)) return false;
+          m.wrap_coef.push_back(coef);
           nw++;
         }
         m.tendon_num.push_back(nw);
@@ -622,15 +652,21 @@ bool Compiler::finish(const XNode* root) {
     if (k->tag == "contact") {
       for (auto& e : k->kids) {
         if (e->tag != "exclude") continue;
-        int b1 = body_by_name.count(e->get("body1")) ? body_by_name[e->get("body1")] : -1;
-        int b2 = body_by_name.count(e->get("body2")) ? body_by_name[e->get("body2")] : -1;
+        const char* n1 = e->get("body1");
+        const char* n2 = e->get("body2");
+        int b1 = n1 && body_by_name.count(n1) ? body_by_name[n1] : -1;
+        int b2 = n2 && body_by_name.count(n2) ? body_by_name[n2] : -1;
         if (b1 < 0 || b2 < 0) { err = "exclude body not found"; return false; }
         m.exclude.emplace_back(std::min(b1, b2), std::max(b1, b2));
       }
     }
     if (k->tag == "keyframe")
       for (auto& e : k->kids)
-        if (e->get("qpos")) m.keyframes[e->get("name") ? e->get("name") : ""] = nums(e->get("qpos"));
+        if (e->get("qpos")) {
+          std::vector<double> kq;
+          if (!numsn(e->get("qpos"), (size_t)m.nq, "key qpos", kq)) return false;
+          m.keyframes[e->get("name") ? e->get("name") : ""] = kq;
+        }
   }
   m.ntendon = (int)m.tendon_adr.size();
   m.nu = (int)m.actuator_trnid.size();

@@ -27,6 +27,8 @@
 // launch shape and reproducible from (seed, counter).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <cstdint>
 
 namespace hs {
@@ -341,7 +343,7 @@ __global__ __launch_bounds__(256) void ppo_loss_bwd_kernel(const float* __restri
 }
 
 // clip_grad_norm_(max_norm) + Adam (torch.optim.Adam, capturable/fused formula) over up to
-// ADAM_MAXT parameter tensors in three launches (torch: a multi-tensor norm, stack, norm, clamp,
+// ADAM_MAXT parameter tensors per chunk in three launches (torch: a multi-tensor norm, stack, norm, clamp,
 // foreach mul and the fused Adam kernel):
 //   adam_sqsum   per-block sums of g^2 over the concatenated gradients (fixed order)
 //   adam_update  every block reduces those partials (same order) to the clip coefficient
@@ -351,6 +353,7 @@ __global__ __launch_bounds__(256) void ppo_loss_bwd_kernel(const float* __restri
 //   adam_step    step[i] = t for every tensor (after all blocks have read the old step)
 // All tensors take the same number of steps (one optimizer), so tensor 0's step is the clock.
 constexpr int ADAM_MAXT = 16, ADAM_TPB = 256, ADAM_PER = 4;
+constexpr int ADAM_MAXCHUNK = 64;   // launch_adam_clip handles up to ADAM_MAXT * ADAM_MAXCHUNK tensors
 
 struct AdamArgs {
   float* p[ADAM_MAXT];
@@ -663,31 +666,48 @@ hipError_t launch_ppo_loss_bwd(const float* logp, const float* v, int B, float c
   return hipGetLastError();
 }
 
+// partial sums of the squared-gradient pass: one per ADAM_TPB * ADAM_PER elements of each chunk of
+// ADAM_MAXT tensors (the per-chunk rounding adds at most one partial per chunk)
 int adam_partials(long long total) {
-  return (int)((total + (long long)ADAM_TPB * ADAM_PER - 1) / ((long long)ADAM_TPB * ADAM_PER));
+  return (int)((total + (long long)ADAM_TPB * ADAM_PER - 1) / ((long long)ADAM_TPB * ADAM_PER)) + ADAM_MAXCHUNK;
 }
 
+// Any number of tensors (<= ADAM_MAXT * ADAM_MAXCHUNK): chunks of ADAM_MAXT share one partials
+// array, so every update block reduces the partials of ALL chunks to the same clip coefficient;
+// the step counters advance after every chunk's update has read them.
 hipError_t launch_adam_clip(int nt, float* const* p, const float* const* g, float* const* m, float* const* v,
                             float* const* step, const long long* numel, float* part, float max_norm, double lr,
                             double b1, double b2, double eps, hipStream_t stream) {
-  if (nt <= 0 || nt > ADAM_MAXT) return hipErrorInvalidValue;
-  AdamArgs a{};
-  a.nt = nt;
-  a.start[0] = 0;
-  for (int t = 0; t < nt; t++) {
-    a.p[t] = p[t];
-    a.g[t] = g[t];
-    a.m[t] = m[t];
-    a.v[t] = v[t];
-    a.step[t] = step[t];
-    a.start[t + 1] = a.start[t] + numel[t];
+  if (nt <= 0 || nt > ADAM_MAXT * ADAM_MAXCHUNK) return hipErrorInvalidValue;
+  const int nchunk = (nt + ADAM_MAXT - 1) / ADAM_MAXT;
+  AdamArgs a[ADAM_MAXCHUNK];
+  int nblk[ADAM_MAXCHUNK], off[ADAM_MAXCHUNK + 1];
+  off[0] = 0;
+  for (int c = 0; c < nchunk; c++) {
+    a[c] = AdamArgs{};
+    a[c].nt = std::min(ADAM_MAXT, nt - c * ADAM_MAXT);
+    a[c].start[0] = 0;
+    for (int j = 0; j < a[c].nt; j++) {
+      const int t = c * ADAM_MAXT + j;
+      a[c].p[j] = p[t];
+      a[c].g[j] = g[t];
+      a[c].m[j] = m[t];
+      a[c].v[j] = v[t];
+      a[c].step[j] = step[t];
+      a[c].start[j + 1] = a[c].start[j] + numel[t];
+    }
+    nblk[c] = (int)((a[c].start[a[c].nt] + (long long)ADAM_TPB * ADAM_PER - 1) / ((long long)ADAM_TPB * ADAM_PER));
+    off[c + 1] = off[c] + nblk[c];
   }
-  const int nblk = adam_partials(a.start[nt]);
-  if (nblk <= 0) return hipSuccess;
-  hipLaunchKernelGGL(adam_sqsum_kernel, dim3(nblk), dim3(ADAM_TPB), 0, stream, a, part);
-  hipLaunchKernelGGL(adam_update_kernel, dim3(nblk), dim3(ADAM_TPB), 0, stream, a, (const float*)part, nblk,
-                     max_norm, (float)lr, (float)b1, (float)b2, (float)(1.0 - b1), (float)(1.0 - b2), (float)eps);
-  hipLaunchKernelGGL(adam_step_kernel, dim3(1), dim3(64), 0, stream, a);
+  if (off[nchunk] <= 0) return hipSuccess;
+  for (int c = 0; c < nchunk; c++)
+    if (nblk[c]) hipLaunchKernelGGL(adam_sqsum_kernel, dim3(nblk[c]), dim3(ADAM_TPB), 0, stream, a[c], part + off[c]);
+  for (int c = 0; c < nchunk; c++)
+    if (nblk[c])
+      hipLaunchKernelGGL(adam_update_kernel, dim3(nblk[c]), dim3(ADAM_TPB), 0, stream, a[c], (const float*)part,
+                         off[nchunk], max_norm, (float)lr, (float)b1, (float)b2, (float)(1.0 - b1), (float)(1.0 - b2),
+                         (float)eps);
+  for (int c = 0; c < nchunk; c++) hipLaunchKernelGGL(adam_step_kernel, dim3(1), dim3(64), 0, stream, a[c]);
   return hipGetLastError();
 }
 

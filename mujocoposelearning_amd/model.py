@@ -7,6 +7,7 @@ the C ABI's ``hs_model_field``.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -18,6 +19,11 @@ _SHAPES = {"body_pos": 3, "body_quat": 4, "body_ipos": 3, "body_iquat": 4, "body
            "jnt_solref": 2, "jnt_solimp": 5, "geom_size": 3, "geom_pos": 3, "geom_quat": 4,
            "geom_friction": 3, "geom_solref": 2, "geom_solimp": 5, "tendon_range": 2, "actuator_ctrlrange": 2,
            "collision_pairs": 2}
+
+
+# the reference's model (XML/humanoid.xml, loaded at custom_env.py:53 / train_sb3.py:183-186),
+# shipped as package data
+HUMANOID_XML = os.path.join(os.path.dirname(os.path.abspath(__file__)), "assets", "humanoid.xml")
 
 
 class HsModel:

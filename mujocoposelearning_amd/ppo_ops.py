@@ -138,7 +138,7 @@ def adam_clip_step(opt, params, max_norm, workspace=None):
     from . import _lib
     grp = opt.param_groups[0]
     assert len(opt.param_groups) == 1 and not grp.get("amsgrad") and not grp.get("weight_decay")
-    assert not grp.get("maximize") and len(params) <= 16
+    assert not grp.get("maximize") and len(params) <= 1024
     dev = params[0].device
     for p in params:
         st = opt.state[p]

@@ -19,8 +19,7 @@ import torch
 from .ppo import PPO
 from .vec_env import HumanoidVecEnv
 
-DEFAULT_XML = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
-                           "humanoid.xml")
+from .model import HUMANOID_XML as DEFAULT_XML   # noqa: E402  (the reference's XML/humanoid.xml)
 
 
 def shard_envs(n_envs: int, world_size: int, rank: int):
@@ -56,7 +55,7 @@ def _resolve_activation(ppo_kwargs: dict) -> dict:
 
 
 def train_humanoid(env_kwargs: dict, ppo_kwargs: dict, xml_path: str = DEFAULT_XML, storage_path=None,
-                   precision: str = "fp32", seed: int = 0, callback=None):
+                   precision: str = "fp64", seed: int = 0, callback=None):
     import torch.distributed as dist
     world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
@@ -65,6 +64,8 @@ def train_humanoid(env_kwargs: dict, ppo_kwargs: dict, xml_path: str = DEFAULT_X
     start, stop = shard_envs(n_total, world, rank)
     env = HumanoidVecEnv(env_config_from_kwargs(env_kwargs, xml_path), n_envs=stop - start, device=local_rank,
                          precision=precision, seed=seed * 1_000_003 + start)
+    if env.graph_safe:     # device reward: the trainer reads neither the aux row nor the ctrl copy
+        env.batch.configure(aux=False, ctrl=False)
     kw = _resolve_activation(ppo_kwargs)
     model = PPO(env, seed=seed, world_size=world, rank=rank, **kw)
     model.learn(total_timesteps=env_kwargs.get("total_timesteps", 20_000_000), callback=callback)

@@ -12,8 +12,11 @@ Two surfaces:
 * Device fast path ``step_tensors(actions)`` / ``reset_tensors()`` returning torch tensors
   that never leave HBM (used by the on-device PPO trainer and bench.py).
 
-Auto-reset noise comes from an on-device counter RNG (seed, env, episode) instead of numpy's
-global MT19937 (the per-env HumanoidEnv keeps the exact numpy stream).
+Reset noise: unseeded, it comes from an on-device counter RNG (seed, env, episode).  After
+``seed(s)`` (what SB3's ``PPO(seed=s)`` calls) every env i draws its resets -- the explicit
+``reset()`` and every auto-reset -- from its own legacy MT19937 stream ``np.random.seed(s + i)``,
+exactly as SubprocVecEnv worker i does (custom_env.py:99-110; SB3 VecEnv.seed gives worker i
+seed + i and the worker's global numpy stream continues across auto-resets).
 """
 from __future__ import annotations
 
@@ -44,10 +47,23 @@ except ImportError:
 
 
 class HumanoidVecEnv(_Base):
-    def __init__(self, env_config, n_envs=8, device=0, precision="fp32", seed=0, model=None, max_newton=None,
+    def __init__(self, env_config, n_envs=None, device=0, precision="fp32", seed=0, model=None, max_newton=None,
                  groups="auto"):
-        if callable(env_config):            # SB3 style list of env_fns is not meaningful on device
-            raise TypeError("pass the env_config dict (train_sb3.py:183-200), not env factories")
+        """``env_config``: the env_config dict (train_sb3.py:183-200), a model path, or SB3's
+        ``[make_env(env_config, i) for i in range(n)]`` list of factories (train_sb3.py:203): all
+        envs of one rank share one config, recovered from the first factory, and ``n_envs``
+        defaults to the list length."""
+        if isinstance(env_config, (list, tuple)):
+            if not env_config or not all(callable(f) for f in env_config):
+                raise TypeError("env_fns must be a non-empty list of env factories")
+            if n_envs is not None and n_envs != len(env_config):
+                raise ValueError(f"n_envs={n_envs} but {len(env_config)} env factories")
+            n_envs = len(env_config)
+            env_config = _config_of_factory(env_config[0])
+        elif callable(env_config):
+            env_config = _config_of_factory(env_config)
+        if n_envs is None:
+            n_envs = 8                      # train_sb3.py's env_kwargs.get('n_envs', 8)
         cfg = env_config if isinstance(env_config, dict) else {"model_path": env_config}
         self.env_config = dict(cfg)
         self.model = model if model is not None else HsModel(cfg["model_path"])
@@ -77,6 +93,8 @@ class HumanoidVecEnv(_Base):
         super().__init__(n_envs, obs_space, act_space)
         self._actions = None
         self._seed = seed
+        self._seeds = None          # pending SB3 seeds (applied by the next reset)
+        self._streams = None        # per-env np.random.RandomState once seeded (host noise mode)
         self.render_mode = None
 
     # ---------------------------------------------------------------- device fast path
@@ -106,7 +124,17 @@ class HumanoidVecEnv(_Base):
         return self.batch.terminal_obs
 
     def reset_tensors(self):
-        return self.batch.reset()
+        """reset() on the device: returns the [N, obs_dim] device obs tensor."""
+        if self._seeds is not None:      # SB3: worker i runs env.reset(seed=seed + i) -> np.random.seed
+            self._streams = [np.random.RandomState(s) for s in self._seeds]
+            self._seeds = None
+        if self._streams is None:
+            return self.batch.reset()
+        qn, vn = self._draw_noise(range(self.num_envs))
+        obs = self.batch.reset(qpos_noise=qn, qvel_noise=vn)
+        if self._host_reward is None:    # device auto-reset reads the pre-drawn next noise
+            self._bind_next_noise()
+        return obs
 
     def step_tensors(self, actions):
         """actions: [N, nu] float32 tensor on the env's GPU (clipped to [-1, 1] by the caller, as
@@ -114,7 +142,10 @@ class HumanoidVecEnv(_Base):
         call; ``self.batch.terminal_obs`` holds pre-reset obs of envs that just finished."""
         if self._host_reward is not None:
             return self._step_host_reward(actions)
-        return self.batch.step(actions)
+        out = self.batch.step(actions)
+        if self._streams is not None:     # host noise streams: refresh the envs that auto-reset (syncs)
+            self._refresh_noise(((out[2] != 0) | (out[3] != 0)).cpu().numpy())
+        return out
 
     def _step_host_reward(self, actions):
         """custom_env.py:201-211 with a host reward callable: step (no auto-reset), evaluate
@@ -134,13 +165,46 @@ class HumanoidVecEnv(_Base):
         done = (term != 0) | (trunc != 0)
         if bool(done.any()):
             b.terminal_obs[done] = obs[done]
-            b.reset(mask=done.to(torch.uint8))
+            b.terminal_step_count[done] = b.step_count[done]
+            b.terminal_total_reward[done] = b.total_reward[done]
+            if self._streams is None:
+                b.reset(mask=done.to(torch.uint8))
+            else:
+                qn, vn = self._draw_noise(np.flatnonzero(done.cpu().numpy()))
+                b.reset(mask=done.to(torch.uint8), qpos_noise=qn, qvel_noise=vn)
         return b.obs, rew, term, trunc
 
     # ---------------------------------------------------------------- SB3 VecEnv API
     def reset(self):
-        obs = self.batch.reset()
-        return obs.double().cpu().numpy()
+        return self.reset_tensors().double().cpu().numpy()
+
+    # ---------------------------------------------------------------- host reset-noise streams
+    def _draw_noise(self, envs):
+        """The next reset's raw noise of each env in ``envs`` from its own stream, in
+        custom_env.py:109-110's draw order (qpos then qvel); rows of other envs are zero."""
+        m = self.model
+        qn, vn = np.zeros((self.num_envs, m.nq)), np.zeros((self.num_envs, m.nv))
+        for i in envs:
+            r = self._streams[i]
+            qn[i] = r.uniform(low=-0.01, high=0.01, size=m.nq)
+            vn[i] = r.uniform(low=-0.01, high=0.01, size=m.nv)
+        return qn, vn
+
+    def _bind_next_noise(self):
+        """Pre-draw every env's next (auto-)reset noise and bind it to the step kernel."""
+        qn, vn = self._draw_noise(range(self.num_envs))
+        self._next_noise = self.batch.set_autoreset_noise(qn, vn)
+
+    def _refresh_noise(self, done):
+        """Envs that just auto-reset consumed their bound noise: draw their next one."""
+        import torch
+        idx = np.flatnonzero(done)
+        if self._streams is None or idx.size == 0:
+            return
+        qn, vn = self._draw_noise(idx)
+        t = torch.as_tensor(idx, device=self.batch.device)
+        self._next_noise[0][t] = torch.as_tensor(qn[idx], device=self.batch.device, dtype=self.batch.dtype)
+        self._next_noise[1][t] = torch.as_tensor(vn[idx], device=self.batch.device, dtype=self.batch.dtype)
 
     def step_async(self, actions):
         self._actions = np.asarray(actions, dtype=np.float32).reshape(self.num_envs, -1)
@@ -157,7 +221,15 @@ class HumanoidVecEnv(_Base):
         dones = term_np | trunc_np
         tot = self.batch.total_reward.double().cpu().numpy()
         step_count = self.batch.step_count.cpu().numpy()
-        term_obs = self.batch.terminal_obs.double().cpu().numpy() if dones.any() else None
+        term_obs = None
+        if dones.any():
+            # the finished episodes' final info (SubprocVecEnv returns the last step's info before
+            # the worker resets: step_count 667 / 750, the episode's total_reward; custom_env.py:216-224)
+            term_obs = self.batch.terminal_obs.double().cpu().numpy()
+            tsc = self.batch.terminal_step_count.cpu().numpy()
+            ttr = self.batch.terminal_total_reward.double().cpu().numpy()
+            step_count = np.where(dones, tsc, step_count)
+            tot = np.where(dones, ttr, tot)
         infos = []
         for i in range(self.num_envs):
             info = {"height": None, "step_count": int(step_count[i]), "truncated": bool(trunc_np[i]),
@@ -176,10 +248,16 @@ class HumanoidVecEnv(_Base):
         self.batch.close()
 
     def seed(self, seed=None):
-        """Re-seeds the on-device reset RNG (affects subsequent resets / auto-resets)."""
-        self._seed = 0 if seed is None else int(seed)
+        """SB3 VecEnv.seed: env i gets seed + i, applied at the next ``reset()``; from then on every
+        reset and auto-reset of env i draws its noise from np.random.RandomState(seed + i), as
+        SubprocVecEnv worker i's global numpy stream does (custom_env.py:99-110).  Also re-seeds
+        the on-device RNG (used when no host streams are active)."""
+        if seed is None:
+            seed = int(np.random.randint(0, np.iinfo(np.uint32).max, dtype=np.uint32))
+        self._seed = int(seed)
         self.batch.set_seed(self._seed)
-        return [self._seed + i for i in range(self.num_envs)]
+        self._seeds = [self._seed + i for i in range(self.num_envs)]
+        return list(self._seeds)
 
     def get_attr(self, attr_name, indices=None):
         idx = self._indices(indices)
@@ -218,6 +296,23 @@ class HumanoidVecEnv(_Base):
         if isinstance(indices, int):
             return [indices]
         return indices
+
+
+def _config_of_factory(fn):
+    """env_config of an SB3 env factory: ``make_env(env_config, rank)`` returns a closure over the
+    config dict (train_sb3.py:108-115), read from the closure cells; otherwise the factory is
+    called once and its env's ``env_config`` read."""
+    for cell in getattr(fn, "__closure__", None) or ():
+        v = cell.cell_contents
+        if isinstance(v, dict) and "model_path" in v:
+            return v
+    env = fn()
+    cfg = getattr(env, "env_config", None)
+    if hasattr(env, "close"):
+        env.close()
+    if not isinstance(cfg, dict):
+        raise TypeError("cannot recover env_config from the env factory")
+    return cfg
 
 
 class _HostViews:

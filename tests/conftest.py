@@ -7,7 +7,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-XML = os.path.join(ROOT, "tests", "golden", "humanoid.xml")
+XML = os.path.join(ROOT, "mujocoposelearning_amd", "assets", "humanoid.xml")
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 

@@ -7,7 +7,8 @@ they are imported from /root/reference and evaluated on a duck-typed ``env_data`
 ``tests/golden/reward_golden.npz``; no reference source is copied.
 
 Also writes ``reset_noise_golden.npz``: the legacy-MT19937 reset noise stream of
-custom_env.py:99-117 for seeds 0..4 (pos noise drawn before vel noise).
+custom_env.py:99-117 for seeds 0..4 (pos noise drawn before vel noise), and three consecutive
+resets of SubprocVecEnv workers 0..3 after VecEnv.seed(100) (seeds 100..103).
 """
 import os
 import sys
@@ -78,6 +79,13 @@ def main():
         np.random.seed(s)
         noise[f"pos_{s}"] = np.random.uniform(low=-0.01, high=0.01, size=28)
         noise[f"vel_{s}"] = np.random.uniform(low=-0.01, high=0.01, size=27)
+    # SubprocVecEnv worker streams after VecEnv.seed(100): worker i reset(seed=100 + i), then two
+    # auto-resets (reset(seed=None)) continuing the worker's global stream (custom_env.py:99-110)
+    for i in range(4):
+        np.random.seed(100 + i)
+        for k in range(3):
+            noise[f"stream_pos_{100 + i}_{k}"] = np.random.uniform(low=-0.01, high=0.01, size=28)
+            noise[f"stream_vel_{100 + i}_{k}"] = np.random.uniform(low=-0.01, high=0.01, size=27)
     np.savez(os.path.join(OUT, "reset_noise_golden.npz"), **noise)
     print("wrote", len(cases), "reward cases")
 

@@ -14,7 +14,7 @@ from mujocoposelearning_amd.model import HsModel  # noqa: E402
 from mujocoposelearning_amd.ppo import PPO  # noqa: E402
 from mujocoposelearning_amd.vec_env import HumanoidVecEnv  # noqa: E402
 
-XML = os.path.join(ROOT, "tests", "golden", "humanoid.xml")
+XML = os.path.join(ROOT, "mujocoposelearning_amd", "assets", "humanoid.xml")
 
 
 def main(iters=400, reward="stand"):

@@ -12,7 +12,7 @@ import torch  # noqa: E402
 from mujocoposelearning_amd.model import HsModel  # noqa: E402
 from mujocoposelearning_amd.vec_env import HumanoidVecEnv  # noqa: E402
 
-XML = os.path.join(ROOT, "tests", "golden", "humanoid.xml")
+XML = os.path.join(ROOT, "mujocoposelearning_amd", "assets", "humanoid.xml")
 
 
 def rate(xml, n=4096, steps=40):

@@ -13,7 +13,7 @@ from mujocoposelearning_amd.batch import HsBatch  # noqa: E402
 from mujocoposelearning_amd.model import HsModel  # noqa: E402
 from oracle.oracle import Oracle  # noqa: E402
 
-XML = os.path.join(ROOT, "tests", "golden", "humanoid.xml")
+XML = os.path.join(ROOT, "mujocoposelearning_amd", "assets", "humanoid.xml")
 
 
 def throughput(n, steps=50, prec="fp32"):

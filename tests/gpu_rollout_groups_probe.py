@@ -13,7 +13,7 @@ from mujocoposelearning_amd.model import HsModel  # noqa: E402
 from mujocoposelearning_amd.ppo import ActorCritic, ppo_act  # noqa: E402
 from mujocoposelearning_amd.vec_env import HumanoidVecEnv  # noqa: E402
 
-XML = os.path.join(ROOT, "tests", "golden", "humanoid.xml")
+XML = os.path.join(ROOT, "mujocoposelearning_amd", "assets", "humanoid.xml")
 
 
 def run(G, n=4096, steps=60):

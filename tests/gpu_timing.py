@@ -20,7 +20,7 @@ NS = len(NAMES)
 
 
 def main(n=4096, steps=20, prec="fp32"):
-    model = HsModel(os.path.join(ROOT, "tests", "golden", "humanoid.xml"))
+    model = HsModel(os.path.join(ROOT, "mujocoposelearning_amd", "assets", "humanoid.xml"))
     b = HsBatch(model, n, precision=prec, seed=1)
     b.configure(frame_skip=3, duration=10.0, reward_id=0)
     b.reset()
@@ -63,7 +63,7 @@ def main(n=4096, steps=20, prec="fp32"):
 def predict(n=4096, steps=60, prec="fp32"):
     """Is per-env Newton work predictable from the previous env step?  (timing build: dbg[11100+env]
     = Newton iterations of env summed over the launch's substeps)"""
-    model = HsModel(os.path.join(ROOT, "tests", "golden", "humanoid.xml"))
+    model = HsModel(os.path.join(ROOT, "mujocoposelearning_amd", "assets", "humanoid.xml"))
     b = HsBatch(model, n, precision=prec, seed=1)
     b.configure(frame_skip=3, duration=10.0, reward_id=0)
     b.reset()

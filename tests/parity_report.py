@@ -18,7 +18,7 @@ from mujocoposelearning_amd.batch import HsBatch  # noqa: E402
 from mujocoposelearning_amd.model import HsModel  # noqa: E402
 from oracle.oracle import Oracle  # noqa: E402
 
-XML = os.path.join(ROOT, "tests", "golden", "humanoid.xml")
+XML = os.path.join(ROOT, "mujocoposelearning_amd", "assets", "humanoid.xml")
 NSUB, EVERY = 1000, 100
 
 

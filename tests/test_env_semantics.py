@@ -96,3 +96,14 @@ def test_stand_reward_foot_term_constant():
     expect = 0.4 * np.exp(-2 * (v[0] - 1) ** 2) + 0.3 * (0.5 * np.exp(-2 * (q[2] - 1.282) ** 2) +
                                                           0.5 * np.exp(-3 * (roll ** 2 + pitch ** 2))) + 0.2 + 0.1
     assert r == pytest.approx(expect, rel=1e-12)
+
+
+def test_worker_reset_streams_golden():
+    """SubprocVecEnv workers after VecEnv.seed(100): worker i's resets draw consecutive (28, 27)
+    blocks of np.random.RandomState(100 + i) -- what HumanoidVecEnv's seeded host streams replay."""
+    g = np.load(os.path.join(GOLDEN, "reset_noise_golden.npz"))
+    for i in range(4):
+        r = np.random.RandomState(100 + i)
+        for k in range(3):
+            assert np.array_equal(r.uniform(low=-0.01, high=0.01, size=28), g[f"stream_pos_{100 + i}_{k}"])
+            assert np.array_equal(r.uniform(low=-0.01, high=0.01, size=27), g[f"stream_vel_{100 + i}_{k}"])

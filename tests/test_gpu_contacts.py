@@ -1,0 +1,181 @@
+"""Contact capacity: the resident kernel tier (32 contacts / 128 rows per env) and the wide tier
+(64 / 256) that re-runs the envs overflowing it (hs_model.h).
+
+A humanoid lying pressed into the floor has up to ~44 contacts / ~150 constraint rows
+(humanoid.xml:105-184: 16 capsules x 2 + 3 spheres against the condim-3 floor, plus limits).
+MuJoCo has no per-env cap, so such states must be solved with every contact:
+  * fp64 one substep on contact-rich lying states == the fp64 oracle (ncon, nefc exactly; qacc
+    <= 1e-8 * scale, qpos <= 1e-12) -- the same bounds as tests/test_gpu_parity.py;
+  * the envs that fit the resident tier give bit-identical results whether or not overflowing
+    envs share their batch (the deferral touches nothing else);
+  * env-step mode: a lying env that terminates in the step is re-run by the wide tier through the
+    auto-reset, with host-bound reset noise -- terminal obs, reward, final info and the fresh obs
+    match the oracle env;
+  * full 667-step episodes of 4096 envs on tapes T0 (zeros) and T1 (U(-1,1)): no contact is
+    ever dropped (warning word HS_WARN_OVERFLOW == 0 for every env).
+"""
+import numpy as np
+import pytest
+
+from conftest import XML
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def model():
+    from mujocoposelearning_amd.model import HsModel
+    return HsModel(XML)
+
+
+def _qaxis(axis, ang):
+    axis = np.asarray(axis, float) / np.linalg.norm(axis)
+    return np.r_[np.cos(ang / 2), np.sin(ang / 2) * axis]
+
+
+def _qmul(a, b):
+    return np.r_[a[0] * b[0] - a[1:] @ b[1:], a[0] * b[1:] + b[0] * a[1:] + np.cross(a[1:], b[1:])]
+
+
+def lying_states(o, n, seed, overflow=True):
+    """Prone / supine / on-the-side humanoids pressed into the floor; with overflow=True only
+    states whose contacts or rows exceed the resident tier (ncon > 32 or nefc > 128) are kept."""
+    M = o.M
+    rng = np.random.default_rng(seed)
+    lo, hi = M["jnt_range"][1:, 0], M["jnt_range"][1:, 1]
+    out = []
+    for _ in range(20000):
+        q = M["qpos0"].copy()
+        q[3:7] = _qmul(_qaxis([0, 0, 1], rng.uniform(-np.pi, np.pi)),
+                       _qmul(_qaxis([0, 1, 0], np.pi / 2 * rng.choice([-1, 1])),
+                             _qaxis([1, 0, 0], rng.uniform(-np.pi, np.pi))))
+        q[7:] = np.clip(rng.uniform(0, 0.3) * rng.normal(size=21), lo, hi)
+        q[2] = rng.uniform(0.0, 0.2)
+        o.reset_data()
+        o.qpos[:] = q
+        o.qvel[:] = 0
+        o.forward()
+        big = o.d.ncon > 32 or o.d.nefc > 128
+        if big == overflow:
+            out.append(q)
+            if len(out) == n:
+                return out
+    raise AssertionError("not enough states")
+
+
+def _oracle_step(o, q, v, c):
+    o.reset_data()
+    o.qpos[:] = q
+    o.qvel[:] = v
+    o.step(c.astype(np.float64), 1)
+    return o.qpos.copy(), o.qvel.copy(), o.get("qacc"), o.d.ncon, o.d.nefc
+
+
+@pytest.mark.parametrize("prec", ["fp64", "fp32"])
+def test_wide_tier_lying_states_match_oracle(model, prec):
+    import torch
+    from mujocoposelearning_amd.batch import HsBatch
+    from oracle.oracle import Oracle
+    o = Oracle(XML)
+    big = lying_states(o, 24, seed=1)
+    small = lying_states(o, 8, seed=2, overflow=False)
+    qs = np.stack(big + small)
+    n = len(qs)
+    rng = np.random.default_rng(5)
+    vs = rng.normal(0, 0.3, (n, 27))
+    cs = rng.uniform(-1, 1, (n, 21)).astype(np.float32)
+    b = HsBatch(model, n, precision=prec)
+    b.set_state(qpos=qs, qvel=vs, time=0.0, qacc_warmstart=0.0)
+    b.physics_step(torch.tensor(cs, device=b.device), 1)
+    st = b.get_state()
+    aux = b.aux.double().cpu().numpy()
+    assert b.warning.sum().item() == 0
+    assert b.wide_reruns() == len(big)               # exactly the overflowing envs were re-run
+    for i in range(n):
+        rq, rv, ra, ncon, nefc = _oracle_step(o, qs[i], vs[i], cs[i])
+        assert int(aux[i, 35]) == ncon and int(aux[i, 36]) == nefc, (i, aux[i, 35:37], ncon, nefc)
+        scale = 1 + np.abs(ra).max()
+        if prec == "fp64":
+            assert np.abs(aux[i, :27] - ra).max() <= 1e-8 * scale, i
+            assert np.abs(st["qpos"][i] - rq).max() <= 1e-12, i
+            assert np.abs(st["qvel"][i] - rv).max() <= 1e-10 * scale, i
+        else:
+            assert np.abs(aux[i, :27] - ra).max() <= 2e-3 * scale, i
+            assert np.abs(st["qvel"][i] - rv).max() <= 1e-5 * scale, i
+            assert np.abs(st["qpos"][i] - rq).max() <= 2e-6 + 1e-7 * scale, i
+    # the resident-tier envs are untouched by sharing the launch with deferred ones
+    b2 = HsBatch(model, len(small), precision=prec)
+    b2.set_state(qpos=np.stack(small), qvel=vs[len(big):], time=0.0, qacc_warmstart=0.0)
+    b2.physics_step(torch.tensor(cs[len(big):], device=b2.device), 1)
+    assert torch.equal(b2.qpos, b.qpos[len(big):]) and torch.equal(b2.qvel, b.qvel[len(big):])
+    assert b2.wide_reruns() == 0
+
+
+def test_wide_tier_env_step_autoreset_matches_oracle_env(model):
+    """MODE_ENV_STEP through the wide tier: 3 substeps, obs, stand reward, termination at
+    time >= duration, auto-reset with host-bound noise (custom_env.py:152-230, 97-130)."""
+    import torch
+    from mujocoposelearning_amd.batch import HsBatch
+    from oracle.env import OracleHumanoidEnv
+    from oracle.oracle import Oracle
+    o = Oracle(XML)
+    qs = np.stack(lying_states(o, 6, seed=3))
+    n = len(qs)
+    rng = np.random.default_rng(7)
+    vs = rng.normal(0, 0.2, (n, 27))
+    acts = rng.uniform(-1, 1, (n, 21)).astype(np.float32)
+    qn, vn = rng.uniform(-0.01, 0.01, (n, 28)), rng.uniform(-0.01, 0.01, (n, 27))
+    t0 = 10.0 - 3 * 0.005 + 1e-3                       # terminates in this step
+    b = HsBatch(model, n, precision="fp64")
+    b.configure(frame_skip=3, duration=10.0, reward_id=0, autoreset=1, max_steps=750)
+    b.set_state(qpos=qs, qvel=vs, time=t0, qacc_warmstart=0.0, ctrl=0.0)
+    b.set_autoreset_noise(qn, vn)
+    b.step(torch.tensor(acts, device=b.device))
+    assert b.wide_reruns() == n and b.warning.sum().item() == 0
+    term_obs, obs = b.terminal_obs.cpu().numpy(), b.obs.cpu().numpy()
+    rew = b.reward.cpu().numpy()
+    for i in range(n):
+        env = OracleHumanoidEnv({"model_path": XML, "duration": 10.0, "frame_skip": 3,
+                                 "reward_config": {"type": "stand"}})
+        env.sim.reset_data()
+        env.sim.qpos[:] = qs[i]
+        env.sim.qvel[:] = vs[i]
+        env.sim.d.time = t0
+        env.step_count = 0
+        ob, r, term, trunc, _ = env.step(acts[i])
+        assert term and not trunc and bool(b.terminated[i]) and not bool(b.truncated[i])
+        sc = 1 + np.abs(ob).max()
+        assert np.abs(term_obs[i] - ob).max() <= 1e-8 * sc, i
+        assert rew[i] == pytest.approx(r, abs=1e-9)
+        assert int(b.terminal_step_count[i]) == 1
+        assert float(b.terminal_total_reward[i]) == pytest.approx(r, abs=1e-9)
+        ob0, _ = env.reset(pos_noise=qn[i], vel_noise=vn[i])
+        assert np.abs(obs[i] - ob0).max() <= 1e-9 * (1 + np.abs(ob0).max()), i
+    assert int(b.step_count.max()) == 0 and np.allclose(b.time.cpu().numpy(), 0.005)
+
+
+@pytest.mark.parametrize("tape", ["T0", "T1"])
+def test_full_episode_4096_envs_drops_no_contact(model, tape):
+    """configs[1] through a whole 667-step episode (every humanoid falls and lies in contact)
+    plus the auto-reset step: HS_WARN_OVERFLOW stays 0 for every env (fp64 headline engine)."""
+    import torch
+    from mujocoposelearning_amd.batch import HsBatch
+    n = 4096
+    b = HsBatch(model, n, precision="fp64", seed=17)
+    b.configure(frame_skip=3, duration=10.0, reward_id=0, autoreset=1, max_steps=750)
+    b.reset()
+    g = torch.Generator(device="cuda").manual_seed(3)
+    max_con = max_rows = 0
+    for k in range(668):
+        a = (torch.zeros(n, 21, device="cuda") if tape == "T0"
+             else torch.rand(n, 21, device="cuda", generator=g) * 2 - 1)
+        b.step(a)
+        if k % 50 == 49:
+            max_con = max(max_con, int(b.aux[:, 35].max()))
+            max_rows = max(max_rows, int(b.aux[:, 36].max()))
+    w = b.warning.cpu().numpy()
+    assert (w == 0).all(), w.sum(0)
+    assert int(b.episode.min()) == 2                      # reset() + the auto-reset at step 667
+    assert max_con >= 8 and max_rows >= 30                # fallen humanoids in contact
+    assert torch.isfinite(b.obs).all()
+    print(f"{tape}: max contacts {max_con}, max rows {max_rows}, wide-tier re-runs {b.wide_reruns()}")

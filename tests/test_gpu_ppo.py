@@ -367,13 +367,20 @@ def test_fused_ppo_loss_matches_torch(B):
     assert torch.allclose(gv, gv_r, rtol=1e-5, atol=1e-9)
 
 
-def test_adam_clip_matches_torch_clip_and_adam():
+@pytest.mark.parametrize("hidden", [1, 20])
+def test_adam_clip_matches_torch_clip_and_adam(hidden):
     """hs_adam_clip (clip_grad_norm_ + Adam in three launches) == torch.nn.utils.clip_grad_norm_ +
-    torch.optim.Adam over several steps, on an MLP's parameter list, clipping active and not."""
+    torch.optim.Adam over several steps, on an MLP's parameter list, clipping active and not.
+    hidden=20: 42 tensors, three chunks of the 16-tensor kernel sharing one clip coefficient."""
     from mujocoposelearning_amd.ppo import adam_clip_step
     torch.manual_seed(0)
-    nets = [torch.nn.Sequential(torch.nn.Linear(352, 256), torch.nn.ReLU(), torch.nn.Linear(256, 21)).cuda()
-            for _ in range(2)]
+
+    def mlp():
+        layers = [torch.nn.Linear(352, 64), torch.nn.ReLU()]
+        for _ in range(hidden - 1):
+            layers += [torch.nn.Linear(64, 64), torch.nn.ReLU()]
+        return torch.nn.Sequential(*layers, torch.nn.Linear(64, 21)).cuda()
+    nets = [mlp() for _ in range(2)]
     nets[1].load_state_dict(nets[0].state_dict())
     opts = [torch.optim.Adam(n.parameters(), lr=3e-4, eps=1e-5) for n in nets]
     g = torch.Generator(device="cuda").manual_seed(1)
@@ -413,3 +420,24 @@ def test_relu_grad_colsum_and_pair():
         s0, s1 = colsum_pair(p2, part)
         assert torch.allclose(s0, p2.double().sum(0).float(), rtol=1e-5, atol=1e-5)
         assert torch.allclose(s1, ref.double().sum(0).float(), rtol=1e-5, atol=1e-5 * rows ** 0.5)
+
+
+def test_ppo_deep_net_arch_trains_on_gpu():
+    """net_arch lists of any depth (main.py --net_arch_pi/--net_arch_vf): 3 + 3 hidden
+    layers are 17 parameter tensors (> one 16-tensor Adam chunk); graphed training runs and
+    changes every parameter."""
+    from mujocoposelearning_amd.model import HsModel
+    from mujocoposelearning_amd.ppo import PPO
+    from mujocoposelearning_amd.vec_env import HumanoidVecEnv
+    env = HumanoidVecEnv({"model_path": XML, "duration": 10.0, "reward_config": {"type": "stand"}, "frame_skip": 3},
+                         n_envs=256, model=HsModel(XML), seed=0)
+    ppo = PPO(env, n_steps=8, batch_size=512, n_epochs=2, seed=0,
+              policy_kwargs={"activation_fn": "ReLU", "net_arch": {"pi": [64, 64, 64], "vf": [64, 64, 64]}})
+    params = [p for p in ppo.policy.parameters()]
+    assert len(params) == 17
+    before = [p.detach().clone() for p in params]
+    ppo.learn(2 * 8 * 256)
+    torch.cuda.synchronize()
+    assert all(not torch.equal(a, p.detach()) for a, p in zip(before, params))
+    assert all(torch.isfinite(p).all() for p in params)
+    env.close()
