@@ -15,6 +15,8 @@ from .model import compile_mjcf
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "build", "libhsim_oracle.so")
+# a prebuilt variant to load instead (tests/test_sanitizers.py: the ASan/UBSan build of the same C)
+LIB_OVERRIDE = os.environ.get("HSIM_ORACLE_LIB")
 
 OMAXB, OMAXJ, OMAXV, OMAXQ, OMAXG, OMAXT, OMAXW, OMAXU = 32, 32, 40, 48, 32, 8, 32, 32
 OMAXCON, OMAXEFC, OMAXPAIR = 160, 640, 512
@@ -106,6 +108,8 @@ class OrcData(C.Structure):
 
 def build(force=False):
     """Compile the C restatement with gcc into oracle/build/ (checker build, not product)."""
+    if LIB_OVERRIDE:
+        return LIB_OVERRIDE
     src = os.path.join(HERE, "hsim_oracle.c")
     if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
         os.makedirs(os.path.dirname(LIB_PATH), exist_ok=True)

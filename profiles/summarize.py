@@ -3,6 +3,13 @@
 HBM bytes per launch follow MI355X_MICROARCH.md (HBM/rocprofv3): FETCH_SIZE and WRITE_SIZE come
 from separate --pmc passes, are in KiB (x1024), and gfx950's FETCH_SIZE counts wide reads at 1/2,
 so the corrected figure is 2*FETCH + WRITE (the raw figure is reported beside it).
+
+Usage: python profiles/summarize.py <tag> <precision> [n_envs] [timed_steps]
+The resident-tier step kernel (``step_kernel<T, 27, ...>``) is summarized; the wide-tier launch
+(``step_kernel_wide``) is listed in the stats table.  Per-launch figures average the last
+``timed_steps`` launches before bench.py's 3 statistics steps (its timed window, after the
+staggered-episode precondition).
+traffic_step_kernel.json keeps one entry per precision (bench.py reads the one it runs).
 """
 import csv
 import json
@@ -11,51 +18,62 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+STATS_STEPS = 3     # bench.py's stats_of() steps after the timed window
 
 
-def main(tag="r01", n_envs=4096, precision="fp32", src=None):
+def is_step(name):
+    return "step_kernel<" in name and "wide" not in name
+
+
+def main(tag="r2a", precision="fp64", n_envs=4096, timed=50, src=None):
+    n_envs, timed = int(n_envs), int(timed)
+    es = 8 if precision == "fp64" else 4
+    algo_env = 83 * es + 21 * 4 + 436 * es + 2          # bench.algo_bytes_per_env_step
     src = src or os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     stats = list(csv.DictReader(open(os.path.join(src, "trace", "trace_kernel_stats.csv"))))
     ktrace = [r for r in csv.DictReader(open(os.path.join(src, "trace", "trace_kernel_trace.csv")))
-              if "step_kernel" in r["Kernel_Name"]]
+              if is_step(r["Kernel_Name"])]
+    ktrace.sort(key=lambda r: int(r["Start_Timestamp"]))
     durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in ktrace]
-    steady = durs[7:] if len(durs) > 10 else durs     # skip reset + warmup launches
+    win = durs[-timed - STATS_STEPS:-STATS_STEPS]
+
     def pmc(name):
-        f = os.path.join(src, name.split("_")[0].lower(), f"{name.split('_')[0].lower()}_counter_collection.csv")
-        rows = [r for r in csv.DictReader(open(f)) if "step_kernel" in r["Kernel_Name"]]
-        vals = [float(r["Counter_Value"]) for r in rows]
-        return vals, rows[0]
+        sub = name.split("_")[0].lower()
+        rows = [r for r in csv.DictReader(open(os.path.join(src, sub, f"{sub}_counter_collection.csv")))
+                if is_step(r["Kernel_Name"])]
+        rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+        return [float(r["Counter_Value"]) for r in rows][-timed - STATS_STEPS:-STATS_STEPS], rows[0]
     fetch, row = pmc("FETCH_SIZE")
     write, _ = pmc("WRITE_SIZE")
-    f_kib = statistics.mean(fetch[7:]) if len(fetch) > 10 else statistics.mean(fetch)
-    w_kib = statistics.mean(write[7:]) if len(write) > 10 else statistics.mean(write)
+    f_kib, w_kib = statistics.mean(fetch), statistics.mean(write)
     raw = (f_kib + w_kib) * 1024
     corrected = (2 * f_kib + w_kib) * 1024
-    algo = 2162 * n_envs
-    out = dict(tag=tag, n_envs=n_envs, precision=precision, kernel="step_kernel",
-               avg_ms_steady=statistics.mean(steady), avg_ms_all=statistics.mean(durs), launches=len(durs),
-               fetch_kib_per_launch=f_kib, write_kib_per_launch=w_kib, hbm_bytes_per_launch_raw=raw,
-               hbm_bytes_per_launch=corrected, algo_bytes_per_launch=algo, traffic_over_algo=corrected / algo,
+    algo = algo_env * n_envs
+    out = dict(tag=tag, n_envs=n_envs, precision=precision, kernel=row["Kernel_Name"][:80],
+               avg_ms_timed=statistics.mean(win), timed_launches=len(win), avg_ms_all=statistics.mean(durs),
+               launches=len(durs), fetch_kib_per_launch=f_kib, write_kib_per_launch=w_kib,
+               hbm_bytes_per_launch_raw=raw, hbm_bytes_per_launch=corrected, algo_bytes_per_env_step=algo_env,
+               algo_bytes_per_launch=algo, traffic_over_algo=corrected / algo,
                vgpr=int(row["VGPR_Count"]), agpr=int(row["Accum_VGPR_Count"]), sgpr=int(row["SGPR_Count"]),
                lds_bytes=int(row["LDS_Block_Size"]), scratch_bytes_per_lane=int(row["Scratch_Size"]),
                grid=int(row["Grid_Size"]), workgroup=int(row["Workgroup_Size"]))
-    json.dump(out, open(os.path.join(ROOT, "profiles", "traffic_step_kernel.json"), "w"), indent=1)
     lines = [f"# rocprofv3 summary `{tag}` -- step kernel, {n_envs} envs, {precision}", "",
-             "Command: `bash profiles/collect.sh` (bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-rollout --no-gae --train-iters 0 --groups 1 --free-groups 0 --no-configs)", "",
+             f"Command: `bash profiles/collect.sh {tag} {precision}` (bench.py --steps {timed} --warmup 5, sim-only "
+             "legs only, staggered-episode precondition)", "",
              "## Kernel stats (rocprofv3 --kernel-trace --stats)", "",
              "| kernel | calls | avg us | min us | max us | % |", "|---|---|---|---|---|---|"]
-    for r in stats[:6]:
+    for r in stats[:8]:
         name = r["Name"][:90].replace("|", "/")
         lines.append(f"| `{name}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | {float(r['MinNs']) / 1e3:.1f} | "
                      f"{float(r['MaxNs']) / 1e3:.1f} | {float(r['Percentage']):.2f} |")
-    lines += ["", f"Steady-state step_kernel launches (after reset + warmup): avg {out['avg_ms_steady']:.3f} ms "
-                  f"over {len(steady)} launches (all {len(durs)} launches: {out['avg_ms_all']:.3f} ms).", "",
-              "## HBM traffic per launch (separate --pmc passes)", "",
+    lines += ["", f"Resident-tier step kernel, timed window (last {len(win)} launches): avg {out['avg_ms_timed']:.3f} ms "
+                  f"(all {len(durs)} launches incl. reset / precondition episode: {out['avg_ms_all']:.3f} ms).", "",
+              "## HBM traffic per launch (separate --pmc passes, timed window)", "",
               f"- FETCH_SIZE {f_kib:,.0f} KiB, WRITE_SIZE {w_kib:,.0f} KiB",
               f"- raw (FETCH+WRITE)*1024 = {raw / 1e6:,.2f} MB; gfx950-corrected (2*FETCH+WRITE)*1024 = "
               f"{corrected / 1e6:,.2f} MB",
-              f"- algorithmic {algo / 1e6:,.2f} MB (2162 B/env step x {n_envs}); traffic/algo = "
-              f"{corrected / algo:.1f}x", "",
+              f"- algorithmic {algo / 1e6:,.2f} MB ({algo_env} B/env step x {n_envs}); traffic/algo = "
+              f"{corrected / algo:.2f}x", "",
               "## Resources", "",
               f"VGPR {out['vgpr']} (+{out['agpr']} AGPR), SGPR {out['sgpr']}, LDS {out['lds_bytes']} B/workgroup, "
               f"scratch {out['scratch_bytes_per_lane']} B/lane, grid {out['grid']} threads x wg {out['workgroup']}."]
@@ -66,10 +84,9 @@ def main(tag="r01", n_envs=4096, precision="fp32", src=None):
             continue
         by = {}
         for r in csv.DictReader(open(f)):
-            if "step_kernel" in r["Kernel_Name"]:
+            if is_step(r["Kernel_Name"]):
                 by.setdefault(r["Dispatch_Id"], {})[r["Counter_Name"]] = float(r["Counter_Value"])
-        ids = sorted(by, key=int)
-        ids = ids[7:] if len(ids) > 10 else ids
+        ids = sorted(by, key=int)[-timed - STATS_STEPS:-STATS_STEPS]
         for k in by[ids[0]]:
             sq[k] = statistics.mean(by[i][k] for i in ids)
     if sq:
@@ -87,11 +104,19 @@ def main(tag="r01", n_envs=4096, precision="fp32", src=None):
                 kc = sq["GRBM_GUI_ACTIVE"] / 8
                 life = 4 * wc / sq["SQ_WAVES"]
                 lines.append(f"- mean wave lifetime {life:,.0f} cycles vs kernel {kc:,.0f} cycles (GRBM_GUI_ACTIVE/8): "
-                             f"{life / kc:.0%} -- the rest is the Newton-iteration tail (one wave per slot at 4096 envs)")
-        json.dump(out, open(os.path.join(ROOT, "profiles", "traffic_step_kernel.json"), "w"), indent=1)
+                             f"{life / kc:.0%}")
+    path = os.path.join(ROOT, "profiles", "traffic_step_kernel.json")
+    try:
+        allp = json.load(open(path))
+        if "precision" in allp:          # r1 single-entry layout
+            allp = {allp["precision"]: allp}
+    except (OSError, ValueError):
+        allp = {}
+    allp[precision] = out
+    json.dump(allp, open(path, "w"), indent=1)
     open(os.path.join(ROOT, "profiles", f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:2])
+    main(*sys.argv[1:])
