@@ -47,6 +47,10 @@ TIMESTEP = 0.005
 EPISODE = math.ceil(DURATION / (FRAME_SKIP * TIMESTEP) - 1e-9)   # 667 env steps (custom_env.py:213)
 HBM_PEAK_GBS = 8000.0
 PROFILE_TRAFFIC = os.path.join(ROOT, "profiles", "traffic_step_kernel.json")
+FLOPS_JSON = os.path.join(ROOT, "profiles", "flops_per_env_step.json")     # oracle/flops.py
+# vector (VALU) peaks: FP32 157.3 TFLOP/s (MI355X_MICROARCH.md); FP64 vector runs at half that rate
+# (78.6 TFLOP/s, AMD's MI355X spec)
+VALU_PEAK_TFLOPS = {"fp32": 157.3, "fp64": 78.6}
 
 
 def algo_bytes_per_env_step(es):
@@ -500,6 +504,14 @@ def main():
             except Exception:
                 traffic = None
         kname = "step_kernel<double,27>" if args.precision == "fp64" else "step_kernel<float,27>"
+        vflops = None
+        if os.path.exists(FLOPS_JSON):
+            fpe = json.load(open(FLOPS_JSON))["mean_total"]
+            ach = fpe * n / (kernel_ms * 1e-3) / 1e12
+            vflops = {"flops_per_env_step": fpe, "achieved_tflops": ach,
+                      "peak_tflops": VALU_PEAK_TFLOPS[args.precision], "frac": ach / VALU_PEAK_TFLOPS[args.precision],
+                      "source": "oracle restatement FLOP count per env step (oracle/flops.py, mean of tapes "
+                                "T0/T1/T2) x envs / live launch time; an upper bound on the kernel's useful FLOPs"}
         out = {
             "metric": "env steps/sec (whole node), humanoid 'stand' task, 1/2/4/8 MI355X",
             "value": value,
@@ -524,7 +536,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
                          "kernel_ms_per_launch": kernel_ms, "envs_per_launch": n,
-                         "algo_bytes_per_env_step": abytes, "valu_issue": issue,
+                         "algo_bytes_per_env_step": abytes, "valu_issue": issue, "valu_flops": vflops,
                          "note": "latency-bound kernel (see valu_issue and DESIGN.md 3.1); HBM fraction reported per "
                                  "BASELINE.json; HIP events over the timed steps on the launch stream (the step "
                                  "kernel + the wide-tier launch, which exits at once when no env overflowed)"},

@@ -679,7 +679,9 @@ struct PhaseClock {
   __device__ __forceinline__ void start() { prev = t0 = __builtin_amdgcn_s_memtime(); }
   __device__ __forceinline__ void stamp(int slot) {
     uint64_t now = __builtin_amdgcn_s_memtime();
-    acc[slot] += now - prev;
+    uint64_t d = now - prev;
+    asm volatile("" : "+v"(d));   // accumulate in VGPRs (stamps sit in divergent regions too)
+    acc[slot] += d;
     prev = now;
   }
 };
@@ -1986,6 +1988,7 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
     if (st.dbg && active && !in_reset) dump_debug(st, st.dbg);
   }
 #ifdef HS_TIMING
+  if constexpr (WIDE) return;      // the diagnostic clock covers the resident tier only
   HS_STAMP(st.clk, 14);
   T* dbg = ka->b.dbg;
   if (sl == 0 && dbg) {

@@ -25,6 +25,13 @@
 #include <stdlib.h>
 #include <string.h>
 
+/* per-stage FLOP attribution for the counting build (oracle/flopcount.h); nothing otherwise */
+#ifndef ORC_NSTAGE
+#define ORC_STAGE(k) ((void)0)
+#endif
+enum { ST_KIN = 0, ST_COM, ST_TENDON, ST_CRB, ST_COLLISION, ST_CONSTRAINT, ST_COMVEL, ST_PASSIVE, ST_REFERENCE,
+       ST_RNE, ST_ACTUATION, ST_SMOOTH, ST_SOLVER, ST_EULER, ST_OTHER };
+
 #define MINVAL 1e-15
 #define MAXVAL 1e10
 #define MINIMP 0.0001
@@ -841,20 +848,22 @@ static void solve_pgs(const OrcModel* m, OrcData* d) {
 void orc_forward(const OrcModel* m, OrcData* d) {
   int nv = m->nv;
   static double L[OMAXV][OMAXV];
-  kinematics(m, d);
-  com_pos(m, d);
-  tendon(m, d);
-  crb(m, d);
-  collision(m, d);
-  make_constraint(m, d);
-  com_vel(m, d);
-  passive(m, d);
-  reference_constraint(m, d);
-  rne(m, d);
-  actuation(m, d);
+  ORC_STAGE(ST_KIN); kinematics(m, d);
+  ORC_STAGE(ST_COM); com_pos(m, d);
+  ORC_STAGE(ST_TENDON); tendon(m, d);
+  ORC_STAGE(ST_CRB); crb(m, d);
+  ORC_STAGE(ST_COLLISION); collision(m, d);
+  ORC_STAGE(ST_CONSTRAINT); make_constraint(m, d);
+  ORC_STAGE(ST_COMVEL); com_vel(m, d);
+  ORC_STAGE(ST_PASSIVE); passive(m, d);
+  ORC_STAGE(ST_REFERENCE); reference_constraint(m, d);
+  ORC_STAGE(ST_RNE); rne(m, d);
+  ORC_STAGE(ST_ACTUATION); actuation(m, d);
+  ORC_STAGE(ST_SMOOTH);
   for (int i = 0; i < nv; i++) d->qfrc_smooth[i] = d->qfrc_passive[i] - d->qfrc_bias[i] + d->qfrc_actuator[i];
   chol(L, d->qM, nv);
   chol_solve(d->qacc_smooth, L, d->qfrc_smooth, nv);
+  ORC_STAGE(ST_SOLVER);
   if (d->nefc == 0) {
     memcpy(d->qacc, d->qacc_smooth, sizeof(double) * nv);
     memset(d->qfrc_constraint, 0, sizeof(double) * nv);
@@ -972,8 +981,11 @@ static void step_impl(const OrcModel* m, OrcData* d, int full) {
   orc_forward(m, d);
   for (int i = 0; i < m->nv; i++)                 /* mj_checkAcc */
     if (isbad(d->qacc[i])) { d->warning_badqacc++; reset_keep_warnings(m, d); orc_forward(m, d); break; }
+  ORC_STAGE(ST_OTHER);
   if (full) orc_contact_forces(m, d);
+  ORC_STAGE(ST_EULER);
   euler(m, d);
+  ORC_STAGE(ST_OTHER);
 }
 
 void orc_step_n_full(const OrcModel* m, OrcData* d, const double* ctrl, int nsub, int full) {
