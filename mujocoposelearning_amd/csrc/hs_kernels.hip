@@ -686,7 +686,22 @@ struct PhaseClock {
   }
 };
 #define HS_STAMP(clk, slot) (clk).stamp(slot)
+// flushed once, inside the substep loop at its exits: a per-lane accumulator live past the loop
+// trips an isel bug ("illegal VGPR to SGPR copy") in this compiler
+#define HS_FLUSH()                                                                              \
+  do {                                                                                           \
+    T* dbg_ = opaque(ka)->b.dbg;                                                                 \
+    if (dbg_ && !WIDE) {                                                                         \
+      if (sl == 0)                                                                               \
+        for (int q = 0; q < NSLOT; q++) { atomicAdd(&dbg_[8000 + q], (T)st.clk.acc[q]); st.clk.acc[q] = 0; } \
+      if (sl == 0) atomicAdd(&dbg_[8030], (T)tot_iter);                                          \
+      if (lane == 0 && blockIdx.x < 2048) dbg_[9000 + blockIdx.x] = (T)(st.clk.prev - st.clk.t0);  \
+      if (sl == 0 && blockIdx.x < 2048) dbg_[11100 + 2 * blockIdx.x + (up ? 1 : 0)] = (T)tot_iter;  \
+      tot_iter = 0;                                                                              \
+    }                                                                                            \
+  } while (0)
 #else
+#define HS_FLUSH() ((void)0)
 struct PhaseClock {
   __device__ __forceinline__ void start() {}
   __device__ __forceinline__ void stamp(int) {}
@@ -1941,7 +1956,7 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
           active = false;   // committed (or deferred); a reset pass below is scratch work for this half
         }
       }
-      if (__ballot(do_reset) == 0) break;
+      if (__ballot(do_reset) == 0) { HS_FLUSH(); break; }
       // custom_env.py:97-130: mj_resetData; qpos = init (z=1.282, upright); += U(+-0.01) noise
       // with z noise x0.1 and no quaternion noise; qvel = U(+-0.01); one mj_step with ctrl = 0.
       KPtr<T> k = opaque(ka);
@@ -1975,6 +1990,7 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
         write_obs(st.m, s, sl, st.qfa, k->b.obs + (size_t)env * obs_dim, obs_dim);
         if (!defer(k)) commit(st.m, k, st, env, time, xws, 0, episode, T(0), warn, k->p.full_state != 0);
       }
+      HS_FLUSH();
       break;
     } else {
       // data.ctrl[:] = action each substep (custom_env.py:159); mj_resetData may have zeroed it
@@ -1987,19 +2003,6 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
 #endif
     if (st.dbg && active && !in_reset) dump_debug(st, st.dbg);
   }
-#ifdef HS_TIMING
-  if constexpr (WIDE) return;      // the diagnostic clock covers the resident tier only
-  HS_STAMP(st.clk, 14);
-  T* dbg = ka->b.dbg;
-  if (sl == 0 && dbg) {
-    for (int q = 0; q < NSLOT; q++) atomicAdd(&dbg[8000 + q], (T)st.clk.acc[q]);
-    atomicAdd(&dbg[8030], (T)st.niter);
-  }
-  // per-wave lifetime of this launch (shader cycles) -> dbg[9000 + wave] (waves < 7000)
-  if (lane == 0 && dbg && blockIdx.x < 2048) dbg[9000 + blockIdx.x] = (T)(st.clk.prev - st.clk.t0);
-  // per-env Newton iterations summed over this launch's substeps -> dbg[11100 + env]
-  if (sl == 0 && dbg && blockIdx.x < 2048) dbg[11100 + 2 * blockIdx.x + (up ? 1 : 0)] = (T)tot_iter;
-#endif
 }
 
 // Resident tier: one wave per env pair, all pairs of the batch in one grid.

@@ -19,12 +19,18 @@ NAMES = ["load", "kinematics", "mass_matrix", "vel+rne", "collision", "rows+aref
 NS = len(NAMES)
 
 
-def main(n=4096, steps=20, prec="fp32"):
+def main(n=4096, steps=20, prec="fp32", staggered=False):
     model = HsModel(os.path.join(ROOT, "mujocoposelearning_amd", "assets", "humanoid.xml"))
     b = HsBatch(model, n, precision=prec, seed=1)
     b.configure(frame_skip=3, duration=10.0, reward_id=0)
     b.reset()
     g = torch.Generator(device="cuda").manual_seed(0)
+    if staggered:
+        # bench.py's window: env i starts i/N into the episode, then one full (667-step) episode
+        t0 = np.floor(np.arange(n) * 667 / n) * 0.015 + 0.005
+        b.set_state(time=t0)
+        for k in range(667):
+            b.step(torch.rand(n, 21, device="cuda", generator=g) * 2 - 1)
     for k in range(5):
         b.step(torch.rand(n, 21, device="cuda", generator=g) * 2 - 1)
     b.set_debug(True)
@@ -41,8 +47,8 @@ def main(n=4096, steps=20, prec="fp32"):
     d = b.get_debug()[8000:8031] - dbg0
     tot = d[:NS].sum()
     per = d[:NS] / (n * steps * 3)
-    print(f"[{prec}] N={n}: {ms:.3f} ms/launch; cycles per env-substep (wave lifetime) {tot / (n * steps * 3):,.0f}; "
-          f"newton iters/substep {d[30] / (n * steps):.2f}")
+    print(f"[{prec}{' staggered' if staggered else ''}] N={n}: {ms:.3f} ms/launch; cycles per env-substep (wave lifetime) {tot / (n * steps * 3):,.0f}; "
+          f"newton iters/env step {d[30] / (n * steps):.2f}")
     for name, c, f in zip(NAMES, per, d[:NS] / tot):
         print(f"  {name:20s} {c:10,.0f} cyc  {100 * f:5.1f}%")
     life = b.get_debug()[9000:9000 + (n + 1) // 2]        # last launch, one value per wave
@@ -93,4 +99,4 @@ if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[2] == "predict":
         predict(prec=sys.argv[1])
         sys.exit(0)
-    main(prec=sys.argv[1] if len(sys.argv) > 1 else "fp32")
+    main(prec=sys.argv[1] if len(sys.argv) > 1 else "fp32", staggered="staggered" in sys.argv[2:])
