@@ -215,17 +215,43 @@ __device__ __forceinline__ T dot6(const T* a, const T* b) {
   return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
 }
 template <typename T>
+__device__ __forceinline__ T rsqrt_t(T x);
+template <>
+__device__ __forceinline__ float rsqrt_t<float>(float x) { return __builtin_amdgcn_rsqf(x); }
+// fp64: v_rsq_f64 (about half precision) + two Newton steps y += y (1 - x y^2) / 2 -- 7 dependent
+// FMAs/MULs instead of the correctly rounded sqrt expansion followed by a correctly rounded divide
+// (~25); within 1-2 ulp of 1/sqrt(x) for the positive, normal arguments it is used on
+template <>
+__device__ __forceinline__ double rsqrt_t<double>(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  double e = fma(-x * y, y, 1.0);
+  y = fma(0.5 * y, e, y);
+  e = fma(-x * y, y, 1.0);
+  return fma(0.5 * y, e, y);
+}
+// 1/x: fp32 is v_rcp_f32 under -fno-hip-fp32-correctly-rounded-divide-sqrt; fp64 is v_rcp_f64 +
+// two Newton steps (within 1-2 ulp of the correctly rounded divide, for normal nonzero x)
+__device__ __forceinline__ float recip(float x) { return 1.0f / x; }
+__device__ __forceinline__ double recip(double x) {
+  double y = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, y, 1.0);
+  y = fma(y, e, y);
+  e = fma(-x, y, 1.0);
+  return fma(y, e, y);
+}
+template <typename T>
 __device__ __forceinline__ T normalize3(T* v) {
-  T n = sqrt(dot3(v, v));
-  if (n < T(1e-15)) { v[0] = 1; v[1] = 0; v[2] = 0; }
-  else { T i = T(1) / n; v[0] *= i; v[1] *= i; v[2] *= i; }
-  return n;
+  const T n2 = dot3(v, v);
+  if (n2 < T(1e-30)) { v[0] = 1; v[1] = 0; v[2] = 0; return sqrt(n2); }
+  const T i = rsqrt_t(n2);
+  v[0] *= i; v[1] *= i; v[2] *= i;
+  return n2 * i;
 }
 template <typename T>
 __device__ __forceinline__ void normalize4(T* q) {
-  T n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
-  if (n < T(1e-15)) { q[0] = 1; q[1] = q[2] = q[3] = 0; }
-  else { T i = T(1) / n; q[0] *= i; q[1] *= i; q[2] *= i; q[3] *= i; }
+  const T n2 = q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3];
+  if (n2 < T(1e-30)) { q[0] = 1; q[1] = q[2] = q[3] = 0; }
+  else { const T i = rsqrt_t(n2); q[0] *= i; q[1] *= i; q[2] *= i; q[3] *= i; }
 }
 // spatial inertia (10-param cinert layout) times motion vector (mju_mulInertVec)
 template <typename T>
@@ -258,14 +284,11 @@ __device__ __forceinline__ void cross_force(const T* v, const T* f, T* r) {
 
 // ------------------------------------------------------------------ row-per-lane dense algebra
 // Cholesky A = L L' of an NV x NV SPD matrix held row-per-lane in each half (sub-lane i: row i);
-// the lower part becomes L, the upper part scratch; dinv (sub-lane i) = 1 / L_ii.  Step k
+// on return A holds L's strictly lower part (diagonal and upper part zeroed, so the substitutions
+// below need no lane selects) and dinv (sub-lane i) = 1 / L_ii.  Step k
 // publishes column k (a_ik, one ds_write) in the env's LDS vector `col`; every lane reads the
 // pivot and a_jk (j > k) back as broadcast ds_reads, so the update is pure FMAs:
 //   A_ij -= (a_ik / a_kk) a_jk.
-template <typename T>
-__device__ __forceinline__ T rsqrt_t(T x) { return T(1) / sqrt(x); }
-template <>
-__device__ __forceinline__ float rsqrt_t<float>(float x) { return __builtin_amdgcn_rsqf(x); }
 
 template <int NV, typename T>
 __device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb)[2]) {
@@ -310,28 +333,67 @@ __device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb)[2
     A[k] = (sl_k == k) ? akk * r : A[k] * r;
     dinv = (sl_k == k) ? r : dinv;
   }
+  const int sl_z = opaque_v(sl);
+  static_for<0, NV>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    A[j] = sl_z > j ? A[j] : T(0);
+  });
 }
-// solve (L L') x = b; sub-lane i holds b_i; returns x_i.  Sub-lane k finishes y_k / x_k itself
-// (times its own 1/L_kk) and one broadcast hands it to the half.
+// solve (L L') x = b (L from chol_rows: strictly lower part, 1/L_ii in dinv); sub-lane i holds b_i;
+// returns x_i.  Forward: at step k every lane subtracts L_ik y_k (zero unless i > k), so lane k's b
+// stops changing once y_k = b_k / L_kk is broadcast, and y = b / L_ii at the end.
 template <int NV, typename T>
 __device__ __forceinline__ T chol_solve(const T (&L)[NV], T dinv, T b, int sl) {
   static_for<0, NV>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
-    const int sl_k = opaque_v(sl);
-    T yk = bcast<k>(b * dinv);
-    b = (sl_k > k) ? b - L[k] * yk : b;
-    b = (sl_k == k) ? yk : b;
+    b = fma(-L[k], bcast<k>(b * dinv), b);
   });
+  b *= dinv;
+  // back substitution x_k = (y_k - sum_{i>k} L_ik x_i) / L_kk in blocks of BS columns, top block
+  // first: the sums over the rows below the block are BS independent half-wave sums (their latencies
+  // overlap), the block's own rows follow as a short chain of broadcasts of L_ik x_i from lane i
+  constexpr int BS = 3;
   T x = 0;
-  static_for<0, NV>([&](auto kc) {
-    constexpr int k = NV - 1 - decltype(kc)::value;
+  static_for<0, (NV + BS - 1) / BS>([&](auto bc) {
+    constexpr int hi = NV - BS * decltype(bc)::value;        // block = columns [lo, hi)
+    constexpr int lo = hi - BS > 0 ? hi - BS : 0;
     const int sl_k = opaque_v(sl);
-    T part = (sl_k > k && sl_k < NV) ? L[k] * x : T(0);
-    T ssum = hsum(part);
-    T xk = bcast<k>((b - ssum) * dinv);
-    x = (sl_k == k) ? xk : x;
+    T ssum[BS];
+    static_for<lo, hi>([&](auto cc) {
+      constexpr int c = decltype(cc)::value;
+      ssum[c - lo] = hsum(L[c] * x);                           // x = 0 on lanes < hi still
+    });
+    static_for<0, hi - lo>([&](auto tc) {
+      constexpr int c = hi - 1 - decltype(tc)::value;         // top of the block down
+      T xc = (b - ssum[c - lo]) * dinv;                      // lane c's value is x_c
+      x = (sl_k == c) ? xc : x;
+      static_for<lo, c>([&](auto dc) {                       // lane c's L_cd x_c to the block's lanes d < c
+        constexpr int d = decltype(dc)::value;
+        ssum[d - lo] += bcast<c>(L[d] * x);
+      });
+    });
   });
   return x;
+}
+// forward substitution y = L^-1 b for G right-hand sides at once (sub-lane i holds b_i of each; the
+// G broadcast chains are independent, so their latencies overlap); returns y_i in place (0 on
+// sub-lanes >= NV, where dinv = 0)
+template <int NV, int G, typename T>
+__device__ __forceinline__ void chol_fwd_multi(const T (&L)[NV], T dinv, T (&b)[G], int sl) {
+  static_for<0, NV>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    static_for<0, G>([&](auto gc) {
+      constexpr int g = decltype(gc)::value;
+      b[g] = fma(-L[k], bcast<k>(b[g] * dinv), b[g]);
+    });
+  });
+  static_for<0, G>([&](auto gc) { b[decltype(gc)::value] *= dinv; });
+}
+template <int NV, typename T>
+__device__ __forceinline__ T chol_fwd(const T (&L)[NV], T dinv, T b, int sl) {
+  T bb[1] = {b};
+  chol_fwd_multi<NV, 1>(L, dinv, bb, sl);
+  return bb[0];
 }
 // (A v)_i for a row-per-lane matrix and a vector in LDS (broadcast ds_reads)
 template <int NV, typename T>
@@ -390,14 +452,28 @@ struct Scratch {
 };
 
 // PGS solver scratch (the <option solver="PGS"> kernel instance only; the Newton instance never
-// allocates it): rows [0, PGS_CACHE) keep J_r and M^-1 J_r' per dof, every row its AR_rr and aref
-constexpr int PGS_CACHE = 32;
+// allocates it).  With M = L L', row r's u_r = L^-1 J_r' (one nv-vector per row) gives the whole dual:
+// AR = J M^-1 J' + R has AR_ik = u_i . u_k + R_i [i == k], and J_r qacc = u_r . (L' qacc).  Rows
+// [0, NC) keep u_r in LDS (later rows rebuild it per use); every row keeps b_r = -aref_r, R_r, AR_rr,
+// 1 / AR_rr and its lookahead Gram terms.
+// Row sweep lookahead: row r's residual u_r . z is started PGS_LA rows early, on a z that still lacks the
+// updates of rows r-PGS_LA .. r-1, and corrected with delta_{r-j} (u_r . u_{r-j}) when row r's turn
+// comes (the Gram terms G_rj are computed once per substep).  The half-wave sum thus leaves the
+// serial chain, which shrinks to a few scalar FMAs per row.
+constexpr int PGS_LA = 3;
+// cached rows: 40 in fp32 keep the resident PGS instance at 4 workgroups per CU; fp64 (48) runs at 2
+template <typename T>
+constexpr int pgs_cache_rows() { return sizeof(T) == 4 ? 40 : 48; }
+template <typename T>
+struct alignas(4 * sizeof(T)) PgsRow {
+  T b, R, ar, ai;                 // -aref_r, R_r, AR_rr, 1 / max(AR_rr, MINVAL)
+  T g[4];                         // G_rj = u_r . u_{r-j}, j = 1..PGS_LA (0 past the first row)
+};
 template <typename T, typename C>
 struct PgsCache {
-  T J[PGS_CACHE][MAXDOF];
-  T MJ[PGS_CACHE][MAXDOF];
-  T AR[C::EFC];
-  T ar[C::EFC];
+  static constexpr int NC = pgs_cache_rows<T>();
+  T u[NC][MAXDOF];
+  PgsRow<T> row[C::EFC];
 };
 
 // ------------------------------------------------------------------ narrow phase
@@ -1186,8 +1262,8 @@ struct Stepper {
           K = -sr[0] / (dmax * dmax);
           B = -sr[1] / dmax;
         }
-        T R = rscale * fmax(T(1e-15), (1 - imp) * dA / imp);
-        D[q] = T(1) / R;
+        T R = rscale * fmax(T(1e-15), (1 - imp) * dA * recip(imp));
+        D[q] = recip(R);
         s.row_D[r] = D[q];
         ar[q] = -B * row_Jx(m, s, rd[q], rc[q]) - K * imp * (pos - margin);
       }
@@ -1363,7 +1439,7 @@ struct Stepper {
             lsdone = true;
           } else {
             if (d1 < 0) lo = alpha; else hi = alpha;
-            T an = d2 > 0 ? alpha - d1 / d2 : T(-1);
+            T an = d2 > 0 ? alpha - d1 * recip(d2) : T(-1);
             if (!(an > lo && an < hi)) an = hi < T(1e29) ? T(0.5) * (lo + hi) : T(2) * alpha;
             if (hi - lo <= (sizeof(T) == 8 ? T(1e-14) : T(1e-6)) * hi) lsdone = true;
             else alpha = an;
@@ -1424,77 +1500,114 @@ struct Stepper {
 
   // mj_solPGS (<option solver="PGS">), restating oracle/hsim_oracle.c solve_pgs: projected
   // Gauss-Seidel on the dual  min 0.5 f'AR f + f'b, f >= 0  (AR = J M^-1 J' + R, b = J qacc_smooth -
-  // aref), rows swept in efc order.  Without forming AR: qacc = qacc_smooth + M^-1 J' f is kept
-  // per dof lane, so a row's residual is J_r qacc + R_r f_r - aref_r (one half-wave sum) and its
-  // update adds delta M^-1 J_r' to qacc.  M is factored once (row-per-lane Cholesky); J_r and
-  // M^-1 J_r' of the first PGS_CACHE rows are kept in LDS, later rows are rebuilt per sweep.
-  // Warm start: the forces of qacc_warmstart under the primal map, kept if their dual cost is
-  // negative.  Stops when a sweep's improvement * scale < tolerance, or after maxit sweeps.
+  // aref), rows swept in efc order, MuJoCo's stopping rule (a sweep's improvement * scale <
+  // tolerance, or maxit sweeps).  Without forming AR (see PgsCache): with z = L' qacc = L^-1
+  // (qfrc_smooth + J'f) kept per dof lane, row r's dual residual is  u_r . z + R_r f_r - aref_r  (z is
+  // the NET acceleration in the factor's basis, so fp32 sums do not cancel two large terms) and its
+  // update adds delta u_r to z.  The half-wave sum u_r . z runs PGS_LA rows ahead (see PGS_LA).
+  // u_r = L^-1 J_r' of the cached rows comes from one multi-right-hand-side forward substitution per
+  // substep.  Warm start: the forces of qacc_warmstart under the primal map, kept if their dual cost
+  // is not positive.  z is re-anchored on the forces every 8 sweeps (fp32 rounding drift); the final
+  // qacc = M^-1 (qfrc_smooth + J'f) comes from the final forces.
   __device__ __forceinline__ void solve_pgs(T xws, int maxit, const T (&D)[C::RPL], const T (&ar)[C::RPL],
                                             const int (&rd)[C::RPL], const T (&rc)[C::RPL], PgsCache<T, C>& pc) {
     phase_begin();
     const int nefc = s.nefc;
     const uint32_t bch = chain_mask(m, sl, nb);
+    const T fs = sl < NV ? fsmooth : T(0);
+    constexpr int NC = PgsCache<T, C>::NC;
+    constexpr int LA = PGS_LA;
     bool vr[C::RPL];
 #pragma unroll
-    for (int q = 0; q < C::RPL; q++) {
-      vr[q] = sl + HL * q < nefc;
-      if (vr[q]) pc.ar[sl + HL * q] = ar[q];
-    }
+    for (int q = 0; q < C::RPL; q++) vr[q] = sl + HL * q < nefc;
     T L[NV];
 #pragma unroll
     for (int j = 0; j < NV; j++) L[j] = Mr[j];
     T dinv = 0;
     chol_rows<NV>(L, dinv, sl, s.u.n.cb);
-    const T qs = chol_solve<NV>(L, dinv, sl < NV ? fsmooth : T(0), sl);     // qacc_smooth
-    // warm start: f = -D (J xws - aref)_-, kept only if its dual cost is negative
+    // warm start: f = -D (J xws - aref)_-;  per-row b_r = -aref_r, R_r
     if (sl < NV) s.vx[sl] = xws;
     WSYNC();
     map_vx<NV>(s, sl, nb, bch);
-    T f[C::RPL];
+    T wc = 0;     // this lane's rows' part of the warm start's dual cost: sum f (0.5 R f - aref)
 #pragma unroll
     for (int q = 0; q < C::RPL; q++) {
-      T jar = vr[q] ? row_Jx(m, s, rd[q], rc[q]) - ar[q] : T(0);
-      f[q] = jar < 0 ? -D[q] * jar : T(0);
-      if (vr[q]) s.row_f[sl + HL * q] = f[q];
+      const int r = sl + HL * q;
+      if (vr[q]) {
+        const T jar = row_Jx(m, s, rd[q], rc[q]) - ar[q];
+        const T f = jar < 0 ? -D[q] * jar : T(0);
+        const T R = recip(D[q]);
+        s.row_f[r] = f;
+        pc.row[r].b = -ar[q];
+        pc.row[r].R = R;
+        wc += f * (T(0.5) * R * f - ar[q]);
+      }
     }
     WSYNC();
+    // rows that exist in either half of the wave (wave-uniform loop bounds)
+    int maxr = nefc;
+    maxr = max(maxr, __shfl_xor(maxr, HL));
+    // u_r of the cached rows (G right-hand sides per forward substitution)
+    constexpr int G = sizeof(T) == 8 ? 4 : 8;
+    const int ncache = maxr < NC ? maxr : NC;
+    for (int r0 = 0; r0 < ncache; r0 += G) {
+      T y[G];
+      static_for<0, G>([&](auto gc) {
+        constexpr int g = decltype(gc)::value;
+        y[g] = r0 + g < nefc ? row_J_lane(r0 + g) : T(0);
+      });
+      chol_fwd_multi<NV, G>(L, dinv, y, sl);
+      static_for<0, G>([&](auto gc) {
+        constexpr int g = decltype(gc)::value;
+        if (r0 + g < NC) pc.u[r0 + g][sl] = sl < NV ? y[g] : T(0);   // MAXDOF == HL: a slot per sub-lane
+      });
+    }
+    WSYNC();
+    // u_r of any row (LDS cache, or rebuilt for rows past it; 0 past the half's rows)
+    auto urow = [&](int r) -> T {
+      if (r < NC) return pc.u[r][sl];
+      T y = chol_fwd<NV>(L, dinv, r < nefc ? row_J_lane(r) : T(0), sl);
+      return sl < NV ? y : T(0);
+    };
+    // AR_rr = |u_r|^2 + R_r and the lookahead Gram terms of every row
+    {
+      T uw[LA + 1];     // u_{r-LA} .. u_r
+#pragma unroll
+      for (int j = 0; j < LA; j++) uw[j] = 0;
+      for (int r = 0; r < maxr; r++) {
+        uw[LA] = urow(r);
+        const T a = hsum(uw[LA] * uw[LA]);
+        T gr[LA];
+#pragma unroll
+        for (int j = 1; j <= LA; j++) gr[j - 1] = hsum(uw[LA] * uw[LA - j]);
+        if (r < nefc && sl == 0) {
+          const T arr = a + pc.row[r].R;
+          pc.row[r].ar = arr;
+          pc.row[r].ai = recip(arr < T(1e-15) ? T(1e-15) : arr);
+#pragma unroll
+          for (int j = 0; j < LA; j++) pc.row[r].g[j] = gr[j];
+        }
+#pragma unroll
+        for (int j = 0; j < LA; j++) uw[j] = uw[j + 1];
+      }
+    }
+    WSYNC();
+    // y0 = L^-1 qfrc_smooth and z = L^-1 (qfrc_smooth + J'f) of the warm-start forces
     contact_aggregates(m, s, sl);
-    const T y = sl < NV ? jtf_lane(m, s, sl, cd) : T(0);
-    T z = chol_solve<NV>(L, dinv, y, sl);                                   // M^-1 J' f
-    if (sl >= NV) z = 0;
-    if (sl < NV) s.vx[sl] = z;
-    WSYNC();
-    map_vx<NV>(s, sl, nb, bch);
-    T c = 0, jz[C::RPL];
-#pragma unroll
-    for (int q = 0; q < C::RPL; q++) jz[q] = vr[q] ? row_Jx(m, s, rd[q], rc[q]) : T(0);
-    WSYNC();
-    if (sl < NV) s.vx[sl] = qs;
-    WSYNC();
-    map_vx<NV>(s, sl, nb, bch);
-#pragma unroll
-    for (int q = 0; q < C::RPL; q++)
-      if (vr[q]) c += f[q] * (T(0.5) * jz[q] + T(0.5) * f[q] / D[q] + row_Jx(m, s, rd[q], rc[q]) - ar[q]);
-    const bool keep = hsum(c) <= T(0);
-    T x = sl < NV ? (keep ? qs + z : qs) : T(0);
-    if (!keep) {
+    T z, y0;
+    {
+      T y2[2] = {fs, fs + (sl < NV ? jtf_lane(m, s, sl, cd) : T(0))};
+      chol_fwd_multi<NV, 2>(L, dinv, y2, sl);
+      y0 = sl < NV ? y2[0] : T(0);
+      z = sl < NV ? y2[1] : T(0);
+    }
+    // keep the warm start only if its dual cost 0.5 f'AR f + f'b = 0.5 |z|^2 - 0.5 |y0|^2 +
+    // sum f (0.5 R f - aref) is not positive
+    if (hsum(wc + T(0.5) * (z * z - y0 * y0)) > T(0)) {
 #pragma unroll
       for (int q = 0; q < C::RPL; q++)
         if (vr[q]) s.row_f[sl + HL * q] = 0;
-    }
-    // rows that exist in either half of the wave (wave-uniform loop bound)
-    int maxr = nefc;
-    maxr = max(maxr, __shfl_xor(maxr, HL));
-    // per-row AR_rr (and the cached J_r, M^-1 J_r')
-    for (int r = 0; r < maxr; r++) {
-      const bool live = r < nefc;
-      T jr = live ? row_J_lane(r) : T(0);
-      T mj = chol_solve<NV>(L, dinv, jr, sl);
-      if (sl >= NV) mj = 0;
-      const T a = hsum(jr * mj) + (live ? T(1) / s.row_D[r] : T(0));
-      if (r < PGS_CACHE && sl < MAXDOF) { pc.J[r][sl] = jr; pc.MJ[r][sl] = mj; }
-      if (live && sl == 0) pc.AR[r] = a;
+      z = y0;
     }
     WSYNC();
     const T scale = m->newton_scale, tol = m->pgs_tol;
@@ -1504,43 +1617,93 @@ struct Stepper {
       m = opaque(m);
       sl = opaque_v(sl);
       T improvement = 0;
-      for (int r = 0; r < maxr; r++) {
-        const bool live = r < nefc && !done;
-        T jr, mj;
-        if (r < PGS_CACHE) {
-          jr = sl < MAXDOF ? pc.J[r][sl] : T(0);
-          mj = sl < MAXDOF ? pc.MJ[r][sl] : T(0);
-        } else {
-          jr = r < nefc ? row_J_lane(r) : T(0);
-          mj = chol_solve<NV>(L, dinv, jr, sl);
-          if (sl >= NV) mj = 0;
+      // ring registers (slot = row mod RING, RING = LA + 1; the row loop is unrolled by RING so every
+      // slot index is a compile-time constant and the pipeline shifts no registers):
+      // U[slot] = u_row, S[slot] = u_row . z_{row-LA-1} (z with rows < row-LA applied),
+      // Dl[slot] = delta_row.  At row r, z still lacks row r-1's update.  Positions past maxr are
+      // phantom rows (u = 0, delta = 0).
+      // LDS operands are loaded one row before their use (P/F: row r+1's scalars and force, un: u of
+      // row r+LA+1), so no row waits on an LDS round trip (a wave issues in order: a load consumed
+      // in the same row would stall it for the full LDS latency); loads are unconditional (clamped
+      // index, masked value) so the row step has no divergent branch.
+      // FAST: every row of both halves is in the u cache (the common case), no rebuild path.
+      auto sweep_rows = [&](auto fastc) {
+        constexpr bool FAST = decltype(fastc)::value;
+        auto uget = [&](int r) -> T {
+          if constexpr (FAST) return pc.u[r][sl];
+          else return urow(r);
+        };
+        constexpr int RING = LA + 1;
+        static_assert(RING % 2 == 0, "P/F double buffer alternates with the row parity");
+        T U[RING], S[RING], Dl[RING];
+#pragma unroll
+        for (int i = 0; i < RING; i++) {
+          U[i] = (i < LA && i < maxr) ? uget(i) : T(0);
+          S[i] = i < LA ? hsum(U[i] * z) : T(0);
+          Dl[i] = 0;
         }
-        const T fr = r < nefc ? s.row_f[r] : T(0);
-        const T Dr = r < nefc ? s.row_D[r] : T(1);
-        const T arr = r < nefc ? pc.AR[r] : T(1);
-        const T res = hsum(jr * x) + fr / Dr - (r < nefc ? pc.ar[r] : T(0));
-        T nf = fr - res / (arr < T(1e-15) ? T(1e-15) : arr);
-        nf = nf < T(0) ? T(0) : nf;
-        const T delta = live ? nf - fr : T(0);
-        x += delta * mj;
-        improvement -= delta * res + T(0.5) * arr * delta * delta;
-        if (live && sl == 0) s.row_f[r] = nf;
-      }
+        PgsRow<T> P[2];
+        T F[2];
+        P[0] = pc.row[0];
+        F[0] = nefc > 0 ? s.row_f[0] : T(0);
+        T unext = LA < maxr ? uget(LA) : T(0);
+        for (int r0 = 0; r0 < maxr; r0 += RING) {
+          static_for<0, RING>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            constexpr int prev = (i + RING - 1) % RING;   // slot of row r-1 (and of row r+LA)
+            constexpr int cur = i & 1, nxt = cur ^ 1;
+            const int r = r0 + i;
+            {   // next row's operands
+              const int rn = r + 1 < C::EFC ? r + 1 : C::EFC - 1;
+              P[nxt] = pc.row[rn];
+              const T fl = s.row_f[rn];
+              F[nxt] = r + 1 < nefc ? fl : T(0);
+            }
+            const T un = unext;                          // u_{r+LA}
+            unext = r + LA + 1 < maxr ? uget(r + LA + 1) : T(0);
+            z = fma(Dl[prev], U[prev], z);               // z_{r-1}: rows < r applied
+            const T Sn = hsum(un * z);                   // start row r+LA's sum on z_{r-1}
+            const bool row = r < nefc;
+            const bool live = row && !done;
+            const PgsRow<T>& pr = P[cur];
+            const T fr = F[cur];
+            T dot = S[i];
+            static_for<1, LA + 1>([&](auto jc) {         // corrections for rows r-1 .. r-LA
+              constexpr int j = decltype(jc)::value;
+              dot = fma(Dl[(i + RING - j) % RING], pr.g[j - 1], dot);
+            });
+            const T res = dot + (pr.b + pr.R * fr);
+            T nf = fr - res * pr.ai;
+            nf = nf < T(0) ? T(0) : nf;
+            const T delta = live ? nf - fr : T(0);
+            const T di = delta * res + T(0.5) * pr.ar * delta * delta;
+            improvement -= row ? di : T(0);
+            if (live && sl == 0) s.row_f[r] = nf;
+            U[prev] = un;                                // row r+LA takes row r-1's slot
+            S[prev] = Sn;
+            Dl[i] = delta;
+          });
+        }
+        z = fma(Dl[RING - 1], U[RING - 1], z);           // the last position's update (0 if phantom)
+      };
+      if (maxr <= NC) sweep_rows(std::true_type{});
+      else sweep_rows(std::false_type{});
       if (!done) it++;
       done = done || (improvement * scale < tol);
       if (__ballot(!done) == 0) break;
-      // re-anchor qacc = qacc_smooth + M^-1 J' f on the current forces once per sweep: the
-      // incremental updates accumulate rounding (fp32 PGS drifts over thousands of sweeps)
-      WSYNC();
-      contact_aggregates(m, s, sl);
-      T zz = chol_solve<NV>(L, dinv, sl < NV ? jtf_lane(m, s, sl, cd) : T(0), sl);
-      x = sl < NV ? qs + zz : T(0);
+      if ((sweep & 7) == 7) {          // re-anchor z on the current forces
+        WSYNC();
+        contact_aggregates(m, s, sl);
+        const T zz = chol_fwd<NV>(L, dinv, fs + (sl < NV ? jtf_lane(m, s, sl, cd) : T(0)), sl);
+        z = sl < NV ? zz : T(0);
+      }
     }
     niter = it;
     WSYNC();
     contact_aggregates(m, s, sl);
     fcon = sl < NV ? jtf_lane(m, s, sl, cd) : T(0);
-    qacc = sl < NV ? x : T(0);
+    const T qa = chol_solve<NV>(L, dinv, fs + fcon, sl);     // M^-1 (qfrc_smooth + J'f)
+    qacc = sl < NV ? qa : T(0);
     WSYNC();
   }
 

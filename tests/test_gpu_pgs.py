@@ -5,7 +5,8 @@ The reference's humanoid.xml runs MuJoCo's default Newton solver, so PGS is an o
 (BASELINE.json's north star names a PGS contact solve).  Tolerances, fp64 kernel:
   * PGS vs oracle PGS, one substep, sweeps run to convergence: |d qacc| <= 1e-7 scale
   * PGS vs the engine's Newton on the same states (both converged): |d qacc| <= 1e-6 scale
-fp32 kernel: |d qacc| <= 2e-3 scale against the fp64 oracle (the Newton fp32 bound)."""
+fp32 kernel (MuJoCo's default 100 sweeps / 1e-8): |d qacc| <= 2e-3 scale against the fp64 oracle (the
+Newton fp32 bound)."""
 import re
 
 import numpy as np
@@ -24,13 +25,15 @@ def _pgs_xml(tmp_path, iterations, tolerance):
     return str(p)
 
 
-def _contact_states(M, n, seed):
+def _contact_states(M, n, seed, deep=False):
+    """Keyframes pushed into the floor; ``deep``: every other round 3 cm deeper (prone / supine then
+    have ~118 constraint rows, past the PGS instance's LDS row cache of 56 / 64)."""
     rng = np.random.default_rng(seed)
     keys = list(M["keyframes"].values())
     out = []
     for i in range(n):
         q = keys[i % len(keys)].copy()
-        q[2] -= 0.002 * (1 + i // len(keys))
+        q[2] -= 0.002 * (1 + i // len(keys)) + (0.03 if deep and (i // len(keys)) % 2 == 1 else 0.0)
         q[7:] += rng.uniform(-0.05, 0.05, 21)
         out.append((q, rng.normal(0, 0.5, 27), rng.uniform(-1, 1, 21).astype(np.float32)))
     return out
@@ -61,11 +64,14 @@ def _oracle_one_substep(o, q, v, c):
 def test_pgs_kernel_matches_oracle_pgs(tmp_path, prec):
     from mujocoposelearning_amd.model import HsModel
     from oracle.oracle import Oracle
-    # fp64: sweeps to convergence; fp32: MuJoCo-like settings (rounding noise stops fp32 short of 1e-20)
-    xml = _pgs_xml(tmp_path, 3000, 1e-20) if prec == "fp64" else _pgs_xml(tmp_path, 300, 1e-12)
+    # fp64: sweeps to convergence; fp32: MuJoCo's defaults (100 sweeps, tolerance 1e-8).  Run far past
+    # them, fp32 rounding noise drives the forces along the pyramid's null directions (the 4 edge
+    # rows of a contact span 3 dimensions; only the tiny R regularises that direction) until their
+    # cancellation in J'f costs the qacc its accuracy -- fp32 PGS is a MuJoCo-defaults mode
+    xml = _pgs_xml(tmp_path, 3000, 1e-20) if prec == "fp64" else _pgs_xml(tmp_path, 100, 1e-8)
     m, o = HsModel(xml), Oracle(xml)
     assert m.field("opt_solver")[0] == 1 and o.m.solver == 1
-    states = _contact_states(o.M, 24, seed=11)
+    states = _contact_states(o.M, 24, seed=11, deep=prec == "fp64")
     st, aux = _gpu_one_substep(m, states, prec)
     rows = 0
     for i, (q, v, c) in enumerate(states):
@@ -80,8 +86,9 @@ def test_pgs_kernel_matches_oracle_pgs(tmp_path, prec):
         else:
             assert np.abs(aux[i, :27] - ra).max() <= 2e-3 * scale, (i, np.abs(aux[i, :27] - ra).max(), scale)
             assert np.abs(st["qvel"][i] - rv).max() <= 1e-5 * scale, i
-    assert rows > 24 * 10       # contact-rich states (the PGS row loop is exercised past PGS_CACHE too)
-    assert int(aux[:, 36].max()) > 32
+    assert rows > 24 * 10       # contact-rich states
+    # fp64: rows past the LDS row cache (u_r rebuilt per use) are exercised too
+    assert int(aux[:, 36].max()) > (64 if prec == "fp64" else 32)
 
 
 def test_pgs_kernel_converges_to_newton_kernel(tmp_path):
