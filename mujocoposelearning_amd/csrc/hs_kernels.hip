@@ -218,17 +218,11 @@ template <typename T>
 __device__ __forceinline__ T rsqrt_t(T x);
 template <>
 __device__ __forceinline__ float rsqrt_t<float>(float x) { return __builtin_amdgcn_rsqf(x); }
-// fp64: v_rsq_f64 (about half precision) + two Newton steps y += y (1 - x y^2) / 2 -- 7 dependent
-// FMAs/MULs instead of the correctly rounded sqrt expansion followed by a correctly rounded divide
-// (~25); within 1-2 ulp of 1/sqrt(x) for the positive, normal arguments it is used on
+// fp64: the correctly rounded 1 / sqrt(x).  (Measured alternative: v_rsq_f64 + two Newton steps is
+// SLOWER in the step kernel -- 305k vs 298k cycles per env substep, the Cholesky pivots dominating --
+// so the fp64 engine keeps the exact form.)
 template <>
-__device__ __forceinline__ double rsqrt_t<double>(double x) {
-  double y = __builtin_amdgcn_rsq(x);
-  double e = fma(-x * y, y, 1.0);
-  y = fma(0.5 * y, e, y);
-  e = fma(-x * y, y, 1.0);
-  return fma(0.5 * y, e, y);
-}
+__device__ __forceinline__ double rsqrt_t<double>(double x) { return 1.0 / sqrt(x); }
 // 1/x: fp32 is v_rcp_f32 under -fno-hip-fp32-correctly-rounded-divide-sqrt; fp64 is v_rcp_f64 +
 // two Newton steps (within 1-2 ulp of the correctly rounded divide, for normal nonzero x)
 __device__ __forceinline__ float recip(float x) { return 1.0f / x; }
@@ -1691,7 +1685,8 @@ struct Stepper {
       if (!done) it++;
       done = done || (improvement * scale < tol);
       if (__ballot(!done) == 0) break;
-      if ((sweep & 7) == 7) {          // re-anchor z on the current forces
+      // re-anchor z on the current forces (fp32: every 8 sweeps; fp64 drifts ~1e-16 per update)
+      if ((sweep & (sizeof(T) == 8 ? 31 : 7)) == (sizeof(T) == 8 ? 31 : 7)) {
         WSYNC();
         contact_aggregates(m, s, sl);
         const T zz = chol_fwd<NV>(L, dinv, fs + (sl < NV ? jtf_lane(m, s, sl, cd) : T(0)), sl);

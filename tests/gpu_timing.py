@@ -3,7 +3,8 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["HSIM_LIB"] = os.path.join(ROOT, "mujocoposelearning_amd", "libhsim_timing.so")
+os.environ["HSIM_LIB"] = os.environ.get("HSIM_TIMING_LIB",
+                                        os.path.join(ROOT, "mujocoposelearning_amd", "libhsim_timing.so"))
 sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
