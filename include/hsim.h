@@ -83,7 +83,14 @@ typedef struct {
   double kneel_params[9];  /* reward_functions.py:71-81: target_height, min_height, max_roll_pitch,
                               com_radius, energy_weight, posture_weight, com_weight, foot_weight,
                               alive_weight */
+  int schedule;            /* HS_SCHED_*: how the step kernel maps env pairs to waves [AUTO] */
 } hs_env_config;
+
+/* hs_env_config.schedule.  AUTO: one wave per env pair when every pair fits on the GPU at once,
+ * else (the fp64 engine at 4096 envs) a persistent grid that runs each env step as two chunk items
+ * (substeps [0, frame_skip - 1), then the last substep + obs / reward / auto-reset) from a queue.
+ * DIRECT: always one wave per pair.  Results are bitwise identical either way. */
+enum { HS_SCHED_AUTO = 0, HS_SCHED_DIRECT = 1 };
 
 /* Device buffers of a batch (row-major, env-major).  Element type of the T* entries is float
  * (HS_FP32) or double (HS_FP64). */
@@ -111,6 +118,10 @@ typedef struct {
 
 typedef struct {
   int n_envs, precision, nq, nv, nu, nbody, obs_dim, elem_size;
+  /* per-env contact / constraint-row capacity of the resident kernel tier (every launch) and of the
+   * wide tier that re-runs the envs overflowing it; only wide-tier overflow drops contacts
+   * (HS_WARN_OVERFLOW).  MuJoCo has no per-env cap (custom_env.py:160). */
+  int resident_con, resident_efc, wide_con, wide_efc;
 } hs_batch_info;
 
 hs_model* hs_model_load(const char* xml_path, char* err, int errsz);

@@ -18,13 +18,15 @@ HS_REWARD_NONE, HS_REWARD_STAND, HS_REWARD_KNEELING, HS_REWARD_WALK = -1, 0, 1, 
 HS_NWARN = 4
 HS_AUXDIM = 40
 HS_OUT_AUX, HS_OUT_CTRL = 1, 2   # hs_env_config.outputs bits
-DBGDIM = 16384
+HS_SCHED_AUTO, HS_SCHED_DIRECT = 0, 1   # hs_env_config.schedule
+DBGDIM = 32768
 
 
 class hs_env_config(C.Structure):
     _fields_ = [("frame_skip", C.c_int), ("max_steps", C.c_int), ("reward_id", C.c_int), ("autoreset", C.c_int),
                 ("max_newton", C.c_int), ("outputs", C.c_int), ("duration", C.c_double),
-                ("init_height", C.c_double), ("noise_scale", C.c_double), ("kneel_params", C.c_double * 9)]
+                ("init_height", C.c_double), ("noise_scale", C.c_double), ("kneel_params", C.c_double * 9),
+                ("schedule", C.c_int)]
 
 
 class hs_buffers(C.Structure):
@@ -35,7 +37,8 @@ class hs_buffers(C.Structure):
 
 
 class hs_batch_info(C.Structure):
-    _fields_ = [(n, C.c_int) for n in ("n_envs", "precision", "nq", "nv", "nu", "nbody", "obs_dim", "elem_size")]
+    _fields_ = [(n, C.c_int) for n in ("n_envs", "precision", "nq", "nv", "nu", "nbody", "obs_dim", "elem_size",
+                                       "resident_con", "resident_efc", "wide_con", "wide_efc")]
 
 
 _LIB = None

@@ -75,6 +75,11 @@ class HsBatch:
         self._free = False
         self.cfg = _lib.hs_env_config()
         check(lib().hs_get_config(self._h, C.byref(self.cfg)))
+        info = _lib.hs_batch_info()
+        check(lib().hs_batch_get_info(self._h, C.byref(info)))
+        # per-env (contacts, constraint rows) of the resident kernel tier and of the wide re-run tier
+        self.resident_capacity = (info.resident_con, info.resident_efc)
+        self.wide_capacity = (info.wide_con, info.wide_efc)
 
     # -- tensors (device views, valid until the next call) ---------------------------------
     def __getattr__(self, name):
@@ -89,8 +94,12 @@ class HsBatch:
 
     # -- configuration ---------------------------------------------------------------------
     def configure(self, frame_skip=None, duration=None, reward_id=None, max_steps=None, autoreset=None,
-                  max_newton=None, init_height=None, noise_scale=None, kneel_params=None, aux=None, ctrl=None):
-        """``aux`` / ``ctrl``: write the optional aux row (qacc, subtree com, contact / row counts,
+                  max_newton=None, init_height=None, noise_scale=None, kneel_params=None, aux=None, ctrl=None,
+                  schedule=None):
+        """``schedule``: "auto" (default; a chunk queue when the env pairs outnumber the resident
+        waves, see include/hsim.h HS_SCHED_AUTO) or "direct" (one wave per env pair); results are
+        bitwise identical.
+        ``aux`` / ``ctrl``: write the optional aux row (qacc, subtree com, contact / row counts,
         solver iterations) and the data.ctrl copy at every commit (both on by default; data views,
         host rewards and statistics read them, the on-device trainer does not)."""
         c = self.cfg
@@ -98,6 +107,8 @@ class HsBatch:
             c.outputs = (c.outputs & ~_lib.HS_OUT_AUX) | (_lib.HS_OUT_AUX if aux else 0)
         if ctrl is not None:
             c.outputs = (c.outputs & ~_lib.HS_OUT_CTRL) | (_lib.HS_OUT_CTRL if ctrl else 0)
+        if schedule is not None:
+            c.schedule = {"auto": _lib.HS_SCHED_AUTO, "direct": _lib.HS_SCHED_DIRECT}[schedule]
         if frame_skip is not None:
             c.frame_skip = int(frame_skip)
         if duration is not None:

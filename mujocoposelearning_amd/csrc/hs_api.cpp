@@ -27,6 +27,8 @@ struct hs_batch {
   const void* ar_qvel_noise = nullptr;
   int* redo = nullptr;                       // wide-tier work list [2 + n] (kernel-managed)
   unsigned long long* redo_total = nullptr;  // cumulative wide-tier re-runs
+  void* mid = nullptr;                       // chunk-queue hand-off rows [n][MIDDIM] (kernel-managed)
+  int* qsync = nullptr;                      // chunk queue claim / exit counters, pair flags (qsync_words)
   hs_env_config cfg{};
 };
 
@@ -81,6 +83,8 @@ hs::EnvBuffers<T> env_buffers(const hs_batch* b) {
   e.term_total_reward = (T*)b->buf.terminal_total_reward;
   e.redo = b->redo;
   e.redo_total = b->redo_total;
+  e.mid = (T*)b->mid;
+  e.qsync = b->qsync;
   e.dbg = b->debug ? (T*)b->dbg : nullptr;
   return e;
 }
@@ -102,6 +106,7 @@ hs::StepParams params_of(const hs_batch* b, int mode, int nsub) {
   for (int k = 0; k < 9; k++) p.kneel[k] = b->cfg.kneel_params[k];
   p.solver = b->model->host.solver == 1 ? hs::SOLVER_PGS : hs::SOLVER_NEWTON;
   p.outputs = b->cfg.outputs;
+  p.schedule = b->cfg.schedule;
   return p;
 }
 
@@ -161,7 +166,8 @@ bool init_state(hs_batch* b) {
          (!b->buf.terminal_step_count || hip_ok(hipMemset(b->buf.terminal_step_count, 0, (size_t)N * 4), "init")) &&
          (!b->buf.terminal_total_reward || hip_ok(hipMemset(b->buf.terminal_total_reward, 0, (size_t)N * es), "init")) &&
          hip_ok(hipMemset(b->redo, 0, (size_t)(N + 2) * sizeof(int)), "init") &&
-         hip_ok(hipMemset(b->redo_total, 0, sizeof(unsigned long long)), "init");
+         hip_ok(hipMemset(b->redo_total, 0, sizeof(unsigned long long)), "init") &&
+         hip_ok(hipMemset(b->qsync, 0, hs::qsync_words(N) * sizeof(int)), "init");
 }
 
 template <typename T>
@@ -312,7 +318,12 @@ hs_batch* hs_batch_create(const hs_model* m, int n_envs, int device, uint64_t se
   }
   if (!hip_ok(hipMalloc(&b->dbg, hs::DBGDIM * 8), "hipMalloc(dbg)") ||
       !hip_ok(hipMalloc((void**)&b->redo, (N + 2) * sizeof(int)), "hipMalloc(redo)") ||
-      !hip_ok(hipMalloc((void**)&b->redo_total, sizeof(unsigned long long)), "hipMalloc(redo_total)")) {
+      !hip_ok(hipMalloc((void**)&b->redo_total, sizeof(unsigned long long)), "hipMalloc(redo_total)") ||
+      // chunk-queue hand-off rows and flags: UNCACHED device memory, so a hand-off between waves on
+      // different CUs / XCDs needs no L1 invalidate or L2 write-back (hs_kernels.hip step_pair)
+      !hip_ok(hipExtMallocWithFlags(&b->mid, N * hs::MIDDIM * es, hipDeviceMallocUncached), "hipMalloc(mid)") ||
+      !hip_ok(hipExtMallocWithFlags((void**)&b->qsync, hs::qsync_words((int)N) * sizeof(int), hipDeviceMallocUncached),
+              "hipMalloc(qsync)")) {
     hs_batch_destroy(b);
     return nullptr;
   }
@@ -336,6 +347,8 @@ void hs_batch_destroy(hs_batch* b) {
   if (b->dbg) (void)hipFree(b->dbg);
   if (b->redo) (void)hipFree(b->redo);
   if (b->redo_total) (void)hipFree(b->redo_total);
+  if (b->mid) (void)hipFree(b->mid);
+  if (b->qsync) (void)hipFree(b->qsync);
   delete b;
 }
 
@@ -347,6 +360,10 @@ int hs_batch_get_info(const hs_batch* b, hs_batch_info* out) {
   out->nq = h.nq; out->nv = h.nv; out->nu = h.nu; out->nbody = h.nbody;
   out->obs_dim = b->obs_dim;
   out->elem_size = b->precision == HS_FP64 ? 8 : 4;
+  out->resident_con = b->precision == HS_FP64 ? hs::MAXCON_F64 : hs::MAXCON;
+  out->resident_efc = b->precision == HS_FP64 ? hs::MAXEFC_F64 : hs::MAXEFC;
+  out->wide_con = hs::MAXCON_WIDE;
+  out->wide_efc = hs::MAXEFC_WIDE;
   return 0;
 }
 

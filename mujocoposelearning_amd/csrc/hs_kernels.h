@@ -9,7 +9,13 @@
 namespace hs {
 
 constexpr int AUXDIM = MAXDOF + 8;   // per env: qacc[nv], com[3], ncon, nefc, newton iters, solver flag
-constexpr int DBGDIM = 16384;        // stage dump (env 0 only) for parity debugging
+constexpr int DBGDIM = 32768;        // stage dump (env 0 only) for parity debugging
+// hand-off row of a queued env step (qpos, qvel, qacc_warmstart, time, warning counters)
+constexpr int MID_Q = 0, MID_V = MAXQ, MID_WS = MAXQ + MAXDOF, MID_TIME = MAXQ + 2 * MAXDOF, MID_W = MID_TIME + 1;
+constexpr int MIDDIM = MID_W + 7;
+// chunk-queue sync words (uncached device memory): claim counter, exit counter, per-pair flags
+constexpr int QS_HEAD = 0, QS_EXIT = 1, QS_FLAG = 2;
+constexpr size_t qsync_words(int n_envs) { return QS_FLAG + (size_t)((n_envs + 1) / 2); }
 
 enum StepMode { MODE_ENV_STEP = 0, MODE_RESET = 1, MODE_PHYSICS = 2 };
 enum RewardId { REWARD_NONE = -1, REWARD_STAND = 0, REWARD_KNEELING = 1, REWARD_WALK = 2 };
@@ -37,6 +43,8 @@ struct EnvBuffers {
   int* term_step_count;  // [N] or null: step_count of envs that auto-reset this step (SB3 final info)
   T* term_total_reward;  // [N] or null: their episode return
   int* redo;             // [2 + N] wide-tier work list: count, done counter, env ids (hs_batch owned)
+  T* mid;                // [N][MIDDIM] state between the chunks of a queued env step (hs_batch owned)
+  int* qsync;            // [qsync_words(N)] chunk queue: claim / exit counters, pair flags (hs_batch owned)
   unsigned long long* redo_total;   // cumulative number of wide-tier re-runs (diagnostics)
   T* dbg;                // [DBGDIM] or nullptr
 };
@@ -58,6 +66,8 @@ struct StepParams {
                          // com_w, foot_w, alive_w (reward_functions.py:71-81)
   int solver;            // SOLVER_NEWTON (MuJoCo default) or SOLVER_PGS: selects the kernel instance
   int outputs;           // OUT_* bits: optional per-env outputs written at commit
+  int schedule;          // HS_SCHED_AUTO (0) / HS_SCHED_DIRECT (1) (hs_env_config.schedule)
+  int queue;             // set by launch_step: 1 = chunk-queue schedule (persistent grid), 0 = one wave per pair
 };
 // optional outputs (hs_env_config.outputs): the aux row (qacc, subtree com, ncon, nefc, solver
 // iterations -- data views and stats) and the data.ctrl copy (data views / host rewards)

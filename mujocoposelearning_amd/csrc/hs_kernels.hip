@@ -39,15 +39,19 @@ static_assert(MAXDOF == HL, "one dof per sub-lane (lim_row slots, dof masks)");
 
 // Per-env contact / constraint-row capacity of a kernel instance (hs_model.h): the resident tier
 // every launch runs with and the wide tier that re-runs the (rare) envs overflowing it.
-template <int NCON, int NEFC>
+template <int NCON, int NEFC, bool W = false>
 struct Cap {
-  static constexpr int CON = NCON;        // contacts (CON / HL per lane)
+  static constexpr int CON = NCON;        // contacts (at most one slot per lane per HL-slot pass)
   static constexpr int EFC = NEFC;        // constraint rows
   static constexpr int RPL = NEFC / HL;   // rows per lane (kept in registers by the row's lane)
-  static_assert(NCON % HL == 0 && NEFC % HL == 0, "capacity in whole half-waves");
+  static constexpr bool WIDE = W;         // the wide (re-run) tier
+  static_assert((NCON % HL == 0 || HL % NCON == 0) && NEFC % HL == 0, "capacity in whole half-waves");
 };
-using Resident = Cap<MAXCON, MAXEFC>;
-using Wide = Cap<MAXCON_WIDE, MAXEFC_WIDE>;
+// resident tier per precision (hs_model.h): fp64 scratch is twice the size, so its tier is halved
+// in contacts to fit 5 workgroups (env pairs) per CU instead of 4
+template <typename T>
+using Resident = std::conditional_t<sizeof(T) == 8, Cap<MAXCON_F64, MAXEFC_F64>, Cap<MAXCON, MAXEFC>>;
+using Wide = Cap<MAXCON_WIDE, MAXEFC_WIDE, true>;
 
 // scheduling fence: keeps the machine scheduler from hoisting loads across iterations of fully
 // unrolled loops (which otherwise inflates VGPR pressure far past the occupancy target)
@@ -133,10 +137,15 @@ __device__ __forceinline__ uint32_t hballot(bool p, bool upper) {
 // Hide a (uniform) pointer's value from the optimiser.  The model pointer is const __restrict__,
 // so without this LICM hoists every per-lane model load (m->dof_bodyid[sl], ...) out of the
 // substep / Newton loops and keeps each one live in a VGPR for the whole kernel.
+// (The value is wave-uniform by construction; readfirstlane only tells the uniformity analysis so,
+// where control flow hides it -- e.g. across the chunk-queue loop -- and folds away otherwise.)
 template <typename P>
 __device__ __forceinline__ P opaque(P p) {
-  asm volatile("" : "+s"(p));
-  return p;
+  uint64_t v = (uint64_t)p;
+  uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  v = ((uint64_t)hi << 32) | lo;
+  asm volatile("" : "+s"(v));
+  return (P)v;
 }
 // The model lives in the constant address space: it is never written by the kernel, so reads at
 // a wave-uniform index become scalar loads (s_load via the scalar cache) even through an
@@ -745,8 +754,8 @@ __device__ __forceinline__ T jtf_lane(MPtr<T> m, const Scratch<T, C>& s, int sl,
 constexpr int NSLOT = 26;
 struct PhaseClock {
   uint64_t acc[NSLOT] = {0};
-  uint64_t prev = 0, t0 = 0;
-  __device__ __forceinline__ void start() { prev = t0 = __builtin_amdgcn_s_memtime(); }
+  uint64_t prev = 0, t0 = 0, rt0 = 0;   // rt0: s_memrealtime (100 MHz, one clock for all XCDs)
+  __device__ __forceinline__ void start() { prev = t0 = __builtin_amdgcn_s_memtime(); rt0 = __builtin_amdgcn_s_memrealtime(); }
   __device__ __forceinline__ void stamp(int slot) {
     uint64_t now = __builtin_amdgcn_s_memtime();
     uint64_t d = now - prev;
@@ -766,7 +775,15 @@ struct PhaseClock {
         for (int q = 0; q < NSLOT; q++) { atomicAdd(&dbg_[8000 + q], (T)st.clk.acc[q]); st.clk.acc[q] = 0; } \
       if (sl == 0) atomicAdd(&dbg_[8030], (T)tot_iter);                                          \
       if (lane == 0 && blockIdx.x < 2048) dbg_[9000 + blockIdx.x] = (T)(st.clk.prev - st.clk.t0);  \
+      if (lane == 0 && blockIdx.x < 2048) {                                                      \
+        dbg_[16384 + blockIdx.x] = (T)(uint32_t)(st.clk.rt0 & 0xFFFFFFu);                          \
+        dbg_[18432 + blockIdx.x] = (T)(uint32_t)(__builtin_amdgcn_s_memrealtime() & 0xFFFFFFu);    \
+      }                                                                                          \
       if (sl == 0 && blockIdx.x < 2048) dbg_[11100 + 2 * blockIdx.x + (up ? 1 : 0)] = (T)tot_iter;  \
+      if (lane == 0 && titem >= 0 && titem < 4096) {   /* queued items: realtime start / end */  \
+        dbg_[20480 + 2 * titem] = (T)(uint32_t)(st.clk.rt0 & 0xFFFFFFu);                            \
+        dbg_[20480 + 2 * titem + 1] = (T)(uint32_t)(__builtin_amdgcn_s_memrealtime() & 0xFFFFFFu);  \
+      }                                                                                          \
       tot_iter = 0;                                                                              \
     }                                                                                            \
   } while (0)
@@ -2000,11 +2017,19 @@ __device__ __forceinline__ void commit(MPtr<T> m, KPtr<T> k, const Stepper<T, NV
 // In the resident tier an env whose contacts / rows overflowed the resident capacity in any
 // substep is NOT committed: it is appended to the wide tier's work list instead, and the wide
 // launch that follows re-runs its whole step from the same (untouched) inputs.
+// Queued schedule (launch_step sets p.queue when the pairs outnumber the resident waves): the
+// pair's substeps [s0, s1) only.  A chunk that ends before the last substep hands the state over
+// through b.mid and sets the pair's flag := s1; the last-substep chunk waits for flag == s0 and
+// starts from that row.  b.mid and the flags live in UNCACHED device memory (hs_api.cpp), so the
+// stores are in memory once `s_waitcnt vmcnt(0)` returns and the consumer's loads cannot hit a
+// stale L1 / L2 line: no cache invalidate or write-back on either side.  Every chunk recomputes the whole mj_step
+// pipeline from (qpos, qvel, qacc_warmstart, time), so the hand-off is exact: results are bitwise
+// those of one wave running all substeps.
 template <typename T, int NV, bool PGS, typename C>
 __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCache<T, C>* pcache, int idx,
-                                          int nidx, const int* list) {
-  constexpr bool WIDE = C::CON > MAXCON;
-  const int lane = threadIdx.x;
+                                          int nidx, const int* list, int s0, int s1, int pair) {
+  constexpr bool WIDE = C::WIDE;
+  const int lane = opaque_v(threadIdx.x);   // (no lane-derived value hoisted out of the chunk-queue loop)
   const bool up = lane >= HL;
   const int sl = lane & (HL - 1);
   bool active = idx < nidx;                           // ghost half for an odd count
@@ -2024,11 +2049,28 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
   uint32_t episode;
   T total, act;
   {
-    time = ka->b.time[env_id];
-    xws = (sl < nv) ? ka->b.qacc_ws[(size_t)env_id * nv + sl] : T(0);
-    if (sl < nq) s.qpos[sl] = ka->b.qpos[(size_t)env_id * nq + sl];
-    if (sl + HL < nq) s.qpos[sl + HL] = ka->b.qpos[(size_t)env_id * nq + sl + HL];
-    if (sl < nv) s.qvel[sl] = ka->b.qvel[(size_t)env_id * nv + sl];
+    if (s0 > 0) {   // queued last substep: wait for the pair's first chunk to hand the state over
+      int* flag = ka->b.qsync + QS_FLAG + pair;
+      if (lane == 0)   // (bounded: a broken protocol shows up as wrong results, not a hung GPU)
+        for (int w = 0; w < (1 << 22) && __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != s0; w++)
+          __builtin_amdgcn_s_sleep(2);
+      if (lane == 0) __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
+      WSYNC();   // (compiler order: the row loads stay behind the poll)
+      const T* r = ka->b.mid + (size_t)env_id * MIDDIM;
+      time = r[MID_TIME];
+      xws = (sl < nv) ? r[MID_WS + sl] : T(0);
+      if (sl < nq) s.qpos[sl] = r[MID_Q + sl];
+      if (sl + HL < nq) s.qpos[sl + HL] = r[MID_Q + sl + HL];
+      if (sl < nv) s.qvel[sl] = r[MID_V + sl];
+#pragma unroll
+      for (int w = 0; w < NWARN; w++) warn[w] = (int)r[MID_W + w];
+    } else {
+      time = ka->b.time[env_id];
+      xws = (sl < nv) ? ka->b.qacc_ws[(size_t)env_id * nv + sl] : T(0);
+      if (sl < nq) s.qpos[sl] = ka->b.qpos[(size_t)env_id * nq + sl];
+      if (sl + HL < nq) s.qpos[sl + HL] = ka->b.qpos[(size_t)env_id * nq + sl + HL];
+      if (sl < nv) s.qvel[sl] = ka->b.qvel[(size_t)env_id * nv + sl];
+    }
     // data.ctrl is an input only to a raw physics call that keeps the current ctrl; env steps set
     // it from the action, resets zero it
     const float* actions = ka->actions;
@@ -2067,15 +2109,34 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
   bool in_reset = false;
 #ifdef HS_TIMING
   int tot_iter = 0;
+  const int titem = (ka->p.queue ? (s0 > 0 ? (nidx + 1) / 2 : 0) + pair : -1);
 #endif
   // One loop, ONE inlined physics_step call site: substeps 0..nsub-1 apply the action; after the
   // last one the env bookkeeping runs; if any half of the wave must reset, one more substep
   // runs with the reset state (a half that is not resetting has already committed and computes
   // on scratch only).  Launch arguments are re-read through k = opaque(ka) at each use.
-  for (int sub = 0;; sub++) {
+  for (int sub = s0;; sub++) {
     st.m = opaque(st.m);
     st.sl = opaque_v(st.sl);
     const int env = opaque_v(env_id);   // per-env addresses recomputed at each use, not kept live
+    if (sub == s1 && s1 < nsub) {         // queued chunk ends before the last substep: hand over
+      KPtr<T> k = opaque(ka);
+      if (active) {
+        T* r = k->b.mid + (size_t)env * MIDDIM;
+        if (sl < nq) r[MID_Q + sl] = s.qpos[sl];
+        if (sl + HL < nq) r[MID_Q + sl + HL] = s.qpos[sl + HL];
+        if (sl < nv) { r[MID_V + sl] = s.qvel[sl]; r[MID_WS + sl] = xws; }
+        if (sl == 0) {
+          r[MID_TIME] = time;
+#pragma unroll
+          for (int w = 0; w < NWARN; w++) r[MID_W + w] = (T)warn[w];
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the row is in memory before the flag is
+      if (lane == 0) __hip_atomic_store(k->b.qsync + QS_FLAG + pair, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      HS_FLUSH();
+      break;
+    }
     if (sub == nsub && !in_reset) {
       if (nsub > 0) {
         KPtr<T> k = opaque(ka);
@@ -2168,14 +2229,52 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
 // registers and runs at 1.  PGS: the <option solver="PGS"> instance (its own LDS cache).
 template <typename T, int NV, bool PGS>
 __global__ __launch_bounds__(64, (sizeof(T) == 4 && !PGS) ? 2 : 1) void step_kernel(KArgs<T> /* read via kernarg ptr */) {
-  __shared__ Scratch<T, Resident> smem[2];
-  PgsCache<T, Resident>* pcache = nullptr;
+  __shared__ Scratch<T, Resident<T>> smem[2];
+  PgsCache<T, Resident<T>>* pcache = nullptr;
   if constexpr (PGS) {
-    __shared__ PgsCache<T, Resident> pgs_smem[2];
+    __shared__ PgsCache<T, Resident<T>> pgs_smem[2];
     pcache = &pgs_smem[threadIdx.x >= HL ? 1 : 0];
   }
   const KPtr<T> ka = (KPtr<T>)__builtin_amdgcn_kernarg_segment_ptr();
-  step_pair<T, NV, PGS, Resident>(ka, smem, pcache, 2 * blockIdx.x + (threadIdx.x >= HL ? 1 : 0), ka->nenv, nullptr);
+  step_pair<T, NV, PGS, Resident<T>>(ka, smem, pcache, 2 * blockIdx.x + (threadIdx.x >= HL ? 1 : 0), ka->nenv, nullptr,
+                                     0, ka->p.nsub, blockIdx.x);
+}
+
+// Resident tier, chunk-queue schedule (launch_step picks it when the env pairs outnumber the waves
+// the GPU holds at once -- the fp64 engine at 1 wave per SIMD -- for multi-substep calls).  A
+// persistent grid claims items from one counter: first every pair's substeps [0, nsub - 1), then
+// every pair's last substep (+ obs / reward / auto-reset), so the launch ends on short items
+// instead of a second generation of whole env steps.  Items are claimed only by
+// running waves and a last-substep item waits only on its own pair's first chunk, claimed npairs
+// items earlier by a running wave: no residency can deadlock it.
+template <typename T, int NV, bool PGS>
+__global__ __launch_bounds__(64, 1) void step_kernel_queue(KArgs<T> /* read via kernarg ptr */) {
+  __shared__ Scratch<T, Resident<T>> smem[2];
+  PgsCache<T, Resident<T>>* pcache = nullptr;
+  if constexpr (PGS) {
+    __shared__ PgsCache<T, Resident<T>> pgs_smem[2];
+    pcache = &pgs_smem[threadIdx.x >= HL ? 1 : 0];
+  }
+  const KPtr<T> ka = (KPtr<T>)__builtin_amdgcn_kernarg_segment_ptr();
+  for (;;) {
+    const KPtr<T> k = opaque(ka);       // nothing uniform kept live across items
+    const int nsub = k->p.nsub, npairs = (k->nenv + 1) / 2;
+    int i = 0;
+    if (threadIdx.x == 0) i = atomicAdd(&k->b.qsync[QS_HEAD], 1);
+    i = __builtin_amdgcn_readfirstlane(i);
+    if (i >= 2 * npairs) break;
+    const bool last = i >= npairs;
+    const int pair = last ? i - npairs : i;
+    step_pair<T, NV, PGS, Resident<T>>(k, smem, pcache, 2 * pair + (opaque_v(threadIdx.x) >= HL ? 1 : 0), k->nenv,
+                                       nullptr, last ? nsub - 1 : 0, last ? nsub : nsub - 1, pair);
+  }
+  // the last wave out resets the counter for the next launch (every wave has made its final claim;
+  // each pair flag was reset by its last-substep item)
+  int* qs = ka->b.qsync;
+  if (threadIdx.x == 0 && atomicAdd(&qs[QS_EXIT], 1) == (int)gridDim.x - 1) {
+    qs[QS_HEAD] = 0;
+    qs[QS_EXIT] = 0;
+  }
 }
 
 // Wide tier: a small grid that strides over the envs the resident launch deferred (usually none:
@@ -2192,7 +2291,8 @@ __global__ __launch_bounds__(64, 1) void step_kernel_wide(KArgs<T> /* read via k
   int* redo = ka->b.redo;
   const int count = redo[0];
   for (int base = 2 * blockIdx.x; base < count; base += 2 * gridDim.x)
-    step_pair<T, NV, PGS, Wide>(ka, smem, pcache, base + (threadIdx.x >= HL ? 1 : 0), count, redo + 2);
+    step_pair<T, NV, PGS, Wide>(ka, smem, pcache, base + (threadIdx.x >= HL ? 1 : 0), count, redo + 2, 0,
+                                ka->p.nsub, 0);
   __threadfence();
   if (threadIdx.x == 0 && atomicAdd(&redo[1], 1) == (int)gridDim.x - 1) {   // every wave has read the list
     redo[0] = 0;
@@ -2205,14 +2305,14 @@ __global__ __launch_bounds__(64, 1) void step_kernel_wide(KArgs<T> /* read via k
 // [xmat MAXBODY*9][geom_xpos MAXGEOM*3][geom z-axis MAXGEOM*3][subtree_com[0] 3].
 template <typename T, int NV>
 __global__ __launch_bounds__(64) void kin_kernel(MPtr<T> m, const T* __restrict__ qpos, T* __restrict__ out) {
-  __shared__ Scratch<T, Resident> smem[2];
+  __shared__ Scratch<T, Resident<T>> smem[2];
   const int lane = threadIdx.x;
   const bool up = lane >= HL;
   const int sl = lane & (HL - 1);
-  Scratch<T, Resident>& s = smem[up ? 1 : 0];
+  Scratch<T, Resident<T>>& s = smem[up ? 1 : 0];
   for (int k = sl; k < m->nq; k += HL) s.qpos[k] = qpos[k];
   WSYNC();
-  Stepper<T, NV, Resident> st(m, s, lane);
+  Stepper<T, NV, Resident<T>> st(m, s, lane);
   st.kinematics();
   if (up) return;
   const int nb = m->nbody, ng = m->ngeom;
@@ -2229,25 +2329,51 @@ __global__ __launch_bounds__(64) void kin_kernel(MPtr<T> m, const T* __restrict_
 
 }  // namespace
 
+// waves of the resident step-kernel instance the device holds at once (occupancy x CUs), cached
+template <typename T>
+int resident_waves(bool pgs) {
+  static int cache[2] = {-1, -1};
+  int& c = cache[pgs ? 1 : 0];
+  if (c < 0) {
+    int dev = 0, per_cu = 0;
+    hipDeviceProp_t prop;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipGetDeviceProperties(&prop, dev);
+    if (e == hipSuccess)
+      e = pgs ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<T, 27, true>, WAVE, 0)
+              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<T, 27, false>, WAVE, 0);
+    c = (e == hipSuccess && per_cu > 0) ? per_cu * prop.multiProcessorCount : 0;
+  }
+  return c;
+}
+
 template <typename T>
 hipError_t launch_step(const DevModel<T>* dmodel, int nv, const EnvBuffers<T>& b, const float* actions,
                        const uint8_t* reset_mask, const T* noise_qpos, const T* noise_qvel,
                        const StepParams& p, int nenv, hipStream_t stream) {
   if (nenv <= 0) return hipSuccess;
   if (nv != 27) return hipErrorInvalidValue;
-  const KArgs<T> args{(MPtr<T>)dmodel, b, actions, reset_mask, noise_qpos, noise_qvel, p, nenv};
-  const dim3 grid((nenv + 1) / 2), block(WAVE);
+  KArgs<T> args{(MPtr<T>)dmodel, b, actions, reset_mask, noise_qpos, noise_qvel, p, nenv};
+  // chunk-queue schedule when the env pairs outnumber the waves the GPU holds at once (the fp64
+  // engine: 1 wave per SIMD), for multi-substep calls (HS_SCHED_DIRECT: never)
+  const int npairs = (nenv + 1) / 2;
+  const int resident = resident_waves<T>(p.solver == SOLVER_PGS);
+  args.p.queue = (p.schedule == 0 && b.mid && b.qsync && p.mode != MODE_RESET && p.nsub >= 2 &&
+                  resident > 0 && npairs > resident) ? 1 : 0;
+  const dim3 grid(args.p.queue ? resident : npairs), block(WAVE);
   // the wide tier's grid: enough waves for a few deferred envs at once, few enough that the
   // common no-overflow launch (every wave reads the count and exits) costs a few microseconds
   const dim3 wgrid(std::min((nenv + 1) / 2, 32));
 #ifndef HS_DEV_NEWTON_ONLY   // development builds: resource-usage checks of the Newton instances only
   if (p.solver == SOLVER_PGS) {
-    hipLaunchKernelGGL((step_kernel<T, 27, true>), grid, block, 0, stream, args);
+    if (args.p.queue) hipLaunchKernelGGL((step_kernel_queue<T, 27, true>), grid, block, 0, stream, args);
+    else hipLaunchKernelGGL((step_kernel<T, 27, true>), grid, block, 0, stream, args);
     if (b.redo) hipLaunchKernelGGL((step_kernel_wide<T, 27, true>), wgrid, block, 0, stream, args);
     return hipGetLastError();
   }
 #endif
-  hipLaunchKernelGGL((step_kernel<T, 27, false>), grid, block, 0, stream, args);
+  if (args.p.queue) hipLaunchKernelGGL((step_kernel_queue<T, 27, false>), grid, block, 0, stream, args);
+  else hipLaunchKernelGGL((step_kernel<T, 27, false>), grid, block, 0, stream, args);
   if (b.redo) hipLaunchKernelGGL((step_kernel_wide<T, 27, false>), wgrid, block, 0, stream, args);
   return hipGetLastError();
 }

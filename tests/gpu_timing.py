@@ -56,6 +56,39 @@ def main(n=4096, steps=20, prec="fp32", staggered=False):
     q = np.percentile(life, [0, 10, 50, 90, 99, 100])
     print("  wave lifetime (last launch, cycles) min/p10/p50/p90/p99/max: " + " / ".join(f"{v:,.0f}" for v in q)
           + f"   mean {life.mean():,.0f}  (launch = max; mean/max = {life.mean() / life.max():.2f})")
+    dbg = b.get_debug()
+    st = dbg[16384:16384 + len(life)].astype(np.int64)      # s_memrealtime (100 MHz) at wave start / end
+    en = dbg[18432:18432 + len(life)].astype(np.int64)
+    base = st.min()
+    st, en = (st - base) % (1 << 24), (en - base) % (1 << 24)
+    span = en.max()
+    ghz = life.mean() / max(1.0, (en - st).mean() * 10.0)   # shader cycles per ns
+    print(f"  realtime: launch span {span * 10 / 1e3:.1f} us, mean wave {((en - st).mean()) * 10 / 1e3:.1f} us "
+          f"(shader clock {ghz:.2f} GHz); wave start p10/p50/p90/max (us) " +
+          " / ".join(f"{v * 10 / 1e3:.1f}" for v in np.percentile(st, [10, 50, 90, 100])))
+    print("  wave end (fraction of span) p10/p50/p90/p99: " +
+          " / ".join(f"{v:.2f}" for v in np.percentile(en / span, [10, 50, 90, 99])))
+    late = st > 0.05 * span
+    print(f"  waves starting in the first 5% of the span: {(~late).sum()}, later: {late.sum()}")
+    busy = np.zeros(200)
+    for a_, e_ in zip(st, en):
+        busy[int(a_ / span * 199):int(e_ / span * 199) + 1] += 1
+    print("  resident waves over the launch (20 bins): " + " ".join(f"{v:.0f}" for v in busy.reshape(20, 10).mean(1)))
+    q0 = dbg[20480:20480 + 8192].reshape(-1, 2).astype(np.int64)
+    qw = dbg[28672:28672 + 4096]
+    if q0.any():    # chunk-queue schedule: per item realtime start / end and flag-wait cycles
+        qs, qe = (q0[:, 0] - q0[:, 0].min()) % (1 << 24), (q0[:, 1] - q0[:, 0].min()) % (1 << 24)
+        span = qe.max()
+        npair = len(life)
+        d0, d1 = (qe - qs)[:npair], (qe - qs)[npair:2 * npair]
+        print(f"  queue: span {span * 10 / 1e3:.1f} us; chunk0 items mean {d0.mean() * 10 / 1e3:.1f} us, last-substep items "
+              f"mean {d1.mean() * 10 / 1e3:.1f} us (p90 {np.percentile(d1, 90) * 10 / 1e3:.1f}, max {d1.max() * 10 / 1e3:.1f})")
+        busy = np.zeros(200)
+        for a_, e_ in zip(qs, qe):
+            busy[int(a_ / span * 199):int(e_ / span * 199) + 1] += 1
+        print("  busy waves over the launch (20 bins): " + " ".join(f"{v:.0f}" for v in busy.reshape(20, 10).mean(1)))
+    np.savez(os.path.join(ROOT, "gpurun_out", f"timing_{prec}.npz"), life=life, st=st, en=en,
+             it=dbg[11100:11100 + 2 * len(life)], q0=q0, qw=qw)
     it = b.get_debug()[11100:11100 + 2 * len(life)].reshape(-1, 2)
     wmax, wsum = it.max(1), it.sum(1)
     print(f"  newton iters per env per launch: mean {it.mean():.1f} max {it.max():.0f}; corr(lifetime, max-of-pair) "

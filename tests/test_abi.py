@@ -63,7 +63,7 @@ def test_config_struct_layout():
     import os
     import re
     from mujocoposelearning_amd import _lib
-    assert C.sizeof(_lib.hs_env_config) == 6 * 4 + 3 * 8 + 9 * 8
+    assert C.sizeof(_lib.hs_env_config) == 6 * 4 + 3 * 8 + 9 * 8 + 8      # + schedule (padded)
     hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "hsim.h")).read()
     body = re.search(r"typedef struct \{(.*?)\} hs_buffers;", hdr, re.S).group(1)
     names = re.findall(r"\*\s*(\w+);", body)
@@ -114,3 +114,30 @@ def test_header_is_plain_c():
     for cc, lang in (("gcc", "c"), ("g++", "c++")):
         if shutil.which(cc):
             subprocess.run([cc, "-fsyntax-only", "-Wall", "-Werror", "-x", lang, hdr], check=True)
+
+
+def test_struct_layouts_match_the_c_compiler(tmp_path):
+    """Size and every field offset of the ctypes mirrors equal what the C compiler lays out for
+    include/hsim.h (hs_env_config, hs_buffers, hs_batch_info)."""
+    import shutil
+    import subprocess
+    from mujocoposelearning_amd import _lib
+    if not shutil.which("gcc"):
+        pytest.skip("no gcc")
+    structs = {"hs_env_config": _lib.hs_env_config, "hs_buffers": _lib.hs_buffers, "hs_batch_info": _lib.hs_batch_info}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "hsim.h"', "int main(void) {"]
+    for name, cls in structs.items():
+        lines.append(f'  printf("{name} size %zu\\n", sizeof({name}));')
+        for f, _ in cls._fields_:
+            lines.append(f'  printf("{name} {f} %zu\\n", offsetof({name}, {f}));')
+    lines.append("  return 0;\n}")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = {tuple(l.split()[:2]): int(l.split()[2]) for l in out if l}
+    for name, cls in structs.items():
+        assert got[(name, "size")] == C.sizeof(cls), name
+        for f, _ in cls._fields_:
+            assert got[(name, f)] == getattr(cls, f).offset, (name, f)

@@ -1,5 +1,5 @@
-"""Contact capacity: the resident kernel tier (32 contacts / 128 rows per env) and the wide tier
-(64 / 256) that re-runs the envs overflowing it (hs_model.h).
+"""Contact capacity: the resident kernel tier (fp32: 32 contacts / 128 rows per env; fp64: 16 / 96)
+and the wide tier (64 / 256) that re-runs the envs overflowing it (hs_model.h).
 
 A humanoid lying pressed into the floor has up to ~44 contacts / ~150 constraint rows
 (humanoid.xml:105-184: 16 capsules x 2 + 3 spheres against the condim-3 floor, plus limits).
@@ -37,9 +37,9 @@ def _qmul(a, b):
     return np.r_[a[0] * b[0] - a[1:] @ b[1:], a[0] * b[1:] + b[0] * a[1:] + np.cross(a[1:], b[1:])]
 
 
-def lying_states(o, n, seed, overflow=True):
+def lying_states(o, n, seed, overflow=True, cap=(32, 128)):
     """Prone / supine / on-the-side humanoids pressed into the floor; with overflow=True only
-    states whose contacts or rows exceed the resident tier (ncon > 32 or nefc > 128) are kept."""
+    states whose contacts or rows exceed the resident tier ``cap`` (ncon, nefc) are kept."""
     M = o.M
     rng = np.random.default_rng(seed)
     lo, hi = M["jnt_range"][1:, 0], M["jnt_range"][1:, 1]
@@ -55,7 +55,7 @@ def lying_states(o, n, seed, overflow=True):
         o.qpos[:] = q
         o.qvel[:] = 0
         o.forward()
-        big = o.d.ncon > 32 or o.d.nefc > 128
+        big = o.d.ncon > cap[0] or o.d.nefc > cap[1]
         if big == overflow:
             out.append(q)
             if len(out) == n:
@@ -77,14 +77,16 @@ def test_wide_tier_lying_states_match_oracle(model, prec):
     from mujocoposelearning_amd.batch import HsBatch
     from oracle.oracle import Oracle
     o = Oracle(XML)
-    big = lying_states(o, 24, seed=1)
-    small = lying_states(o, 8, seed=2, overflow=False)
+    cap = HsBatch(model, 2, precision=prec).resident_capacity
+    big = lying_states(o, 24, seed=1, cap=cap)
+    small = lying_states(o, 8, seed=2, overflow=False, cap=cap)
     qs = np.stack(big + small)
     n = len(qs)
     rng = np.random.default_rng(5)
     vs = rng.normal(0, 0.3, (n, 27))
     cs = rng.uniform(-1, 1, (n, 21)).astype(np.float32)
     b = HsBatch(model, n, precision=prec)
+    assert b.wide_capacity == (64, 256) and cap == ((16, 96) if prec == "fp64" else (32, 128))
     b.set_state(qpos=qs, qvel=vs, time=0.0, qacc_warmstart=0.0)
     b.physics_step(torch.tensor(cs, device=b.device), 1)
     st = b.get_state()
@@ -119,7 +121,7 @@ def test_wide_tier_env_step_autoreset_matches_oracle_env(model):
     from oracle.env import OracleHumanoidEnv
     from oracle.oracle import Oracle
     o = Oracle(XML)
-    qs = np.stack(lying_states(o, 6, seed=3))
+    qs = np.stack(lying_states(o, 6, seed=3))            # over the fp32 tier, so over the fp64 one too
     n = len(qs)
     rng = np.random.default_rng(7)
     vs = rng.normal(0, 0.2, (n, 27))

@@ -111,6 +111,37 @@ def test_full_size_determinism_and_batch_invariance(model):
     assert torch.equal(b1.qpos[0], bN.qpos[idx]) and torch.equal(b1.obs[0], bN.obs[idx])
 
 
+def test_chunk_queue_schedule_bitwise_equals_direct(model):
+    """The fp64 engine at configs[1] size runs on the chunk-queue schedule (2048 env pairs > 1024
+    resident waves: each env step as two items, the state handed over through uncached memory,
+    DESIGN.md 3.1).  It must give bitwise the states, obs, rewards, done flags, auto-reset info and
+    warnings of one wave per pair -- through falls, contacts and auto-resets (staggered clocks: some
+    envs terminate at every step), including odd batch sizes (a ghost half-wave)."""
+    import torch
+    for n in (4096, 3001):
+        g = torch.Generator(device="cuda").manual_seed(4)
+        acts = torch.rand(40, n, 21, device="cuda", generator=g) * 2 - 1
+        t0 = np.floor(np.arange(n) * 667 / n) * 0.015 + 0.005
+        outs = []
+        for sched in ("auto", "direct"):
+            b = _batch(model, n, prec="fp64", seed=3)
+            b.configure(schedule=sched)
+            b.reset()
+            b.set_state(time=t0)
+            tr = []
+            for k in range(40):
+                b.step(acts[k])
+                if k % 10 == 9:
+                    tr += [b.obs.clone(), b.reward.clone(), b.terminated.clone(), b.truncated.clone()]
+            tr += [b.qpos.clone(), b.qvel.clone(), b.qacc_warmstart.clone(), b.time.clone(), b.warning.clone(),
+                   b.terminal_obs.clone(), b.terminal_step_count.clone(), b.terminal_total_reward.clone(),
+                   b.episode.clone(), b.aux.clone()]
+            outs.append(tr)
+        assert int(outs[0][-2].min()) >= 1 and int(outs[0][-2].max()) >= 2      # auto-resets happened
+        for x, y in zip(*outs):
+            assert torch.equal(x, y)
+
+
 def test_reset_distribution_device_rng(model):
     """On-device reset noise: U(-.01, .01) per coordinate, z noise x0.1, quaternion exact; the
     reset then runs exactly one substep (time 0.005)."""
