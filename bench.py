@@ -314,6 +314,7 @@ def main():
     value = n * args.steps * ranks / elapsed
     stats = stats_of(env, tape, EPISODE + args.warmup + args.steps)
     kernel_ms = step_ms
+    queued = env.batch.queued()
     env.close()
 
     # ---- fp32 sim-only leg (the throughput engine; tolerance-based parity, not the headline)
@@ -503,7 +504,8 @@ def main():
                                  "source": f"SQ_INSTS_VALU per launch from profiles ({tr.get('tag')})"}
             except Exception:
                 traffic = None
-        kname = "step_kernel<double,27>" if args.precision == "fp64" else "step_kernel<float,27>"
+        kname = ("step_kernel_queue" if queued else "step_kernel") + (
+            "<double,27>" if args.precision == "fp64" else "<float,27>")
         vflops = None
         if os.path.exists(FLOPS_JSON):
             fpe = json.load(open(FLOPS_JSON))["mean_total"]
@@ -536,6 +538,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kname,
                          "kernel_ms_per_launch": kernel_ms, "envs_per_launch": n,
+                         "schedule": ("chunk queue: persistent grid of resident waves, two items per env step "
+                                      "(DESIGN.md 3.1)" if queued else "one wave per env pair"),
                          "algo_bytes_per_env_step": abytes, "valu_issue": issue, "valu_flops": vflops,
                          "note": "latency-bound kernel (see valu_issue and DESIGN.md 3.1); HBM fraction reported per "
                                  "BASELINE.json; HIP events over the timed steps on the launch stream (the step "

@@ -122,6 +122,9 @@ typedef struct {
    * wide tier that re-runs the envs overflowing it; only wide-tier overflow drops contacts
    * (HS_WARN_OVERFLOW).  MuJoCo has no per-env cap (custom_env.py:160). */
   int resident_con, resident_efc, wide_con, wide_efc;
+  /* waves of the resident step kernel the device holds at once (2 envs per wave); with more env
+   * pairs than this, HS_SCHED_AUTO runs multi-substep calls on the chunk-queue schedule */
+  int resident_waves;
 } hs_batch_info;
 
 hs_model* hs_model_load(const char* xml_path, char* err, int errsz);

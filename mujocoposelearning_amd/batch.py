@@ -80,6 +80,14 @@ class HsBatch:
         # per-env (contacts, constraint rows) of the resident kernel tier and of the wide re-run tier
         self.resident_capacity = (info.resident_con, info.resident_efc)
         self.wide_capacity = (info.wide_con, info.wide_efc)
+        self.resident_waves = info.resident_waves
+
+    def queued(self, nsub=None):
+        """True when an env step of this batch runs on the chunk-queue schedule (HS_SCHED_AUTO, more
+        env pairs than resident waves, >= 2 substeps; include/hsim.h)."""
+        nsub = self.cfg.frame_skip if nsub is None else nsub
+        n = max(hi - lo for _, lo, hi in self._groups)
+        return (self.cfg.schedule == _lib.HS_SCHED_AUTO and nsub >= 2 and 0 < self.resident_waves < (n + 1) // 2)
 
     # -- tensors (device views, valid until the next call) ---------------------------------
     def __getattr__(self, name):

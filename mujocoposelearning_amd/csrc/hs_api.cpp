@@ -364,6 +364,11 @@ int hs_batch_get_info(const hs_batch* b, hs_batch_info* out) {
   out->resident_efc = b->precision == HS_FP64 ? hs::MAXEFC_F64 : hs::MAXEFC;
   out->wide_con = hs::MAXCON_WIDE;
   out->wide_efc = hs::MAXEFC_WIDE;
+  {
+    DeviceGuard g(b->device);
+    const bool pgs = b->model->host.solver == 1;
+    out->resident_waves = b->precision == HS_FP64 ? hs::resident_waves<double>(pgs) : hs::resident_waves<float>(pgs);
+  }
   return 0;
 }
 

@@ -81,6 +81,10 @@ hipError_t launch_step(const DevModel<T>* dmodel, int nv, const EnvBuffers<T>& b
                        const uint8_t* reset_mask, const T* noise_qpos, const T* noise_qvel,
                        const StepParams& p, int nenv, hipStream_t stream);
 
+// waves of the resident step-kernel instance the current device holds at once (0 if unknown)
+template <typename T>
+int resident_waves(bool pgs);
+
 // mj_kinematics/mj_comPos of one state (device qpos[nq]) -> out[KINDIM] (see kin_kernel)
 constexpr int KINDIM = MAXBODY * 12 + MAXGEOM * 6 + 3;
 template <typename T>

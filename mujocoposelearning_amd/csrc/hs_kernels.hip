@@ -47,8 +47,7 @@ struct Cap {
   static constexpr bool WIDE = W;         // the wide (re-run) tier
   static_assert((NCON % HL == 0 || HL % NCON == 0) && NEFC % HL == 0, "capacity in whole half-waves");
 };
-// resident tier per precision (hs_model.h): fp64 scratch is twice the size, so its tier is halved
-// in contacts to fit 5 workgroups (env pairs) per CU instead of 4
+// resident tier per precision (hs_model.h)
 template <typename T>
 using Resident = std::conditional_t<sizeof(T) == 8, Cap<MAXCON_F64, MAXEFC_F64>, Cap<MAXCON, MAXEFC>>;
 using Wide = Cap<MAXCON_WIDE, MAXEFC_WIDE, true>;
@@ -2393,6 +2392,8 @@ hipError_t launch_kinematics(const DevModel<T>* dmodel, int nv, const T* qpos, T
   hipLaunchKernelGGL((kin_kernel<T, 27>), dim3(1), dim3(WAVE), 0, stream, (MPtr<T>)dmodel, qpos, out);
   return hipGetLastError();
 }
+template int resident_waves<float>(bool);
+template int resident_waves<double>(bool);
 template hipError_t launch_kinematics<float>(const DevModel<float>*, int, const float*, float*, hipStream_t);
 template hipError_t launch_kinematics<double>(const DevModel<double>*, int, const double*, double*, hipStream_t);
 

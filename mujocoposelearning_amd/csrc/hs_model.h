@@ -30,8 +30,11 @@ constexpr int MAXPAIR = 192;  // static candidate geom pairs
 //    with this capacity.  Only overflow of the wide tier drops contacts (warning word).
 constexpr int MAXCON = 32;    // resident tier: contacts per env (one half-wave lane each)
 constexpr int MAXEFC = 128;   // resident tier: constraint rows per env (4 per half-wave lane)
-constexpr int MAXCON_F64 = 16;    // fp64 resident tier (twice the bytes per value: 5 env pairs per CU)
-constexpr int MAXEFC_F64 = 96;
+// fp64 resident tier: the same capacity.  (Halving it to 16 / 96 cuts the fp64 scratch to 5 env pairs
+// per CU of LDS, but the fp64 engine's registers already hold it to 4 -- 1 wave per SIMD -- so it
+// bought nothing; measured r2c.)
+constexpr int MAXCON_F64 = 32;
+constexpr int MAXEFC_F64 = 128;
 constexpr int MAXCON_WIDE = 64;    // wide tier (2 contacts per lane)
 constexpr int MAXEFC_WIDE = 256;   // wide tier (8 rows per lane)
 constexpr int MAXLEVEL = 16;

@@ -22,7 +22,9 @@ STATS_STEPS = 3     # bench.py's stats_of() steps after the timed window
 
 
 def is_step(name):
-    return "step_kernel<" in name and "wide" not in name
+    # the resident-tier step kernel: one wave per pair (step_kernel<...>) or the chunk-queue schedule
+    # (step_kernel_queue<...>, the fp64 engine at 4096 envs)
+    return ("step_kernel<" in name or "step_kernel_queue<" in name) and "wide" not in name
 
 
 def main(tag="r2a", precision="fp64", n_envs=4096, timed=50, src=None):
@@ -73,7 +75,14 @@ def main(tag="r2a", precision="fp64", n_envs=4096, timed=50, src=None):
               f"- raw (FETCH+WRITE)*1024 = {raw / 1e6:,.2f} MB; gfx950-corrected (2*FETCH+WRITE)*1024 = "
               f"{corrected / 1e6:,.2f} MB",
               f"- algorithmic {algo / 1e6:,.2f} MB ({algo_env} B/env step x {n_envs}); traffic/algo = "
-              f"{corrected / algo:.2f}x", "",
+              f"{corrected / algo:.2f}x"] + ([
+              f"- chunk-queue schedule: + the hand-off of each env between its two items (qpos, qvel, warm start, "
+              f"time, 4 warning counters = 87 values written once and read once: {2 * 87 * es} B/env, "
+              f"{2 * 87 * es * n_envs / 1e6:.2f} MB/launch) through UNCACHED memory, whose 8-byte lane accesses the "
+              f"TCC counters report at ~4-5x (r2c: +16 MB WRITE_SIZE, +7 MB FETCH_SIZE vs the one-wave-per-pair "
+              f"kernel r2a); traffic/(algo + hand-off) = {corrected / (algo + 2 * 87 * es * n_envs):.2f}x; "
+              f"{corrected / (statistics.mean(win) * 1e-3) / 1e9:.0f} GB/s of the 8 TB/s HBM"]
+              if "queue" in row["Kernel_Name"] else []) + ["",
               "## Resources", "",
               f"VGPR {out['vgpr']} (+{out['agpr']} AGPR), SGPR {out['sgpr']}, LDS {out['lds_bytes']} B/workgroup, "
               f"scratch {out['scratch_bytes_per_lane']} B/lane, grid {out['grid']} threads x wg {out['workgroup']}."]

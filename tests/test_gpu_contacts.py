@@ -1,5 +1,5 @@
-"""Contact capacity: the resident kernel tier (fp32: 32 contacts / 128 rows per env; fp64: 16 / 96)
-and the wide tier (64 / 256) that re-runs the envs overflowing it (hs_model.h).
+"""Contact capacity: the resident kernel tier (32 contacts / 128 rows per env, both precisions;
+hs_batch_info reports it) and the wide tier (64 / 256) that re-runs the envs overflowing it (hs_model.h).
 
 A humanoid lying pressed into the floor has up to ~44 contacts / ~150 constraint rows
 (humanoid.xml:105-184: 16 capsules x 2 + 3 spheres against the condim-3 floor, plus limits).
@@ -86,7 +86,7 @@ def test_wide_tier_lying_states_match_oracle(model, prec):
     vs = rng.normal(0, 0.3, (n, 27))
     cs = rng.uniform(-1, 1, (n, 21)).astype(np.float32)
     b = HsBatch(model, n, precision=prec)
-    assert b.wide_capacity == (64, 256) and cap == ((16, 96) if prec == "fp64" else (32, 128))
+    assert b.wide_capacity == (64, 256) and cap == (32, 128)
     b.set_state(qpos=qs, qvel=vs, time=0.0, qacc_warmstart=0.0)
     b.physics_step(torch.tensor(cs, device=b.device), 1)
     st = b.get_state()
