@@ -36,6 +36,10 @@ def run(xml, prec, n=4096, steps=30):
         a = env.batch.aux.double().cpu().numpy()
         w = a[:, 37] * np.maximum(a[:, 36], 1)
         work.append((w.max(), w.mean(), a[:, 37].max(), a[:, 36].max(), (a[:, 37] >= 100).sum()))
+    warn = env.batch.warning.sum(0).tolist()
+    print(f"    schedule: {'chunk queue' if env.batch.queued() else 'one wave per pair'} (resident waves "
+          f"{env.batch.resident_waves}); warnings over {300 + steps} staggered steps [badqpos, badqvel, badqacc "
+          f"(mj_checkAcc resets), overflow] = {warn}", flush=True)
     env.close()
     ms = np.array(ms)
     work = np.array(work)
@@ -47,7 +51,7 @@ def main():
     src = open(XML).read()
     d = tempfile.mkdtemp()
     for prec in ("fp64", "fp32"):
-        for it in (100, 50, 25):
+        for it in ((100,) if "defaults" in sys.argv else (100, 50, 25)):
             xml = os.path.join(d, f"pgs{it}.xml")
             open(xml, "w").write(re.sub(r"<option[^>]*/>", f'<option timestep="0.005" solver="PGS" iterations="{it}"/>',
                                         src, count=1))
