@@ -68,6 +68,7 @@ struct StepParams {
   int outputs;           // OUT_* bits: optional per-env outputs written at commit
   int schedule;          // HS_SCHED_AUTO (0) / HS_SCHED_DIRECT (1) (hs_env_config.schedule)
   int queue;             // set by launch_step: 1 = chunk-queue schedule (persistent grid), 0 = one wave per pair
+  int qmul;              // chunk-queue claim order: item i -> pair (i * qmul) mod npairs (qmul coprime to npairs)
 };
 // optional outputs (hs_env_config.outputs): the aux row (qacc, subtree com, ncon, nefc, solver
 // iterations -- data views and stats) and the data.ctrl copy (data views / host rewards)

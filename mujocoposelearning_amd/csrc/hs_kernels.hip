@@ -2243,9 +2243,10 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !PGS) ? 2 : 1) void step_ker
 // the GPU holds at once -- the fp64 engine at 1 wave per SIMD -- for multi-substep calls).  A
 // persistent grid claims items from one counter: first every pair's substeps [0, nsub - 1), then
 // every pair's last substep (+ obs / reward / auto-reset), so the launch ends on short items
-// instead of a second generation of whole env steps.  Items are claimed only by
-// running waves and a last-substep item waits only on its own pair's first chunk, claimed npairs
-// items earlier by a running wave: no residency can deadlock it.
+// instead of a second generation of whole env steps; pairs are taken in a fixed
+// multiplicative permutation (p.qmul).  Items are claimed only by running waves and a last-substep
+// item waits only on its own pair's first chunk, claimed npairs items earlier by a running wave: no
+// residency can deadlock it.
 template <typename T, int NV, bool PGS>
 __global__ __launch_bounds__(64, 1) void step_kernel_queue(KArgs<T> /* read via kernarg ptr */) {
   __shared__ Scratch<T, Resident<T>> smem[2];
@@ -2263,7 +2264,7 @@ __global__ __launch_bounds__(64, 1) void step_kernel_queue(KArgs<T> /* read via 
     i = __builtin_amdgcn_readfirstlane(i);
     if (i >= 2 * npairs) break;
     const bool last = i >= npairs;
-    const int pair = last ? i - npairs : i;
+    const int pair = (int)((uint64_t)(last ? i - npairs : i) * (uint32_t)k->p.qmul % (uint32_t)npairs);
     step_pair<T, NV, PGS, Resident<T>>(k, smem, pcache, 2 * pair + (opaque_v(threadIdx.x) >= HL ? 1 : 0), k->nenv,
                                        nullptr, last ? nsub - 1 : 0, last ? nsub : nsub - 1, pair);
   }
@@ -2359,6 +2360,17 @@ hipError_t launch_step(const DevModel<T>* dmodel, int nv, const EnvBuffers<T>& b
   const int resident = resident_waves<T>(p.solver == SOLVER_PGS);
   args.p.queue = (p.schedule == 0 && b.mid && b.qsync && p.mode != MODE_RESET && p.nsub >= 2 &&
                   resident > 0 && npairs > resident) ? 1 : 0;
+  // claim order: a fixed multiplicative permutation of the pairs (the same for both chunk kinds, so a
+  // pair's last substep is still claimed npairs items after its first chunk).  Items whose cost is
+  // correlated with the env index -- e.g. env clocks staggered by index, bench.py's window -- are
+  // spread over the launch instead of arriving together at its end.
+  args.p.qmul = 1;
+  if (args.p.queue) {
+    auto gcd = [](uint32_t a, uint32_t b) { while (b) { uint32_t t = a % b; a = b; b = t; } return a; };
+    uint32_t q = (uint32_t)(0.6180339887 * npairs) | 1u;
+    while (gcd(q, (uint32_t)npairs) != 1u) q += 2;
+    args.p.qmul = (int)(q % (uint32_t)npairs == 0 ? 1 : q);
+  }
   const dim3 grid(args.p.queue ? resident : npairs), block(WAVE);
   // the wide tier's grid: enough waves for a few deferred envs at once, few enough that the
   // common no-overflow launch (every wave reads the count and exits) costs a few microseconds

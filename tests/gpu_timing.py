@@ -129,7 +129,39 @@ def predict(n=4096, steps=60, prec="fp32"):
           f"{np.mean(srt):,.0f} ({np.mean(srt) / np.mean(rnd):.3f}); ideal {h[1:].sum(1).mean() / 2:,.0f}")
 
 
+def predict_queue(n=4096, prec="fp64", steps=6):
+    """Chunk-queue schedule: is a pair's item cost predictable from the previous env step's?
+    (timing build: per-item realtime start / end of the last launch, staggered mix)"""
+    model = HsModel(os.path.join(ROOT, "mujocoposelearning_amd", "assets", "humanoid.xml"))
+    b = HsBatch(model, n, precision=prec, seed=1)
+    b.configure(frame_skip=3, duration=10.0, reward_id=0)
+    b.reset()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    b.set_state(time=np.floor(np.arange(n) * 667 / n) * 0.015 + 0.005)
+    for k in range(667):
+        b.step(torch.rand(n, 21, device="cuda", generator=g) * 2 - 1)
+    b.set_debug(True)
+    np_ = (n + 1) // 2
+    hist = []
+    for k in range(steps):
+        b.step(torch.rand(n, 21, device="cuda", generator=g) * 2 - 1)
+        q0 = b.get_debug()[20480:20480 + 4 * np_].reshape(-1, 2).astype(np.int64)
+        d = ((q0[:, 1] - q0[:, 0]) % (1 << 24)) * 10 / 1e3
+        hist.append((d[:np_], d[np_:2 * np_]))
+    c0 = np.mean([np.corrcoef(hist[i][0], hist[i + 1][0])[0, 1] for i in range(steps - 1)])
+    c1 = np.mean([np.corrcoef(hist[i][1], hist[i + 1][1])[0, 1] for i in range(steps - 1)])
+    ct = np.mean([np.corrcoef(hist[i][0] + hist[i][1], hist[i + 1][1])[0, 1] for i in range(steps - 1)])
+    cw = np.mean([np.corrcoef(hist[i][0], hist[i][1])[0, 1] for i in range(steps)])
+    print(f"[{prec}] per-pair item durations, consecutive steps: corr(chunk0) {c0:.2f}, corr(last) {c1:.2f}, "
+          f"corr(prev total, last) {ct:.2f}; within a step corr(chunk0, last) {cw:.2f}")
+    np.savez(os.path.join(ROOT, "gpurun_out", f"predict_queue_{prec}.npz"), d0=np.array([h[0] for h in hist]),
+             d1=np.array([h[1] for h in hist]))
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[2] == "predict_queue":
+        predict_queue(prec=sys.argv[1])
+        sys.exit(0)
     if len(sys.argv) > 2 and sys.argv[2] == "predict":
         predict(prec=sys.argv[1])
         sys.exit(0)
