@@ -306,17 +306,22 @@ def test_device_rollout_deferred_timelimit_bootstrap():
     env.close()
 
 
-def test_graphed_rollout_matches_eager_rollout():
+@pytest.mark.parametrize("prec,n,steps", [("fp32", 256, 12), ("fp64", 4096, 6)])
+def test_graphed_rollout_matches_eager_rollout(prec, n, steps):
     """The device rollout captured as one HIP graph (PPO._capture_rollout) writes exactly what the
     eager loop writes: two identical envs + policies, one graphed and one eager, two rollouts
-    each (the second replays the graph with fresh noise and a reset inside)."""
+    each (the second replays the graph with fresh noise and a reset inside).  The fp64 case at
+    configs[1] size runs the env steps on the chunk-queue schedule (persistent grid, self-resetting
+    claim counter and pair flags) inside the replayed graph."""
     from mujocoposelearning_amd.model import HsModel
     from mujocoposelearning_amd.ppo import PPO
     from mujocoposelearning_amd.vec_env import HumanoidVecEnv
     model = HsModel(XML)
-    cfg = {"model_path": XML, "duration": 0.2, "reward_config": {"type": "stand"}, "frame_skip": 3}
-    envs = [HumanoidVecEnv(cfg, n_envs=256, model=model, seed=0) for _ in range(2)]
-    kw = dict(n_steps=12, batch_size=1024, n_epochs=1, seed=0,
+    cfg = {"model_path": XML, "duration": 0.2 if prec == "fp32" else 0.1, "reward_config": {"type": "stand"},
+           "frame_skip": 3}
+    envs = [HumanoidVecEnv(cfg, n_envs=n, model=model, seed=0, precision=prec) for _ in range(2)]
+    assert envs[0].batch.queued() == (prec == "fp64")
+    kw = dict(n_steps=steps, batch_size=min(1024, n * steps), n_epochs=1, seed=0,
               policy_kwargs={"activation_fn": "ReLU", "net_arch": {"pi": [256, 256], "vf": [256, 256]}})
     pa, pb = PPO(envs[0], **kw), PPO(envs[1], **kw)
     pb.graphs = False
