@@ -125,11 +125,18 @@ def test_struct_layouts_match_the_c_compiler(tmp_path):
     if not shutil.which("gcc"):
         pytest.skip("no gcc")
     structs = {"hs_env_config": _lib.hs_env_config, "hs_buffers": _lib.hs_buffers, "hs_batch_info": _lib.hs_batch_info}
+    # the INTEGRATION.md stub's own mirror of hs_env_config must match too
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    stub = re.search(r"(class HsEnvConfig\(C.Structure\):.*?\]\n)", text, re.S).group(1)
+    ns = {"C": C}
+    exec(stub, ns)
+    structs["hs_env_config_stub"] = ns["HsEnvConfig"]
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "hsim.h"', "int main(void) {"]
     for name, cls in structs.items():
-        lines.append(f'  printf("{name} size %zu\\n", sizeof({name}));')
+        cname = name.replace("_stub", "")
+        lines.append(f'  printf("{name} size %zu\\n", sizeof({cname}));')
         for f, _ in cls._fields_:
-            lines.append(f'  printf("{name} {f} %zu\\n", offsetof({name}, {f}));')
+            lines.append(f'  printf("{name} {f} %zu\\n", offsetof({cname}, {f}));')
     lines.append("  return 0;\n}")
     src = tmp_path / "layout.c"
     src.write_text("\n".join(lines))
