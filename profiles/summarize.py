@@ -44,7 +44,9 @@ def main(tag="r2a", precision="fp64", n_envs=4096, timed=50, src=None):
         rows = [r for r in csv.DictReader(open(os.path.join(src, sub, f"{sub}_counter_collection.csv")))
                 if is_step(r["Kernel_Name"])]
         rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-        return [float(r["Counter_Value"]) for r in rows][-timed - STATS_STEPS:-STATS_STEPS], rows[0]
+        # (the timed window's kernel: the first dispatch is the reset launch, which is always the
+        # one-wave-per-pair instance)
+        return [float(r["Counter_Value"]) for r in rows][-timed - STATS_STEPS:-STATS_STEPS], rows[-1 - STATS_STEPS]
     fetch, row = pmc("FETCH_SIZE")
     write, _ = pmc("WRITE_SIZE")
     f_kib, w_kib = statistics.mean(fetch), statistics.mean(write)
