@@ -2050,10 +2050,14 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
   {
     if (s0 > 0) {   // queued last substep: wait for the pair's first chunk to hand the state over
       int* flag = ka->b.qsync + QS_FLAG + pair;
-      if (lane == 0)   // (bounded: a broken protocol shows up as wrong results, not a hung GPU)
-        for (int w = 0; w < (1 << 22) && __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != s0; w++)
+      int seen = s0;
+      if (lane == 0) {   // bounded (~0.5 s): a broken hand-off must not hang the GPU
+        int w = 0;
+        while ((seen = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != s0 && ++w < (1 << 22))
           __builtin_amdgcn_s_sleep(2);
-      if (lane == 0) __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
+        __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
+      }
+      const bool lost = __builtin_amdgcn_readfirstlane(seen) != s0;
       WSYNC();   // (compiler order: the row loads stay behind the poll)
       const T* r = ka->b.mid + (size_t)env_id * MIDDIM;
       time = r[MID_TIME];
@@ -2063,6 +2067,9 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
       if (sl < nv) s.qvel[sl] = r[MID_V + sl];
 #pragma unroll
       for (int w = 0; w < NWARN; w++) warn[w] = (int)r[MID_W + w];
+      // never seen in practice; if it were, the state is poisoned so that mj_checkPos resets the
+      // env and counts HS_WARN_BADQPOS -- loud, like MuJoCo's warning path, never silent
+      if (lost && sl == 2) s.qpos[2] = T(NAN);
     } else {
       time = ka->b.time[env_id];
       xws = (sl < nv) ? ka->b.qacc_ws[(size_t)env_id * nv + sl] : T(0);
