@@ -2336,22 +2336,25 @@ __global__ __launch_bounds__(64) void kin_kernel(MPtr<T> m, const T* __restrict_
 
 }  // namespace
 
-// waves of the resident step-kernel instance the device holds at once (occupancy x CUs), cached
+// waves of the resident step-kernel instance the current device holds at once (occupancy x CUs),
+// cached per device (a racing first call computes the same value twice: benign)
 template <typename T>
 int resident_waves(bool pgs) {
-  static int cache[2] = {-1, -1};
-  int& c = cache[pgs ? 1 : 0];
-  if (c < 0) {
-    int dev = 0, per_cu = 0;
-    hipDeviceProp_t prop;
-    hipError_t e = hipGetDevice(&dev);
-    if (e == hipSuccess) e = hipGetDeviceProperties(&prop, dev);
-    if (e == hipSuccess)
-      e = pgs ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<T, 27, true>, WAVE, 0)
-              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<T, 27, false>, WAVE, 0);
-    c = (e == hipSuccess && per_cu > 0) ? per_cu * prop.multiProcessorCount : 0;
-  }
-  return c;
+  constexpr int MAXDEV = 64;
+  static int cache[2][MAXDEV] = {};   // 0: not yet computed
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 0;
+  int* c = dev < MAXDEV ? &cache[pgs ? 1 : 0][dev] : nullptr;
+  if (c && *c != 0) return *c > 0 ? *c : 0;
+  int per_cu = 0, v = -1;
+  hipDeviceProp_t prop;
+  hipError_t e = hipGetDeviceProperties(&prop, dev);
+  if (e == hipSuccess)
+    e = pgs ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<T, 27, true>, WAVE, 0)
+            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, step_kernel<T, 27, false>, WAVE, 0);
+  if (e == hipSuccess && per_cu > 0) v = per_cu * prop.multiProcessorCount;
+  if (c) *c = v;
+  return v > 0 ? v : 0;
 }
 
 template <typename T>
