@@ -1,7 +1,7 @@
 """Learning-curve sanity of the on-device PPO (SB3 is not importable, so the trainer
 is judged by the stand reward rising).  bench.py's train config: 4096 envs, n_steps 32,
 batch 32768, 4 epochs, lr 3e-4, MLP[256,256] ReLU.
-python tests/gpu_learning_curve.py [iters] [stand|kneeling] [fp32|fp64]"""
+python tests/gpu_learning_curve.py [iters] [stand|kneeling] [fp32|fp64] [seed]"""
 import os
 import sys
 import time
@@ -18,10 +18,10 @@ from mujocoposelearning_amd.vec_env import HumanoidVecEnv  # noqa: E402
 XML = os.path.join(ROOT, "mujocoposelearning_amd", "assets", "humanoid.xml")
 
 
-def main(iters=400, reward="stand", precision="fp32"):
+def main(iters=400, reward="stand", precision="fp32", seed=0):
     env = HumanoidVecEnv({"model_path": XML, "duration": 10.0, "reward_config": {"type": reward}, "frame_skip": 3},
-                         n_envs=4096, model=HsModel(XML), seed=0, precision=precision)
-    ppo = PPO(env, n_steps=32, batch_size=32768, n_epochs=4, learning_rate=3e-4, seed=0,
+                         n_envs=4096, model=HsModel(XML), seed=seed, precision=precision)
+    ppo = PPO(env, n_steps=32, batch_size=32768, n_epochs=4, learning_rate=3e-4, seed=seed,
               policy_kwargs={"activation_fn": "ReLU", "net_arch": {"pi": [256, 256], "vf": [256, 256]}})
     t0 = time.perf_counter()
     rows = []
@@ -42,4 +42,4 @@ def main(iters=400, reward="stand", precision="fp32"):
 
 if __name__ == "__main__":
     main(int(sys.argv[1]) if len(sys.argv) > 1 else 400, sys.argv[2] if len(sys.argv) > 2 else "stand",
-         sys.argv[3] if len(sys.argv) > 3 else "fp32")
+         sys.argv[3] if len(sys.argv) > 3 else "fp32", int(sys.argv[4]) if len(sys.argv) > 4 else 0)
