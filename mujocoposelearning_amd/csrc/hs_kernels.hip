@@ -531,6 +531,14 @@ __device__ __forceinline__ int collide_pair(const Scratch<T, C>& s, const int4 i
   const T* a2 = s.u.k.gax[g2];
   const T r1 = sz[0], h1 = sz[1], r2 = sz[2], h2 = sz[3];
   int n = 0;
+  if (fn >= PAIR_SPHERE_SPHERE) {
+    // bounding spheres (radius + half-length, MuJoCo's geom_rbound) apart: no contact.  Exact (a
+    // contact needs dist <= 0 between the geoms, inside both bounds), so only a shortcut -- and when
+    // no lane of the wave holds a near pair, the wave skips the capsule-capsule branch altogether
+    const T d[3] = {p1[0] - p2[0], p1[1] - p2[1], p1[2] - p2[2]};
+    const T R = r1 + h1 + r2 + h2;
+    if (dot3(d, d) > R * R) return 0;
+  }
   if (fn == PAIR_PLANE_SPHERE) {
     n = plane_sphere(p1, a1, p2, r2, c0) ? 1 : 0;
   } else if (fn == PAIR_PLANE_CAPSULE) {
