@@ -438,6 +438,7 @@ struct Scratch {
   uint32_t con_m1[C::CON];    // dof chain masks of the contact's bodies (m1 = 0: world)
   uint32_t con_m2[C::CON];
   T con_mu[C::CON];
+  uint32_t con_act[(C::CON + HL - 1) / HL];   // contacts with a nonzero force (contact_aggregates)
   uint16_t lim_row[MAXDOF];   // joint-limit rows of a dof: (lo row + 1) | (hi row + 1) << 8
   uint32_t dense_mask[C::RPL];   // rows added as dense rank-1 Hessian terms (tendons, body-body)
   int row_kid[C::EFC];
@@ -697,11 +698,15 @@ __device__ __forceinline__ void row_u(MPtr<T> m, const Scratch<T, C>& s, int kin
 }
 
 // per-contact aggregates from current row forces: U = sum D u u' (active rows), F = sum f u
+// and the mask of contacts whose force is nonzero (the others add exact zeros to J'f and the Newton
+// Hessian, so those loops skip them)
 template <typename T, typename C>
 __device__ __forceinline__ void contact_aggregates(MPtr<T> m, Scratch<T, C>& s, int sl) {
+  const bool up = threadIdx.x >= HL;
 #pragma unroll
   for (int cs = 0; cs < C::CON; cs += HL) {
     const int c = cs + sl;
+    bool act = false;
     if (c < s.ncon) {
       int adr = s.con_adr[c];
       int nr = (s.con_bb[c] >> 16) == 1 ? 1 : 4;
@@ -720,9 +725,19 @@ __device__ __forceinline__ void contact_aggregates(MPtr<T> m, Scratch<T, C>& s, 
       }
       for (int k = 0; k < 6; k++) s.con_U[c][k] = U[k];
       for (int k = 0; k < 3; k++) s.con_F[c][k] = F[k];
+      act = F[0] != T(0) || F[1] != T(0) || F[2] != T(0) || U[0] != T(0) || U[1] != T(0) || U[2] != T(0);
     }
+    const uint32_t mk = hballot(act, up);
+    if (sl == 0) s.con_act[cs / HL] = mk;
   }
   WSYNC();
+}
+// for each contact c with a nonzero force, in contact order: f(c)
+template <typename C, typename F>
+__device__ __forceinline__ void for_active_contacts(const uint32_t* act, F&& f) {
+#pragma unroll
+  for (int w = 0; w < (C::CON + HL - 1) / HL; w++)
+    for (uint32_t mk = act[w]; mk; mk &= mk - 1u) f(w * HL + __builtin_ctz(mk));
 }
 
 // (J' f)_i for dof sub-lane i (contacts via point Jacobians, joint limits via the dof's
@@ -730,7 +745,7 @@ __device__ __forceinline__ void contact_aggregates(MPtr<T> m, Scratch<T, C>& s, 
 template <typename T, typename C>
 __device__ __forceinline__ T jtf_lane(MPtr<T> m, const Scratch<T, C>& s, int sl, const T* cd) {
   T acc = 0;
-  for (int c = 0; c < s.ncon; c++) {
+  for_active_contacts<C>(s.con_act, [&](int c) {
     int in2 = bit(s.con_m2[c], sl), in1 = bit(s.con_m1[c], sl);
     if (in1 != in2) {
       T r[3] = {s.con_pos[c][0] - s.com[0], s.con_pos[c][1] - s.com[1], s.con_pos[c][2] - s.com[2]};
@@ -740,7 +755,7 @@ __device__ __forceinline__ T jtf_lane(MPtr<T> m, const Scratch<T, C>& s, int sl,
       T v = dot3(jp, s.con_F[c]);
       acc += in2 ? v : -v;
     }
-  }
+  });
   if (sl < MAXDOF) {
     int lr = s.lim_row[sl];
     int lo = (lr & 0xff) - 1, hi = (lr >> 8) - 1;
@@ -1300,7 +1315,7 @@ struct Stepper {
   __device__ __forceinline__ void solve(T xws, int maxit, T tol, const T (&D)[C::RPL], const T (&ar)[C::RPL],
                                         const int (&rd)[C::RPL], const T (&rc)[C::RPL]) {
     phase_begin();
-    const int nefc = s.nefc, ncon = s.ncon;
+    const int nefc = s.nefc;
     T x = sl < NV ? xws : T(0);
     bool vr[C::RPL];
 #pragma unroll
@@ -1341,9 +1356,9 @@ struct Stepper {
       {
         T aug[6] = {0, 0, 0, 0, 0, 0};
         T dadd = 0;
-        for (int c = 0; c < ncon; c++) {
-          if (s.con_m1[c] != 0u) continue;           // body-body: dense rank-1 rows below
-          if (!bit(s.con_m2[c], sl)) continue;
+        for_active_contacts<C>(s.con_act, [&](int c) {   // (contacts with U = 0 add exact zeros)
+          if (s.con_m1[c] != 0u) return;           // body-body: dense rank-1 rows below
+          if (!bit(s.con_m2[c], sl)) return;
           T r[3] = {s.con_pos[c][0] - s.com[0], s.con_pos[c][1] - s.com[1], s.con_pos[c][2] - s.com[2]};
           T w[3];
           cross3(cd, r, w);
@@ -1354,7 +1369,7 @@ struct Stepper {
           T rz[3];
           cross3(r, z, rz);
           for (int k = 0; k < 3; k++) { aug[k] += rz[k]; aug[3 + k] += z[k]; }
-        }
+        });
         {   // active joint-limit rows of this dof (diagonal)
           int lr = s.lim_row[sl];
           int lo = (lr & 0xff) - 1, hi = (lr >> 8) - 1;
