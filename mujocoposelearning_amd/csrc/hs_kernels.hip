@@ -1387,7 +1387,7 @@ struct Stepper {
         // dense_mask; the loop runs max(#rows of either half) times (wave-uniform control)
         uint32_t dm[C::RPL];
 #pragma unroll
-        for (int q = 0; q < C::RPL; q++) dm[q] = s.dense_mask[q];
+        for (int q = 0; q < C::RPL; q++) dm[q] = s.dense_mask[q] & hballot(act[q], up);   // active ones only
         for (;;) {
           int r = -1;
 #pragma unroll
