@@ -1056,12 +1056,11 @@ struct Stepper {
   __device__ __forceinline__ void mass_matrix() {
     phase_begin();
     if (sl > 0 && sl < nb) {
-      const uint32_t dm = m->body_descmask[sl];
+      const uint32_t dm = m->body_descmask[sl] & ~1u & ((nb < 32 ? (1u << nb) : 0u) - 1u);
       T a[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll 4
-      for (int c = 1; c < nb; c++) {   // predicated (no divergent branch), partially unrolled
-        const bool in = (dm >> c) & 1u;
-        for (int k = 0; k < 10; k++) a[k] += in ? s.cinert[c][k] : T(0);
+      for (uint32_t mk = dm; mk; mk &= mk - 1u) {   // the subtree's bodies only, ascending
+        const int c = __builtin_ctz(mk);
+        for (int k = 0; k < 10; k++) a[k] += s.cinert[c][k];
       }
       for (int k = 0; k < 10; k++) s.u.c.crb[sl][k] = a[k];
     }
@@ -1092,14 +1091,13 @@ struct Stepper {
   // mj_comVel (cvel, cdof_dot), mj_passive, mj_fwdActuation, mj_rne -> fsmooth
   __device__ __forceinline__ void velocity_forces() {
     phase_begin();
-    int nv = m->nv;
     if (sl < nb) {
       T v[6] = {0, 0, 0, 0, 0, 0};
       if (sl > 0) {
         const uint32_t ch = m->body_chainmask[sl];
-#pragma unroll 4
-        for (int j = 0; j < nv; j++) {
-          const T q = ((ch >> j) & 1u) ? s.qvel[j] : T(0);
+        for (uint32_t mk = ch; mk; mk &= mk - 1u) {   // the chain's dofs only, ascending
+          const int j = __builtin_ctz(mk);
+          const T q = s.qvel[j];
           for (int k = 0; k < 6; k++) v[k] = fma(s.cdof[j][k], q, v[k]);
         }
       }
@@ -1108,9 +1106,9 @@ struct Stepper {
     if (sl < NV) {
       const uint32_t dm = m->dof_dotmask[sl];
       T v[6] = {0, 0, 0, 0, 0, 0}, cdd[6];
-#pragma unroll 4
-      for (int j = 0; j < nv; j++) {
-        const T q = ((dm >> j) & 1u) ? s.qvel[j] : T(0);
+      for (uint32_t mk = dm; mk; mk &= mk - 1u) {   // ascending, set bits only
+        const int j = __builtin_ctz(mk);
+        const T q = s.qvel[j];
         for (int k = 0; k < 6; k++) v[k] = fma(s.cdof[j][k], q, v[k]);
       }
       cross_motion(v, cd, cdd);
@@ -1120,9 +1118,9 @@ struct Stepper {
     if (sl > 0 && sl < nb) {   // RNE: cacc, cfrc_body
       const uint32_t ch = m->body_chainmask[sl];
       T a[6] = {0, 0, 0, -m->gravity[0], -m->gravity[1], -m->gravity[2]};
-#pragma unroll 4
-      for (int j = 0; j < nv; j++) {
-        const T q = ((ch >> j) & 1u) ? s.qvel[j] : T(0);
+      for (uint32_t mk = ch; mk; mk &= mk - 1u) {   // the chain's dofs only, ascending
+        const int j = __builtin_ctz(mk);
+        const T q = s.qvel[j];
         for (int k = 0; k < 6; k++) a[k] = fma(s.u.r.cdofdot[j][k], q, a[k]);
       }
       T f[6], t[6], t2[6];
@@ -1133,12 +1131,11 @@ struct Stepper {
     }
     WSYNC();
     if (sl > 0 && sl < nb) {   // subtree sums of cfrc_body
-      const uint32_t dm = m->body_descmask[sl];
+      const uint32_t dm = m->body_descmask[sl] & ~1u & ((nb < 32 ? (1u << nb) : 0u) - 1u);
       T a[6] = {0, 0, 0, 0, 0, 0};
-#pragma unroll 4
-      for (int c = 1; c < nb; c++) {
-        const bool in = (dm >> c) & 1u;
-        for (int k = 0; k < 6; k++) a[k] += in ? s.u.r.cfrc[c][k] : T(0);
+      for (uint32_t mk = dm; mk; mk &= mk - 1u) {   // the subtree's bodies only, ascending
+        const int c = __builtin_ctz(mk);
+        for (int k = 0; k < 6; k++) a[k] += s.u.r.cfrc[c][k];
       }
       for (int k = 0; k < 6; k++) s.u.r.csub[sl][k] = a[k];
     }
