@@ -1029,16 +1029,26 @@ struct Stepper {
     phase_begin();
     int ncon = 0;
     const int npair = m->npair;
+    // the next pass's pair records are loaded while this pass runs (their L1/L2 latency is otherwise
+    // exposed at the top of every pass: one wave per SIMD in fp64)
+    int4 info_n = make_int4(0, 0, 0, 0);
+    T sz_n[4] = {0, 0, 0, 0};
+    if (sl < npair) {
+      info_n = make_int4(m->pair_info[sl][0], m->pair_info[sl][1], m->pair_info[sl][2], m->pair_info[sl][3]);
+      for (int k = 0; k < 4; k++) sz_n[k] = m->pair_size[sl][k];
+    }
     for (int base = 0; base < npair; base += HL) {
       int p = base + sl;
       Con<T> c0, c1;
       int n = 0;
-      if (p < npair) {
-        const int4 info = make_int4(m->pair_info[p][0], m->pair_info[p][1], m->pair_info[p][2], m->pair_info[p][3]);
-        T sz[4];
-        for (int k = 0; k < 4; k++) sz[k] = m->pair_size[p][k];
-        n = collide_pair(s, info, sz, c0, c1);
+      const int4 info = info_n;
+      T sz[4] = {sz_n[0], sz_n[1], sz_n[2], sz_n[3]};
+      if (p + HL < npair) {
+        info_n = make_int4(m->pair_info[p + HL][0], m->pair_info[p + HL][1], m->pair_info[p + HL][2],
+                           m->pair_info[p + HL][3]);
+        for (int k = 0; k < 4; k++) sz_n[k] = m->pair_size[p + HL][k];
       }
+      if (p < npair) n = collide_pair(s, info, sz, c0, c1);
       uint32_t m1 = hballot(n >= 1, up), m2 = hballot(n >= 2, up);
       int pre = below(m1, sl) + below(m2, sl);
       if (n >= 1) store_contact(m, s, ncon + pre, c0, p);
