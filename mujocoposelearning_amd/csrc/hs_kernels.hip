@@ -1356,8 +1356,8 @@ struct Stepper {
       HS_STAMP(clk, 7);
       T jtf = jtf_lane(m, s, sl, cd);
       T g = sl < NV ? Mx - fsmooth - jtf : T(0);
-      T gn = sqrt(hsum(g * g));
-      done = done || (scale * gn < tol);
+      const T gn2 = hsum(g * g);                 // |g| scale < tol, squared (no sqrt on the chain)
+      done = done || (scale * scale * gn2 < tol * tol);
       HS_STAMP(clk, 8);
       if (__ballot(!done) == 0) break;       // both envs of the wave converged
       // Hessian lower rows: M + contact (tree form) + joint limits (diag) + dense rank-1 rows
