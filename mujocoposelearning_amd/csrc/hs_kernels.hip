@@ -348,7 +348,7 @@ __device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb)[2
 // stops changing once y_k = b_k / L_kk is broadcast, and y = b / L_ii at the end.
 template <int NV, typename T>
 __device__ __forceinline__ T chol_solve(const T (&L)[NV], T dinv, T b, int sl) {
-  static_for<0, NV>([&](auto kc) {
+  static_for<0, NV - 1>([&](auto kc) {      // column NV - 1 has no row below it: skipped
     constexpr int k = decltype(kc)::value;
     b = fma(-L[k], bcast<k>(b * dinv), b);
   });
@@ -384,7 +384,7 @@ __device__ __forceinline__ T chol_solve(const T (&L)[NV], T dinv, T b, int sl) {
 // sub-lanes >= NV, where dinv = 0)
 template <int NV, int G, typename T>
 __device__ __forceinline__ void chol_fwd_multi(const T (&L)[NV], T dinv, T (&b)[G], int sl) {
-  static_for<0, NV>([&](auto kc) {
+  static_for<0, NV - 1>([&](auto kc) {      // the last column changes no row: skipped
     constexpr int k = decltype(kc)::value;
     static_for<0, G>([&](auto gc) {
       constexpr int g = decltype(gc)::value;
