@@ -290,8 +290,24 @@ def main():
         barrier()
         return max_over_ranks(time.perf_counter() - t0), ev0.elapsed_time(ev1) / steps
 
+    def ints_over_ranks(vals, op):
+        """elementwise MAX / SUM of a list of per-rank integer counters over all ranks"""
+        t = torch.tensor(vals, dtype=torch.int64, device=red_dev)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM)
+        return [int(x) for x in t.tolist()]
+
+    def warn_stats(e):
+        """per-env warning counters (bad qpos / qvel / qacc, contact overflow) summed over the
+        rank's envs, reported as the MAX over ranks (and the node SUM), plus wide-tier re-runs"""
+        w = [int(x) for x in e.batch.warning.sum(0).tolist()]
+        rr = int(e.batch.wide_reruns())
+        return dict(warnings=ints_over_ranks(w, "max"), warnings_node_sum=ints_over_ranks(w, "sum"),
+                    wide_tier_reruns=ints_over_ranks([rr], "max")[0])
+
     def stats_of(e, tape, k0, steps=3):
-        """aux-row statistics of a few further (untimed) steps of the same batch."""
+        """aux-row statistics of a few further (untimed) steps of the same batch (this rank's envs;
+        the warning counters are reduced over ranks)."""
         e.batch.configure(aux=True)
         for k in range(steps):
             e.step_tensors(tape[(k0 + k) % tape.shape[0]])
@@ -300,8 +316,7 @@ def main():
         return dict(mean_contacts=float(a[:, 35].mean()), max_contacts=int(a[:, 35].max()),
                     mean_rows=float(a[:, 36].mean()), max_rows=int(a[:, 36].max()),
                     mean_newton_iters=float(a[:, 37].mean()),
-                    fallen_frac=float((e.batch.qpos[:, 2] < 0.8).double().mean()),
-                    warnings=e.batch.warning.sum(0).tolist(), wide_tier_reruns=e.batch.wide_reruns())
+                    fallen_frac=float((e.batch.qpos[:, 2] < 0.8).double().mean()), **warn_stats(e))
 
     if args.protocol:
         return run_protocol(args, rank, world, ranks, make_env, make_tape, precondition, timed, stats_of)
@@ -352,8 +367,7 @@ def main():
                                 mean_newton_iters=float(ax[:, 37].mean()),
                                 fallen_frac=float((e.batch.qpos[:, 2] < 0.8).double().mean())))
             episodes[kind] = dict(value=n * EPISODE * ranks / tot_t, unit="env_steps/s", steps=EPISODE,
-                                  phases=per, warnings=e.batch.warning.sum(0).tolist(),
-                                  wide_tier_reruns=e.batch.wide_reruns())
+                                  phases=per, **warn_stats(e))
             e.close()
 
     # ---- rollout mode: policy MLP[256,256] forward + sampling + env step (on device)

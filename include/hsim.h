@@ -15,6 +15,7 @@
  *   hs_step              <- HumanoidEnv.step: frame_skip x mj_step, _get_state, reward, done
  *                           custom_env.py:152-230 (+ SB3 auto-reset on done)
  *   hs_physics_step      <- raw `data.ctrl[:] = a; mujoco.mj_step(model, data)` custom_env.py:159-160
+ *   hs_debug_lose_handoff   (test hook: mj_step's warning + mj_resetData path, custom_env.py:160)
  *   hs_state_io          <- reads/writes of data.qpos/qvel/qacc_warmstart/time/ctrl (custom_env.py:105-117)
  *   hs_get_buffers       <- data.* arrays as device buffers (obs, reward, terminated, ...)
  *   hs_last_error        <- mujoco's error callback / MjModel load error string
@@ -86,11 +87,14 @@ typedef struct {
   int schedule;            /* HS_SCHED_*: how the step kernel maps env pairs to waves [AUTO] */
 } hs_env_config;
 
-/* hs_env_config.schedule.  AUTO: one wave per env pair when every pair fits on the GPU at once,
- * else (the fp64 engine at 4096 envs) a persistent grid that runs each env step as two chunk items
- * (substeps [0, frame_skip - 1), then the last substep + obs / reward / auto-reset) from a queue.
- * DIRECT: always one wave per pair.  Results are bitwise identical either way. */
-enum { HS_SCHED_AUTO = 0, HS_SCHED_DIRECT = 1 };
+/* hs_env_config.schedule.  AUTO: one wave per env (the upper half-wave mirrors the lower one and
+ * commits nothing) when every env gets a resident wave of its own (small batches, e.g. configs[4]'s
+ * 1024 envs per GPU); else one wave per env pair when every pair fits on the GPU at once; else (the
+ * fp64 engine at 4096 envs) a persistent grid that runs each env step as two chunk items (substeps
+ * [0, frame_skip - 1), then the last substep + obs / reward / auto-reset) from a queue.
+ * DIRECT: always one wave per pair.  SINGLE: always one wave per env.  Results are bitwise
+ * identical whichever schedule runs. */
+enum { HS_SCHED_AUTO = 0, HS_SCHED_DIRECT = 1, HS_SCHED_SINGLE = 2 };
 
 /* Device buffers of a batch (row-major, env-major).  Element type of the T* entries is float
  * (HS_FP32) or double (HS_FP64). */
@@ -156,8 +160,18 @@ int hs_step(hs_batch* b, const float* actions, void* stream);
  * SubprocVecEnv-exact mode where worker i continues its own np.random stream seeded with
  * seed + i (custom_env.py:99-110, SB3 VecEnv.seed).  The arrays stay owned by the caller. */
 int hs_set_autoreset_noise(hs_batch* b, const void* qpos_noise, const void* qvel_noise);
-/* ctrl: [N][nu] float32 device (NULL = keep current ctrl).  nsub raw mj_step's, obs refreshed. */
+/* ctrl: [N][nu] float32 device (NULL = keep current ctrl).  nsub raw mj_step's, obs refreshed.
+ * Resets and raw physics calls always write data.ctrl; env steps (hs_step) only with HS_OUT_CTRL.
+ * After an hs_step with HS_OUT_CTRL off the ctrl buffer no longer holds data.ctrl, and until it is
+ * rewritten (a full hs_reset, an hs_physics_step with ctrl, an hs_state_io set of ctrl) both
+ * hs_physics_step(ctrl = NULL) and an hs_state_io get of ctrl fail instead of using it. */
 int hs_physics_step(hs_batch* b, const float* ctrl, int nsub, void* stream);
+/* Test hook of the chunk-queue schedule (never used on the product path): from the next launch on,
+ * the hand-off of env `env`'s pair (env / 2) is treated as lost by its last-substep item, exactly as
+ * if its bounded wait had timed out -- the env is poisoned (qpos[2] = NaN), so mj_checkPos resets it
+ * (MuJoCo's warning path: HS_WARN_BADQPOS += 1, qpos0, time 0) and the step continues from there.
+ * env = -1 turns it off.  Only launches on the queued schedule consult it. */
+int hs_debug_lose_handoff(hs_batch* b, int env);
 
 /* Synchronous host<->device state copy in fp64.  dir 0: device -> host, 1: host -> device.
  * Any pointer may be NULL.  Arrays are [N][nq], [N][nv], [N][nv], [N], [N][nu]. */

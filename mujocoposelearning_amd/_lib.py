@@ -18,7 +18,7 @@ HS_REWARD_NONE, HS_REWARD_STAND, HS_REWARD_KNEELING, HS_REWARD_WALK = -1, 0, 1, 
 HS_NWARN = 4
 HS_AUXDIM = 40
 HS_OUT_AUX, HS_OUT_CTRL = 1, 2   # hs_env_config.outputs bits
-HS_SCHED_AUTO, HS_SCHED_DIRECT = 0, 1   # hs_env_config.schedule
+HS_SCHED_AUTO, HS_SCHED_DIRECT, HS_SCHED_SINGLE = 0, 1, 2   # hs_env_config.schedule
 DBGDIM = 32768
 
 
@@ -78,6 +78,7 @@ def lib():
         "hs_state_io": (i, [vp, i, vp, vp, vp, vp, vp]),
         "hs_kinematics": (i, [vp, i, vp, vp, vp, vp, vp, vp]),
         "hs_set_debug": (i, [vp, i]),
+        "hs_debug_lose_handoff": (i, [vp, i]),
         "hs_get_debug": (i, [vp, vp, i]),
         "hs_synchronize": (i, [vp]),
         "hs_batch_counters": (i, [vp, vp]),
@@ -110,7 +111,7 @@ def lib():
 
 EXPORTED = ("hs_model_load", "hs_model_free", "hs_model_field", "hs_batch_create", "hs_batch_destroy",
             "hs_batch_get_info", "hs_get_buffers", "hs_set_config", "hs_set_seed", "hs_get_config", "hs_reset", "hs_step", "hs_set_autoreset_noise",
-            "hs_physics_step", "hs_state_io", "hs_kinematics", "hs_set_debug", "hs_get_debug", "hs_synchronize", "hs_batch_counters", "hs_gae",
+            "hs_physics_step", "hs_state_io", "hs_kinematics", "hs_set_debug", "hs_debug_lose_handoff", "hs_get_debug", "hs_synchronize", "hs_batch_counters", "hs_gae",
             "hs_ppo_act", "hs_ppo_post", "hs_gauss_logp", "hs_gauss_logp_grad",
             "hs_ppo_loss_workspace", "hs_ppo_loss", "hs_ppo_loss_grad", "hs_adam_workspace", "hs_adam_clip",
             "hs_colsum_partial_rows", "hs_relu_grad_colsum", "hs_colsum_pair",

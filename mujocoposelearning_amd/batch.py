@@ -89,6 +89,17 @@ class HsBatch:
         n = max(hi - lo for _, lo, hi in self._groups)
         return (self.cfg.schedule == _lib.HS_SCHED_AUTO and nsub >= 2 and 0 < self.resident_waves < (n + 1) // 2)
 
+    def schedule_name(self, nsub=None):
+        """The schedule an env step of this batch runs on (the largest group's; hs_kernels.hip
+        launch_step): "queue" (chunk queue), "single" (one wave per env) or "paired"."""
+        if self.queued(nsub):
+            return "queue"
+        n = max(hi - lo for _, lo, hi in self._groups)
+        s = self.cfg.schedule
+        if s == _lib.HS_SCHED_SINGLE or (s == _lib.HS_SCHED_AUTO and 0 < self.resident_waves and n <= self.resident_waves):
+            return "single"
+        return "paired"
+
     # -- tensors (device views, valid until the next call) ---------------------------------
     def __getattr__(self, name):
         t = self.__dict__.get("t")
@@ -104,9 +115,10 @@ class HsBatch:
     def configure(self, frame_skip=None, duration=None, reward_id=None, max_steps=None, autoreset=None,
                   max_newton=None, init_height=None, noise_scale=None, kneel_params=None, aux=None, ctrl=None,
                   schedule=None):
-        """``schedule``: "auto" (default; a chunk queue when the env pairs outnumber the resident
-        waves, see include/hsim.h HS_SCHED_AUTO) or "direct" (one wave per env pair); results are
-        bitwise identical.
+        """``schedule``: "auto" (default: one wave per env when every env fits the resident waves, a
+        chunk queue when the env pairs outnumber them, else one wave per env pair; include/hsim.h
+        HS_SCHED_AUTO), "direct" (one wave per env pair) or "single" (one wave per env); results
+        are bitwise identical.
         ``aux`` / ``ctrl``: write the optional aux row (qacc, subtree com, contact / row counts,
         solver iterations) and the data.ctrl copy at every commit (both on by default; data views,
         host rewards and statistics read them, the on-device trainer does not)."""
@@ -116,7 +128,8 @@ class HsBatch:
         if ctrl is not None:
             c.outputs = (c.outputs & ~_lib.HS_OUT_CTRL) | (_lib.HS_OUT_CTRL if ctrl else 0)
         if schedule is not None:
-            c.schedule = {"auto": _lib.HS_SCHED_AUTO, "direct": _lib.HS_SCHED_DIRECT}[schedule]
+            c.schedule = {"auto": _lib.HS_SCHED_AUTO, "direct": _lib.HS_SCHED_DIRECT,
+                          "single": _lib.HS_SCHED_SINGLE}[schedule]
         if frame_skip is not None:
             c.frame_skip = int(frame_skip)
         if duration is not None:
@@ -243,12 +256,16 @@ class HsBatch:
 
     # -- host state access (through the C ABI, synchronous, fp64) ---------------------------
     def get_state(self):
+        """qpos / qvel / qacc_warmstart / time (and ctrl, while the data.ctrl copy is written:
+        ``configure(ctrl=True)``, the default) as fp64 host arrays."""
         N, m = self.n, self.model
         out = dict(qpos=np.zeros((N, m.nq)), qvel=np.zeros((N, m.nv)), qacc_warmstart=np.zeros((N, m.nv)),
                    time=np.zeros(N), ctrl=np.zeros((N, m.nu)))
         keys = ("qpos", "qvel", "qacc_warmstart", "time", "ctrl")
+        if not self.cfg.outputs & _lib.HS_OUT_CTRL:
+            del out["ctrl"]
         for h, lo, hi in self._groups:
-            check(lib().hs_state_io(h, 0, *[out[k][lo:hi].ctypes.data for k in keys]))
+            check(lib().hs_state_io(h, 0, *[out[k][lo:hi].ctypes.data if k in out else None for k in keys]))
         return out
 
     def set_state(self, qpos=None, qvel=None, qacc_warmstart=None, time=None, ctrl=None):
@@ -284,6 +301,14 @@ class HsBatch:
 
     def set_debug(self, on=True):
         check(lib().hs_set_debug(self._h, int(bool(on))))
+
+    def debug_lose_handoff(self, env):
+        """Test hook (hs_debug_lose_handoff): the chunk-queue hand-off of ``env``'s pair is treated
+        as lost in the following queued launches (the env is poisoned and mj_checkPos resets it);
+        ``env=None`` turns it off."""
+        for h, lo, hi in self._groups:
+            inside = env is not None and lo <= int(env) < hi
+            check(lib().hs_debug_lose_handoff(h, int(env) - lo if inside else -1))
 
     def get_debug(self):
         out = np.zeros(_lib.DBGDIM)

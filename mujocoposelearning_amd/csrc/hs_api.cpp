@@ -30,6 +30,8 @@ struct hs_batch {
   void* mid = nullptr;                       // chunk-queue hand-off rows [n][MIDDIM] (kernel-managed)
   int* qsync = nullptr;                      // chunk queue claim / exit counters, pair flags (qsync_words)
   hs_env_config cfg{};
+  bool ctrl_stale = false;                   // env steps ran with HS_OUT_CTRL off: buf.ctrl is not data.ctrl
+  int lose_pair1 = 0;                        // hs_debug_lose_handoff test hook (pair + 1; 0 = off)
 };
 
 namespace {
@@ -107,6 +109,7 @@ hs::StepParams params_of(const hs_batch* b, int mode, int nsub) {
   p.solver = b->model->host.solver == 1 ? hs::SOLVER_PGS : hs::SOLVER_NEWTON;
   p.outputs = b->cfg.outputs;
   p.schedule = b->cfg.schedule;
+  p.dbg_lose_pair1 = b->lose_pair1;
   return p;
 }
 
@@ -384,7 +387,8 @@ int hs_set_config(hs_batch* b, const hs_env_config* cfg) {
   if (cfg->max_newton < 1) return fail("max_newton must be >= 1");
   if (cfg->reward_id < HS_REWARD_NONE || cfg->reward_id > HS_REWARD_WALK) return fail("unknown reward id");
   if (cfg->outputs & ~(HS_OUT_AUX | HS_OUT_CTRL)) return fail("unknown output bits");
-  if (cfg->schedule != HS_SCHED_AUTO && cfg->schedule != HS_SCHED_DIRECT) return fail("unknown schedule");
+  if (cfg->schedule != HS_SCHED_AUTO && cfg->schedule != HS_SCHED_DIRECT && cfg->schedule != HS_SCHED_SINGLE)
+    return fail("unknown schedule");
   b->cfg = *cfg;
   return 0;
 }
@@ -402,13 +406,24 @@ int hs_get_config(const hs_batch* b, hs_env_config* cfg) {
 }
 
 int hs_reset(hs_batch* b, const uint8_t* mask, const void* qpos_noise, const void* qvel_noise, void* stream) {
-  return launch(b, hs::MODE_RESET, nullptr, mask, qpos_noise, qvel_noise, 1, stream);
+  int rc = launch(b, hs::MODE_RESET, nullptr, mask, qpos_noise, qvel_noise, 1, stream);
+  if (rc == 0 && !mask) b->ctrl_stale = false;     // every env's data.ctrl is 0 again (mj_resetData)
+  return rc;
 }
 
 int hs_step(hs_batch* b, const float* actions, void* stream) {
   if (!actions) return fail("hs_step: actions must not be NULL");
   if (!b) return fail("null batch");
-  return launch(b, hs::MODE_ENV_STEP, actions, nullptr, b->ar_qpos_noise, b->ar_qvel_noise, b->cfg.frame_skip, stream);
+  int rc = launch(b, hs::MODE_ENV_STEP, actions, nullptr, b->ar_qpos_noise, b->ar_qvel_noise, b->cfg.frame_skip, stream);
+  if (rc == 0 && !(b->cfg.outputs & HS_OUT_CTRL)) b->ctrl_stale = true;
+  return rc;
+}
+
+int hs_debug_lose_handoff(hs_batch* b, int env) {
+  if (!b) return fail("null batch");
+  if (env < -1 || env >= b->n) return fail("env index out of range");
+  b->lose_pair1 = env < 0 ? 0 : env / 2 + 1;
+  return 0;
 }
 
 int hs_set_autoreset_noise(hs_batch* b, const void* qpos_noise, const void* qvel_noise) {
@@ -421,12 +436,21 @@ int hs_set_autoreset_noise(hs_batch* b, const void* qpos_noise, const void* qvel
 
 int hs_physics_step(hs_batch* b, const float* ctrl, int nsub, void* stream) {
   if (nsub < 1) return fail("nsub must be >= 1");
-  return launch(b, hs::MODE_PHYSICS, ctrl, nullptr, nullptr, nullptr, nsub, stream);
+  if (!b) return fail("null batch");
+  if (!ctrl && b->ctrl_stale)
+    return fail("hs_physics_step: ctrl == NULL keeps data.ctrl, but env steps ran with HS_OUT_CTRL off so the "
+                "ctrl buffer is stale; pass ctrl, set it with hs_state_io, or enable HS_OUT_CTRL");
+  int rc = launch(b, hs::MODE_PHYSICS, ctrl, nullptr, nullptr, nullptr, nsub, stream);
+  if (rc == 0 && ctrl) b->ctrl_stale = false;
+  return rc;
 }
 
 int hs_state_io(hs_batch* b, int dir, double* qpos, double* qvel, double* qacc_warmstart, double* time, double* ctrl) {
   if (!b) return fail("null batch");
   if (dir != 0 && dir != 1) return fail("dir must be 0 (get) or 1 (set)");
+  if (dir == 0 && ctrl && b->ctrl_stale)
+    return fail("hs_state_io: ctrl requested, but env steps ran with HS_OUT_CTRL off (the ctrl buffer is stale)");
+  if (dir == 1 && ctrl) b->ctrl_stale = false;
   DeviceGuard g(b->device);
   if (!hip_ok(hipDeviceSynchronize(), "sync")) return -1;
   return b->precision == HS_FP64 ? state_io<double>(b, dir, qpos, qvel, qacc_warmstart, time, ctrl)

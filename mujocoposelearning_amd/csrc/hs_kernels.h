@@ -14,6 +14,8 @@ constexpr int DBGDIM = 32768;        // stage dump (env 0 only) for parity debug
 constexpr int MID_Q = 0, MID_V = MAXQ, MID_WS = MAXQ + MAXDOF, MID_TIME = MAXQ + 2 * MAXDOF, MID_W = MID_TIME + 1;
 constexpr int MIDDIM = MID_W + 7;
 // chunk-queue sync words (uncached device memory): claim counter, exit counter, per-pair flags
+// (0 idle; s1 = state handed over; -1 = abandoned by a consumer that timed out -- the late producer
+// resets it; every flag is 0 again when a launch ends)
 constexpr int QS_HEAD = 0, QS_EXIT = 1, QS_FLAG = 2;
 constexpr size_t qsync_words(int n_envs) { return QS_FLAG + (size_t)((n_envs + 1) / 2); }
 
@@ -69,7 +71,10 @@ struct StepParams {
   int schedule;          // HS_SCHED_AUTO (0) / HS_SCHED_DIRECT (1) (hs_env_config.schedule)
   int queue;             // set by launch_step: 1 = chunk-queue schedule (persistent grid), 0 = one wave per pair
   int qmul;              // chunk-queue claim order: item i -> pair (i * qmul) mod npairs (qmul coprime to npairs)
+  int dbg_lose_pair1;    // test hook (hs_debug_lose_handoff): pair + 1 whose hand-off is treated as lost; 0 = off
+  int single;            // set by launch_step: 1 = one env per wave (upper half-wave a ghost), 0 = env pairs
 };
+enum Schedule { SCHED_AUTO = 0, SCHED_DIRECT = 1, SCHED_SINGLE = 2 };   // hs_env_config.schedule
 // optional outputs (hs_env_config.outputs): the aux row (qacc, subtree com, ncon, nefc, solver
 // iterations -- data views and stats) and the data.ctrl copy (data views / host rewards)
 enum Outputs { OUT_AUX = 1, OUT_CTRL = 2 };

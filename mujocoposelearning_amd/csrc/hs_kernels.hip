@@ -445,6 +445,7 @@ struct Scratch {
   T row_D[C::EFC];
   T row_f[C::EFC];
   int ncon, nefc, nlim, njl;   // njl: joint-limit rows (tendon rows are [njl, nlim))
+  int niter;                   // this env's Newton iterations (the wave's loop runs for the slower env)
   union {   // phase-local arrays (aliased)
     struct { T xpos[MAXBODY][3]; T xmat[MAXBODY][9]; T xquat[MAXBODY][4]; T xanchor[MAXJNT][3];
              T xaxis[MAXJNT][3]; T gpos[MAXGEOM][3]; T gax[MAXGEOM][3]; } k;   // kinematics + collision
@@ -1342,6 +1343,7 @@ struct Stepper {
     HS_STAMP(clk, 6);
     bool done = false;      // this half-wave's solver has converged
     int it = 0;
+    if (sl == 0) s.niter = maxit;   // per env: the iteration at which this half converged
     for (; it < maxit; it++) {
       m = opaque(m);
       sl = opaque_v(sl);
@@ -1357,7 +1359,9 @@ struct Stepper {
       T jtf = jtf_lane(m, s, sl, cd);
       T g = sl < NV ? Mx - fsmooth - jtf : T(0);
       const T gn2 = hsum(g * g);                 // |g| scale < tol, squared (no sqrt on the chain)
-      done = done || (scale * scale * gn2 < tol * tol);
+      const bool conv = scale * scale * gn2 < tol * tol;
+      if (conv && !done && sl == 0) s.niter = it;
+      done = done || conv;
       HS_STAMP(clk, 8);
       if (__ballot(!done) == 0) break;       // both envs of the wave converged
       // Hessian lower rows: M + contact (tree form) + joint limits (diag) + dense rank-1 rows
@@ -1503,11 +1507,15 @@ struct Stepper {
           changed = changed || (vr[q] && ((nj < 0) != act[q]));
           jar[q] = nj;
         }
-        if (hballot(changed, up) == 0 && fabs(alpha - T(1)) < T(1e-3)) done = true;
+        if (hballot(changed, up) == 0 && fabs(alpha - T(1)) < T(1e-3)) {
+          done = true;
+          if (sl == 0) s.niter = it + 1;
+        }
       }
       if (__ballot(!done) == 0) { it++; break; }
     }
-    niter = it;
+    WSYNC();
+    niter = s.niter;
     // final forces -> qfrc_constraint
 #pragma unroll
     for (int q = 0; q < C::RPL; q++)
@@ -2025,7 +2033,9 @@ __device__ __forceinline__ void commit(MPtr<T> m, KPtr<T> k, const Stepper<T, NV
     k->b.qacc_ws[(size_t)env * nv + sl] = xws;
     if (outputs & OUT_AUX) k->b.aux[(size_t)env * AUXDIM + sl] = st.qacc;
   }
-  if (sl < nu && (outputs & OUT_CTRL)) k->b.ctrl[(size_t)env * nu + sl] = s.ctrl[sl];
+  // data.ctrl: always for resets and raw physics calls (rare); for env steps only with OUT_CTRL
+  // (the host marks the buffer stale otherwise, hs_api.cpp)
+  if (sl < nu && ((outputs & OUT_CTRL) || k->p.mode != MODE_ENV_STEP)) k->b.ctrl[(size_t)env * nu + sl] = s.ctrl[sl];
   if (sl == 0) {
     k->b.time[env] = time;
     k->b.step_count[env] = step_count;
@@ -2060,15 +2070,16 @@ __device__ __forceinline__ void commit(MPtr<T> m, KPtr<T> k, const Stepper<T, NV
 // stale L1 / L2 line: no cache invalidate or write-back on either side.  Every chunk recomputes the whole mj_step
 // pipeline from (qpos, qvel, qacc_warmstart, time), so the hand-off is exact: results are bitwise
 // those of one wave running all substeps.
+// ghost: this half-wave mirrors env idx (the single-env schedule's upper half) and commits nothing.
 template <typename T, int NV, bool PGS, typename C>
 __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCache<T, C>* pcache, int idx,
-                                          int nidx, const int* list, int s0, int s1, int pair) {
+                                          int nidx, const int* list, int s0, int s1, int pair, bool ghost = false) {
   constexpr bool WIDE = C::WIDE;
   const int lane = opaque_v(threadIdx.x);   // (no lane-derived value hoisted out of the chunk-queue loop)
   const bool up = lane >= HL;
   const int sl = lane & (HL - 1);
-  bool active = idx < nidx;                           // ghost half for an odd count
-  const int ei = active ? idx : nidx - 1;
+  bool active = idx < nidx && !ghost;                 // ghost half: odd count, or the single-env schedule
+  const int ei = idx < nidx ? idx : nidx - 1;
   const int env_id = list ? list[ei] : ei;
   const int mode = ka->p.mode;
   if (mode == MODE_RESET && ka->reset_mask && !ka->reset_mask[env_id]) active = false;
@@ -2086,12 +2097,27 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
   {
     if (s0 > 0) {   // queued last substep: wait for the pair's first chunk to hand the state over
       int* flag = ka->b.qsync + QS_FLAG + pair;
-      int seen = s0;
+      int seen = 0;
       if (lane == 0) {   // bounded (~0.5 s): a broken hand-off must not hang the GPU
+        const bool force = pair + 1 == ka->p.dbg_lose_pair1;   // test hook: treat this pair's hand-off as lost
         int w = 0;
-        while ((seen = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != s0 && ++w < (1 << 22))
-          __builtin_amdgcn_s_sleep(2);
-        __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
+        if (!force)
+          while ((seen = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != s0 && ++w < (1 << 22))
+            __builtin_amdgcn_s_sleep(2);
+        if (seen == s0) {
+          __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // consumed: clean for the next launch
+        } else {
+          // Timed out (or forced): mark the pair abandoned (-1) so that a producer arriving late
+          // cleans the flag up itself instead of leaving a stale s0 that the next launch's
+          // consumer would match.  If the producer stored s0 in the meantime, the CAS fails:
+          // consume the flag here (and use the row, unless forced).
+          int expect = 0;
+          if (!__hip_atomic_compare_exchange_strong(flag, &expect, -1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT)) {
+            __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (!force) seen = expect;
+          }
+        }
       }
       const bool lost = __builtin_amdgcn_readfirstlane(seen) != s0;
       WSYNC();   // (compiler order: the row loads stay behind the poll)
@@ -2175,7 +2201,12 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
         }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the row is in memory before the flag is
-      if (lane == 0) __hip_atomic_store(k->b.qsync + QS_FLAG + pair, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) {
+        int* flag = k->b.qsync + QS_FLAG + pair;
+        // -1: the consumer timed out and poisoned the env; leave the flag clean for the next launch
+        if (__hip_atomic_exchange(flag, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == -1)
+          __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       HS_FLUSH();
       break;
     }
@@ -2203,12 +2234,14 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
             k->b.terminated[env] = term;
             k->b.truncated[env] = trunc;
           }
+          // the final step's info of a finished episode (SubprocVecEnv returns its step_count /
+          // total_reward before resetting, custom_env.py:216-224), with or without auto-reset
+          if ((term || trunc) && active && sl == 0) {
+            if (k->b.term_step_count) k->b.term_step_count[env] = step_count;
+            if (k->b.term_total_reward) k->b.term_total_reward[env] = total;
+          }
           if ((term || trunc) && k->p.autoreset && active) {
             write_obs(st.m, s, sl, st.qfa, k->b.terminal_obs + (size_t)env * obs_dim, obs_dim);
-            // the final step's info (SubprocVecEnv returns the finished episode's step_count /
-            // total_reward before resetting, custom_env.py:216-224)
-            if (sl == 0 && k->b.term_step_count) k->b.term_step_count[env] = step_count;
-            if (sl == 0 && k->b.term_total_reward) k->b.term_total_reward[env] = total;
             do_reset = true;
           }
         }
@@ -2278,8 +2311,12 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !PGS) ? 2 : 1) void step_ker
     pcache = &pgs_smem[threadIdx.x >= HL ? 1 : 0];
   }
   const KPtr<T> ka = (KPtr<T>)__builtin_amdgcn_kernarg_segment_ptr();
-  step_pair<T, NV, PGS, Resident<T>>(ka, smem, pcache, 2 * blockIdx.x + (threadIdx.x >= HL ? 1 : 0), ka->nenv, nullptr,
-                                     0, ka->p.nsub, blockIdx.x);
+  const bool up = threadIdx.x >= HL;
+  // single-env schedule (small batches, p.single): env blockIdx.x on the lower half, its mirror on
+  // the upper half (same data, so the same control flow), one env per wave
+  const bool single = ka->p.single != 0;
+  step_pair<T, NV, PGS, Resident<T>>(ka, smem, pcache, single ? (int)blockIdx.x : 2 * blockIdx.x + (up ? 1 : 0),
+                                     ka->nenv, nullptr, 0, ka->p.nsub, blockIdx.x, single && up);
 }
 
 // Resident tier, chunk-queue schedule (launch_step picks it when the env pairs outnumber the waves
@@ -2417,7 +2454,12 @@ hipError_t launch_step(const DevModel<T>* dmodel, int nv, const EnvBuffers<T>& b
     while (gcd(q, (uint32_t)npairs) != 1u) q += 2;
     args.p.qmul = (int)(q % (uint32_t)npairs == 0 ? 1 : q);
   }
-  const dim3 grid(args.p.queue ? resident : npairs), block(WAVE);
+  // single-env schedule: one wave per env (the upper half-wave a ghost of the lower) when every
+  // env gets a resident wave of its own -- small batches (configs[4]'s 1024 envs per GPU) would
+  // otherwise leave SIMDs idle with one wave per env pair
+  args.p.single = (!args.p.queue && (p.schedule == SCHED_SINGLE ||
+                                     (p.schedule == 0 && resident > 0 && nenv <= resident))) ? 1 : 0;
+  const dim3 grid(args.p.queue ? resident : (args.p.single ? nenv : npairs)), block(WAVE);
   // the wide tier's grid: enough waves for a few deferred envs at once, few enough that the
   // common no-overflow launch (every wave reads the count and exits) costs a few microseconds
   const dim3 wgrid(std::min((nenv + 1) / 2, 32));

@@ -9,8 +9,11 @@ trainer, train_sb3.py:208-231) so rollouts never leave HBM.
 * GAE(gamma, lambda) reverse scan; per-minibatch advantage normalisation; clipped surrogate,
   value MSE (vf_coef 0.5), entropy bonus, clip_grad_norm(max_grad_norm 0.5), Adam(eps 1e-5).
 * Multi-GPU: envs are sharded per rank; each optimizer step all-reduces the flattened gradient
-  bucket ONCE (RCCL over xGMI, ~1.27 MB at [256,256]) and averages it -- no other collective on
-  the data path.
+  bucket ONCE (RCCL over xGMI, ~1.27 MB at [256,256]) -- no other collective on the data path
+  (SURVEY.md 8e).  Ranks stay in lockstep for ANY shard sizes (train_sb3.py:203 accepts any
+  n_envs): at construction the ranks agree once on every rank's env count, so all of them run the
+  same number of rollout timesteps, minibatches per epoch and all-reduces; each rank's gradient is
+  weighted by its share of the rollout samples before the sum.
 """
 from __future__ import annotations
 
@@ -203,12 +206,18 @@ class PPO:
 
     def __init__(self, env, learning_rate=3e-4, n_steps=2048, batch_size=64, n_epochs=10, gamma=0.99,
                  gae_lambda=0.95, clip_range=0.2, ent_coef=0.0, vf_coef=0.5, max_grad_norm=0.5,
-                 policy_kwargs=None, seed=0, world_size=None, rank=None):
+                 policy_kwargs=None, seed=0, world_size=None, rank=None, sync_grads=None):
         import torch.distributed as dist
         if world_size is None:
             world_size = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
         if rank is None:
             rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+        # sync_grads: all-reduce the gradient bucket every optimizer step (default: world > 1; True
+        # with a world-1 group runs the collective anyway -- the RCCL smoke test of tests/)
+        self.sync_grads = world_size > 1 if sync_grads is None else bool(sync_grads)
+        if self.sync_grads and not (dist.is_available() and dist.is_initialized()):
+            raise RuntimeError("PPO: gradient sync needs an initialised torch.distributed process group "
+                               f"(world_size={world_size}); see train.init_distributed")
         pk = dict(policy_kwargs or {})
         net = pk.get("net_arch", {"pi": [64, 64], "vf": [64, 64]})
         if isinstance(net, (list, tuple)):
@@ -236,6 +245,7 @@ class PPO:
         self.ent_coef, self.vf_coef, self.max_grad_norm = ent_coef, vf_coef, max_grad_norm
         self.world_size, self.rank = world_size, rank
         N, T, D, A = env.num_envs, n_steps, env.obs_dim, env.act_dim
+        self._plan_minibatches(N)
         f, dev = torch.float32, self.device
         self.buf = dict(obs=torch.zeros(T, N, D, dtype=f, device=dev), act=torch.zeros(T, N, A, dtype=f, device=dev),
                         rew=torch.zeros(T, N, dtype=f, device=dev), start=torch.zeros(T, N, dtype=f, device=dev),
@@ -285,7 +295,7 @@ class PPO:
         boot = b["boot"].view(-1).nonzero().squeeze(1)
         if boot.numel():                                        # deferred TimeLimit bootstrap
             b["rew"].view(-1)[boot] += self.gamma * pol.value(b["tobs"].view(T * N, -1)[boot])
-        self.num_timesteps += T * N * self.world_size
+        self.num_timesteps += T * self.n_envs_global
         last_v = pol.value(self.obs)
         return gae(b["rew"], b["val"], b["start"], last_v, self.episode_start, self.gamma, self.gae_lambda)
 
@@ -361,9 +371,62 @@ class PPO:
             self.obs = obs.float().clone()
             self.episode_start = done.float()
         self.ep_returns += b["epret"][b["done"]].tolist()      # one device -> host transfer per rollout
-        self.num_timesteps += self.n_steps * env.num_envs * self.world_size
+        self.num_timesteps += self.n_steps * self.n_envs_global
         last_v = pol.value(self.obs)
         return gae(b["rew"], b["val"], b["start"], last_v, self.episode_start, self.gamma, self.gae_lambda)
+
+    # -- multi-rank lockstep ---------------------------------------------------------------------
+    def _comm_device(self):
+        import torch.distributed as dist
+        return self.device if dist.get_backend() == "nccl" else torch.device("cpu")
+
+    def _plan_minibatches(self, n_local):
+        """Agree (one all-reduce at construction) on every rank's env count, then fix the per-epoch
+        minibatch plan so that every rank issues the same number of gradient all-reduces:
+
+        * world 1: SB3's plan -- ceil(M / batch_size) minibatches of batch_size, the last one short;
+        * world > 1: n_mb = max over ranks of ceil(M_r / batch_size) minibatches per epoch on EVERY
+          rank, each rank splitting its own permutation of M_r = n_steps * N_r samples into n_mb
+          near-equal chunks (sizes differ by at most one; equal to batch_size for even shards whose
+          M_r is a multiple of it, i.e. the usual case).  Gradients are weighted by the rank's share
+          M_r / M_total before the sum, so uneven shards count per sample.
+        """
+        world, T, bs = self.world_size, self.n_steps, self.batch_size
+        if world > 1 or self.sync_grads:
+            import torch.distributed as dist
+            counts = torch.zeros(world, dtype=torch.int64, device=self._comm_device())
+            counts[self.rank] = n_local
+            dist.all_reduce(counts)
+            counts = [int(c) for c in counts.cpu()]
+            if counts[self.rank] != n_local or min(counts) <= 0:
+                raise RuntimeError(f"PPO: inconsistent env counts across ranks: {counts}")
+        else:
+            counts = [n_local]
+        self.env_counts = counts
+        self.n_envs_global = sum(counts)
+        M = T * n_local
+        if world == 1:
+            self.n_minibatches = -(-M // bs)
+            self._mb_bounds = [min(s, M) for s in range(0, M + bs, bs)][: self.n_minibatches + 1]
+            self._mb_bounds[-1] = M
+        else:
+            self.n_minibatches = max(-(-(T * c) // bs) for c in counts)
+            if T * min(counts) < self.n_minibatches:
+                raise ValueError(f"batch_size={bs} is too small for env shards {counts} x n_steps={T}: "
+                                 "a rank would get an empty minibatch")
+            self._mb_bounds = [(j * M) // self.n_minibatches for j in range(self.n_minibatches + 1)]
+        sizes = {b - a for a, b in zip(self._mb_bounds, self._mb_bounds[1:])}
+        self._chunk = sizes.pop() if len(sizes) == 1 else None     # uniform minibatch size (graphable)
+        self.grad_weight = (T * n_local) / (T * self.n_envs_global) if self.sync_grads else 1.0
+
+    def _agree_stop(self, stop):
+        """Every rank leaves learn() at the same iteration (a callback may stop one rank only)."""
+        if self.world_size == 1:
+            return stop
+        import torch.distributed as dist
+        f = torch.tensor([1 if stop else 0], dtype=torch.int32, device=self._comm_device())
+        dist.all_reduce(f, op=dist.ReduceOp.MAX)
+        return bool(f.item())
 
     def _allreduce_flat(self, flat):
         import torch.distributed as dist
@@ -375,12 +438,12 @@ class PPO:
             dist.all_reduce(flat)        # ONE RCCL all-reduce per optimizer step (xGMI ring)
 
     def _allreduce_grads(self):
-        if self.world_size == 1:
+        if not self.sync_grads:
             return
         grads = [p.grad for p in self.flat]
         flat = torch.cat([g.reshape(-1) for g in grads])
+        flat.mul_(self.grad_weight)      # this rank's share of the samples (1/world for even shards)
         self._allreduce_flat(flat)
-        flat /= self.world_size
         o = 0
         for g in grads:
             n = g.numel()
@@ -410,7 +473,7 @@ class PPO:
         b = self.buf
         T, N = self.n_steps, self.env.num_envs
         M = T * N
-        if self.device.type == "cuda" and self.graphs and M % self.batch_size == 0:
+        if self.device.type == "cuda" and self.graphs and self._chunk is not None:
             return self._train_graphed(adv, ret)
         obs = b["obs"].reshape(M, -1)
         act = b["act"].reshape(M, -1)
@@ -419,8 +482,8 @@ class PPO:
         stats = []
         for epoch in range(self.n_epochs):
             perm = torch.randperm(M, device=self.device)
-            for s in range(0, M, self.batch_size):
-                loss, pg, vf = self._minibatch_loss(obs, act, old_logp, adv, ret, perm[s:s + self.batch_size])
+            for s, e in zip(self._mb_bounds, self._mb_bounds[1:]):
+                loss, pg, vf = self._minibatch_loss(obs, act, old_logp, adv, ret, perm[s:e])
                 self.opt.zero_grad(set_to_none=True)
                 loss.backward()
                 self._allreduce_grads()
@@ -448,7 +511,7 @@ class PPO:
         bucket (world > 1) is the one eager call between the two replays.  The warm-up steps
         capture needs are undone (parameters and Adam state restored in place), so graphed
         training takes exactly the eager path's optimizer steps."""
-        b, M, bs = self.buf, self.n_steps * self.env.num_envs, self.batch_size
+        b, M, bs = self.buf, self.n_steps * self.env.num_envs, self._chunk
         dev = self.device
         self._g_idx = torch.zeros(bs, dtype=torch.long, device=dev)
         self._g_adv = torch.zeros(M, dtype=torch.float32, device=dev)
@@ -457,22 +520,23 @@ class PPO:
         src = (b["obs"].view(M, -1), b["act"].view(M, -1), b["logp"].view(-1), self._g_adv, self._g_ret)
         params = list(self.policy.parameters())
 
-        world = self.world_size
-        self._g_flat = torch.zeros(sum(p.numel() for p in params), dtype=torch.float32, device=dev) if world > 1 else None
+        sync, w = self.sync_grads, float(self.grad_weight)
+        self._g_flat = torch.zeros(sum(p.numel() for p in params), dtype=torch.float32, device=dev) if sync else None
 
         def g1_body():
             loss, pg, vf = self._minibatch_loss(*src, self._g_idx)
             loss.backward()
             self._g_stats.add_(torch.stack([pg.detach(), vf.detach()]))
-            if world > 1:                # the gradient bucket the eager all-reduce sends
+            if sync:                     # the weighted gradient bucket the eager all-reduce sends
                 torch.cat([p.grad.reshape(-1) for p in params], out=self._g_flat)
+                self._g_flat.mul_(w)
 
         def g2_body():
-            if world > 1:                # averaged bucket back into the .grad tensors
+            if sync:                     # summed bucket back into the .grad tensors
                 o = 0
                 for p in params:
                     n = p.numel()
-                    p.grad.copy_(self._g_flat[o:o + n].view_as(p.grad)).mul_(1.0 / world)
+                    p.grad.copy_(self._g_flat[o:o + n].view_as(p.grad))
                     o += n
             self._clip_and_step()
 
@@ -521,17 +585,17 @@ class PPO:
             if self._graphs is None:
                 return self.train(adv, ret)       # capture failed: self.graphs is now False
         g1, g2 = self._graphs
-        M, bs = self.n_steps * self.env.num_envs, self.batch_size
+        M = self.n_steps * self.env.num_envs
         self._g_adv.copy_(adv.reshape(-1))
         self._g_ret.copy_(ret.reshape(-1))
         self._g_stats.zero_()
         n = 0
         for epoch in range(self.n_epochs):
             perm = torch.randperm(M, device=self.device)
-            for s in range(0, M, bs):
-                self._g_idx.copy_(perm[s:s + bs])
+            for s, e in zip(self._mb_bounds, self._mb_bounds[1:]):
+                self._g_idx.copy_(perm[s:e])
                 g1.replay()
-                if self.world_size > 1:
+                if self.sync_grads:
                     self._allreduce_flat(self._g_flat)
                 g2.replay()
                 n += 1
@@ -550,7 +614,7 @@ class PPO:
             mean_ret = float(np.mean(self.ep_returns[-100:])) if self.ep_returns else float("nan")
             self.logger = dict(iteration=it, timesteps=self.num_timesteps, rollout_s=t1 - t0, train_s=t2 - t1,
                                ep_rew_mean=mean_ret, **st)
-            if callback is not None and callback(self) is False:
+            if self._agree_stop(callback is not None and callback(self) is False):
                 break
         return self
 
@@ -570,7 +634,7 @@ class PPO:
                 "gamma": self.gamma, "gae_lambda": self.gae_lambda, "clip_range": self.clip_range,
                 "ent_coef": self.ent_coef, "vf_coef": self.vf_coef, "max_grad_norm": self.max_grad_norm,
                 "learning_rate": self.learning_rate, "num_timesteps": self.num_timesteps,
-                "n_envs": self.env.num_envs * self.world_size,
+                "n_envs": self.n_envs_global,
                 "policy_kwargs": {"net_arch": self.net_arch,
                                   "activation_fn": act if isinstance(act, str) else act.__name__}}
 

@@ -115,8 +115,10 @@ class HumanoidVecEnv(_Base):
     @property
     def graph_safe(self):
         """step_tensors is launches only (device reward, one stream, no host sync), so a trainer
-        may capture it in a HIP graph."""
-        return self._host_reward is None and getattr(self.batch, "_streams", None) is None
+        may capture it in a HIP graph.  Not while SB3-seeded host reset-noise streams are active
+        (or pending from ``seed()``): step_tensors then reads the done flags back every step."""
+        return (self._host_reward is None and getattr(self.batch, "_streams", None) is None
+                and self._streams is None and self._seeds is None)
 
     @property
     def terminal_obs(self):

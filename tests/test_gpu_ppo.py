@@ -273,8 +273,62 @@ def test_graphed_update_world2_allreduce(tmp_path):
     assert torch.equal(r[0]["graphed"], r[1]["graphed"]), "ranks diverged in the graphed update"
     assert torch.allclose(r[0]["graphed"], r[0]["eager"], rtol=1e-4, atol=1e-6)
     n = r[0]["graphed"].numel()
-    # 2 epochs x (8 x 256 / 1024) minibatches, graphed + eager: 8 buckets of n
-    assert r[0]["calls"] == [n] * 8
+    # 2 epochs x (8 x 256 / 1024) minibatches, graphed + eager: 8 buckets of n (plus the env-count
+    # agreement of each PPO's construction)
+    assert [c for c in r[0]["calls"] if c == n] == [n] * 8
+    assert r[0]["calls"] == r[1]["calls"]
+
+
+def test_rccl_world1_bucket_allreduce_between_graph_replays():
+    """RCCL really executes: a world-1 ``nccl`` process group (RCCL on ROCm) with the gradient
+    sync forced on runs the graphed update's bucket all-reduce as an eager device collective
+    between the G1 and G2 replays of every optimizer step.  With one rank the all-reduce is the
+    identity, so the weights must equal those of the same update without the collective."""
+    import socket
+    import torch.distributed as dist
+    from mujocoposelearning_amd.model import HsModel
+    from mujocoposelearning_amd.ppo import PPO
+    from mujocoposelearning_amd.vec_env import HumanoidVecEnv
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    calls = []
+    real = dist.all_reduce
+
+    def counting(t, *a, **k):
+        calls.append((t.numel(), t.device.type))
+        return real(t, *a, **k)
+    dist.all_reduce = counting
+    try:
+        assert dist.get_backend() == "nccl"
+        env = HumanoidVecEnv({"model_path": XML, "duration": 10.0, "reward_config": {"type": "stand"},
+                              "frame_skip": 3}, n_envs=256, model=HsModel(XML), seed=3)
+        kw = dict(n_steps=8, batch_size=1024, n_epochs=2, seed=0,
+                  policy_kwargs={"activation_fn": "ReLU", "net_arch": {"pi": [64, 64], "vf": [64, 64]}})
+        pa, pb = PPO(env, sync_grads=True, **kw), PPO(env, **kw)
+        assert pa.sync_grads and not pb.sync_grads and pa.grad_weight == 1.0
+        adv, ret = pa.collect_rollouts()
+        for k in pa.buf:
+            pb.buf[k].copy_(pa.buf[k])
+        for p in (pa, pb):
+            for it in range(2):                 # the second call replays the captured graphs
+                torch.manual_seed(11 + it)
+                p.train(adv, ret)
+        torch.cuda.synchronize()
+        assert pa._graphs is not None and pb._graphs is not None
+        n = sum(q.numel() for q in pa.policy.parameters())
+        buckets = [c for c in calls if c[0] == n]
+        # 2 train calls x 2 epochs x (8 x 256 / 1024) minibatches, every bucket on the device
+        assert buckets == [(n, "cuda")] * 8, calls
+        for x, y in zip(pa.policy.parameters(), pb.policy.parameters()):
+            assert torch.allclose(x, y, rtol=1e-5, atol=1e-7), float((x - y).abs().max())
+        env.close()
+    finally:
+        dist.all_reduce = real
+        dist.destroy_process_group()
 
 
 def test_device_rollout_deferred_timelimit_bootstrap():

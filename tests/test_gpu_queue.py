@@ -1,0 +1,177 @@
+"""The fp64 chunk-queue schedule at configs[1] size (4096 envs = 2048 env pairs > 1024 resident
+waves; hs_kernels.hip step_kernel_queue) on its two rare paths:
+
+* contact overflow inside the queue: an env whose contacts / rows overflow the resident tier in a
+  queued first chunk carries the overflow count through the hand-off row; its last-substep item
+  defers it to the wide tier, which re-runs the whole env step from the untouched inputs;
+* a lost hand-off: a last-substep item whose bounded wait times out poisons its env pair
+  (qpos[2] = NaN), so mj_checkPos resets them -- MuJoCo's warning + mj_resetData path of mj_step
+  (custom_env.py:160) -- and the pair's flag is left clean for the next launch.  The wait never
+  times out in practice; the hs_debug_lose_handoff test hook forces it.
+"""
+import numpy as np
+import pytest
+
+from conftest import XML
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def model():
+    from mujocoposelearning_amd.model import HsModel
+    return HsModel(XML)
+
+
+def _batch(model, n, seed=3):
+    from mujocoposelearning_amd.batch import HsBatch
+    b = HsBatch(model, n, precision="fp64", seed=seed)
+    b.configure(frame_skip=3, duration=10.0, reward_id=0, autoreset=1, max_steps=750)
+    return b
+
+
+def _copy_state(src, dst):
+    st = src.get_state()
+    dst.set_state(**st)
+    for k in ("step_count", "episode", "total_reward", "warning"):
+        getattr(dst, k).copy_(getattr(src, k))
+
+
+def test_queue_with_wide_tier_reruns_bitwise_equals_direct(model):
+    """4096 fp64 envs on the queue, 16 of them lying pressed into the floor (over the resident
+    tier's 32 contacts / 128 rows) among freshly reset ones: schedule 'auto' (queue) and 'direct'
+    give bitwise the same states and outputs, and both re-run exactly the overflowing envs."""
+    import torch
+    from oracle.oracle import Oracle
+    from test_gpu_contacts import lying_states
+    n = 4096
+    o = Oracle(XML)
+    lying = np.stack(lying_states(o, 16, seed=11))
+    idx = np.arange(16) * 255 + 7                      # spread over the batch (pairs and halves)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    acts = torch.rand(4, n, 21, device="cuda", generator=g) * 2 - 1
+    outs, reruns = [], []
+    for sched in ("auto", "direct"):
+        b = _batch(model, n)
+        b.configure(schedule=sched)
+        b.reset()
+        st = b.get_state()
+        st["qpos"][idx] = lying
+        st["qvel"][idx] = 0.0
+        st["qacc_warmstart"][idx] = 0.0
+        b.set_state(**st)
+        assert b.queued() == (sched == "auto")
+        b.step(acts[0])
+        r = [b.wide_reruns()]
+        tr = [b.obs.clone(), b.reward.clone(), b.qpos.clone()]
+        for k in range(1, 4):
+            b.step(acts[k])
+        r.append(b.wide_reruns())
+        tr += [b.qpos.clone(), b.qvel.clone(), b.qacc_warmstart.clone(), b.time.clone(), b.obs.clone(),
+               b.reward.clone(), b.warning.clone(), b.aux.clone()]
+        outs.append(tr)
+        reruns.append(r)
+        b.close()
+    assert reruns[0] == reruns[1], reruns
+    assert reruns[0][0] == len(idx)                    # exactly the overflowing envs, in the first step
+    assert int(outs[0][-2][:, 3].sum()) == 0           # nothing dropped (re-run, not truncated)
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
+
+
+def test_forced_lost_handoff_resets_the_pair_and_leaves_the_queue_clean(model):
+    import torch
+    n, k = 4096, 1234
+    pair = [k - k % 2, k - k % 2 + 1]
+    others = np.setdiff1d(np.arange(n), pair)
+    g = torch.Generator(device="cuda").manual_seed(8)
+    acts = torch.rand(4, n, 21, device="cuda", generator=g) * 2 - 1
+    a, ref = _batch(model, n), _batch(model, n)
+    for b in (a, ref):
+        b.reset()
+        b.step(acts[0])
+        b.step(acts[1])
+    assert a.queued() and torch.equal(a.qpos, ref.qpos)
+    a.debug_lose_handoff(k)
+    a.step(acts[2])
+    ref.step(acts[2])
+    a.debug_lose_handoff(None)
+    torch.cuda.synchronize()
+    # every other env is bitwise what the undisturbed run computed
+    for name in ("qpos", "qvel", "qacc_warmstart", "time", "obs", "reward", "warning", "step_count"):
+        x, y = getattr(a, name), getattr(ref, name)
+        assert torch.equal(x[others], y[others]), name
+    # the pair: mj_checkPos -> HS_WARN_BADQPOS += 1 and mj_resetData (qpos0, qvel 0, ctrl 0, time 0),
+    # then the last substep from there: == one raw mj_step from the reset state with ctrl 0
+    w = a.warning.cpu().numpy()
+    assert (w[pair, 0] == 1).all() and w[pair, 1:].sum() == 0 and w[others].sum() == 0
+    c = _batch(model, 2)
+    c.set_state(qpos=np.tile(model.qpos0, (2, 1)), qvel=0.0, qacc_warmstart=0.0, time=0.0, ctrl=0.0)
+    c.physics_step(torch.zeros(2, 21, device=c.device), 1)
+    for name in ("qpos", "qvel", "qacc_warmstart", "time"):
+        assert torch.equal(getattr(a, name)[pair], getattr(c, name)), name
+    assert np.allclose(a.time[pair].cpu().numpy(), 0.005)
+    assert torch.isfinite(a.obs[pair]).all()
+    # the next launch is clean: no stale flag makes the pair's last substep read an old hand-off row.
+    # Replaying A's state on the direct schedule gives bitwise A's queued result, and no warning.
+    d = _batch(model, n)
+    d.configure(schedule="direct")
+    _copy_state(a, d)
+    a.step(acts[3])
+    d.step(acts[3])
+    for name in ("qpos", "qvel", "qacc_warmstart", "time", "obs", "reward", "warning"):
+        assert torch.equal(getattr(a, name), getattr(d, name)), name
+    assert int(a.warning[:, 0].sum()) == 2
+
+
+def test_physics_step_refuses_stale_ctrl(model):
+    """hs_physics_step(ctrl=NULL) keeps data.ctrl; after env steps that skipped the ctrl copy
+    (HS_OUT_CTRL off, the trainer's setting) that buffer is stale, so the call fails loudly."""
+    import torch
+    from mujocoposelearning_amd._lib import HsimError
+    b = _batch(model, 4)
+    b.reset()
+    b.physics_step(None, 1)                              # fresh reset: ctrl is 0, valid
+    b.configure(ctrl=False)
+    b.step(torch.zeros(4, 21, device=b.device))
+    with pytest.raises(HsimError, match="stale"):
+        b.physics_step(None, 1)
+    assert "ctrl" not in b.get_state()
+    b.configure(ctrl=True)
+    b.set_state(ctrl=0.5)                                # rewriting ctrl makes it valid again
+    b.physics_step(None, 1)
+    assert np.allclose(b.get_state()["ctrl"], 0.5)
+
+
+@pytest.mark.parametrize("prec", ["fp64", "fp32"])
+def test_single_env_schedule_bitwise_equals_paired(model, prec):
+    """Small batches (BASELINE.json configs[4]: full-state obs, 1024 envs per GPU) run one env per
+    wave with the upper half-wave as a ghost ("single", HS_SCHED_AUTO when every env fits the
+    resident waves).  It must give bitwise the states and outputs of one wave per env pair --
+    through falls, contacts and staggered auto-resets -- at 1024 envs and at an odd count."""
+    import torch
+    from mujocoposelearning_amd.batch import HsBatch
+    for n in (1024, 777):
+        g = torch.Generator(device="cuda").manual_seed(6)
+        acts = torch.rand(30, n, 21, device="cuda", generator=g) * 2 - 1
+        t0 = np.floor(np.arange(n) * 667 / n) * 0.015 + 0.005
+        outs = []
+        for sched in ("auto", "direct"):
+            b = HsBatch(model, n, precision=prec, seed=3, full_state=True)
+            b.configure(frame_skip=3, duration=10.0, reward_id=1, autoreset=1, max_steps=750, schedule=sched)
+            assert b.schedule_name() == ("single" if sched == "auto" else "paired"), (n, b.resident_waves)
+            b.reset()
+            b.set_state(time=t0)
+            tr = []
+            for k in range(30):
+                b.step(acts[k])
+                if k % 10 == 9:
+                    tr += [b.obs.clone(), b.reward.clone(), b.terminated.clone(), b.truncated.clone()]
+            tr += [b.qpos.clone(), b.qvel.clone(), b.qacc_warmstart.clone(), b.time.clone(), b.warning.clone(),
+                   b.terminal_obs.clone(), b.terminal_step_count.clone(), b.terminal_total_reward.clone(),
+                   b.episode.clone(), b.aux.clone(), b.cfrc_ext.clone(), b.subtree_linvel.clone()]
+            outs.append(tr)
+            b.close()
+        assert int(outs[0][-4].max()) >= 2                  # auto-resets happened
+        for x, y in zip(*outs):
+            assert torch.equal(x, y)

@@ -142,10 +142,14 @@ def _free_port():
     return port
 
 
-def _dist_worker(rank, world, port, out_dir):
+def _dist_worker(rank, world, port, out_dir, n_envs=None, stop_rank=None):
+    """One rank of a gloo world: a ToyEnv holding this rank's shard of ``n_envs`` envs (8 per
+    rank when None).  ``stop_rank``: that rank's callback alone asks to stop after iteration 1."""
     import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mujocoposelearning_amd.train import init_distributed
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), LOCAL_RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    assert init_distributed("gloo") == (world, rank, rank)
     calls = []
     real = dist.all_reduce
 
@@ -154,29 +158,103 @@ def _dist_worker(rank, world, port, out_dir):
         return real(t, *a, **k)
     dist.all_reduce = counting
     try:
-        env = ToyEnv(n=8, seed=100 + rank)            # different data per rank (env shard)
+        lo, hi = shard_envs(n_envs, world, rank) if n_envs else (8 * rank, 8 * rank + 8)
+        env = ToyEnv(n=hi - lo, seed=100 + rank)            # different data per rank (env shard)
         model = PPO(env, n_steps=8, batch_size=16, n_epochs=2,
                     policy_kwargs={"net_arch": {"pi": [16, 16], "vf": [16, 16]}})
         assert model.world_size == world and model.rank == rank
-        model.learn(total_timesteps=8 * 8 * world * 2)
+        total = n_envs or 8 * world
+        cb = (lambda m: not (rank == stop_rank and m.logger["iteration"] == 1)) if stop_rank is not None else None
+        model.learn(total_timesteps=8 * total * 2, callback=cb)
         flat = torch.cat([p.detach().reshape(-1) for p in model.policy.parameters()])
-        torch.save({"flat": flat, "calls": calls, "steps": model.num_timesteps}, os.path.join(out_dir, f"r{rank}.pt"))
+        torch.save({"flat": flat, "calls": calls, "steps": model.num_timesteps, "n_mb": model.n_minibatches,
+                    "bounds": model._mb_bounds, "w": model.grad_weight},
+                   os.path.join(out_dir, f"r{rank}.pt"))
     finally:
         dist.all_reduce = real
         dist.destroy_process_group()
 
 
+def _run_world(tmp_path, world, **kw):
+    port = _free_port()
+    mp.start_processes(_dist_worker, args=(world, port, str(tmp_path), kw.get("n_envs"), kw.get("stop_rank")),
+                       nprocs=world, join=True, start_method="spawn")
+    return [torch.load(tmp_path / f"r{i}.pt", weights_only=True) for i in range(world)]
+
+
 def test_gloo_world2_one_allreduce_per_step_identical_weights(tmp_path):
-    world, port = 2, _free_port()
-    mp.start_processes(_dist_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True,
-                       start_method="spawn")
-    r = [torch.load(tmp_path / f"r{i}.pt", weights_only=True) for i in range(world)]
+    world = 2
+    r = _run_world(tmp_path, world)
     assert torch.equal(r[0]["flat"], r[1]["flat"]), "ranks diverged: gradient all-reduce missing"
     n_params = r[0]["flat"].numel()
     # 2 iterations x 2 epochs x (64 samples / 16 per minibatch) = 16 optimizer steps, one bucket each
     for x in r:
-        assert x["calls"] == [n_params] * 16
+        assert [c for c in x["calls"] if c == n_params] == [n_params] * 16
         assert x["steps"] == 8 * 8 * world * 2
+        assert x["w"] == 0.5
+
+
+def test_gloo_world3_uneven_shards_stay_in_lockstep(tmp_path):
+    """n_envs=10 over 3 ranks (shards 4/3/3, train_sb3.py:203 accepts any n_envs): every rank runs
+    the same number of minibatches and all-reduces, the global timestep count, and ends with the
+    same weights; gradients are weighted by the rank's sample share."""
+    world = 3
+    r = _run_world(tmp_path, world, n_envs=10)
+    n_params = r[0]["flat"].numel()
+    for x in r[1:]:
+        assert torch.equal(r[0]["flat"], x["flat"]), "ranks diverged"
+        assert x["calls"] == r[0]["calls"], "ranks issued different collectives (an RCCL hang)"
+    for i, x in enumerate(r):
+        assert x["steps"] == 8 * 10 * 2                    # global env count, not world x local
+        assert x["n_mb"] == 2                              # max over ranks of ceil(8 * N_r / 16)
+        m = 8 * (4 if i == 0 else 3)
+        assert x["bounds"] == [0, m // 2, m]
+        assert abs(x["w"] - m / 80) < 1e-15
+        # 2 iterations x 2 epochs x 2 minibatches
+        assert [c for c in x["calls"] if c == n_params] == [n_params] * 8
+    assert abs(sum(x["w"] for x in r) - 1.0) < 1e-12
+
+
+def test_gloo_world2_callback_stop_on_one_rank_stops_all(tmp_path):
+    r = _run_world(tmp_path, 2, stop_rank=1)
+    assert r[0]["steps"] == r[1]["steps"] == 8 * 16          # both left after iteration 1
+    assert r[0]["calls"] == r[1]["calls"]
+
+
+def test_init_distributed_without_launcher_and_without_gpu(monkeypatch):
+    from mujocoposelearning_amd.train import init_distributed
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    assert init_distributed() == (1, 0, 0)
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("RANK", "0")
+    if not torch.cuda.is_available():
+        with pytest.raises(RuntimeError, match="no GPU"):
+            init_distributed()
+
+
+def test_ppo_sync_without_group_raises():
+    with pytest.raises(RuntimeError, match="process group"):
+        PPO(ToyEnv(n=4), n_steps=4, batch_size=8, world_size=2, rank=0)
+
+
+def test_minibatch_plan_world1_is_sb3():
+    m = PPO(ToyEnv(n=5), n_steps=4, batch_size=8)           # M = 20: 8, 8, 4 (SB3's short last batch)
+    assert m._mb_bounds == [0, 8, 16, 20] and m._chunk is None and m.n_envs_global == 5
+    m = PPO(ToyEnv(n=4), n_steps=4, batch_size=8)
+    assert m._mb_bounds == [0, 8, 16] and m._chunk == 8
+
+
+def test_train_module_cli_loads_reference_style_config(tmp_path):
+    from mujocoposelearning_amd.train import load_config_from_file
+    p = tmp_path / "config.py"
+    p.write_text('config = {"env_kwargs": {"n_envs": 8, "reward_function": "stand"}, '
+                 '"ppo_kwargs": {"policy_kwargs": {"activation_fn": "ReLU"}}}\n')
+    cfg = load_config_from_file(str(p))
+    assert cfg["env_kwargs"]["n_envs"] == 8
+    bad = tmp_path / "bad.py"
+    bad.write_text("x = 1\n")
+    with pytest.raises(ValueError):
+        load_config_from_file(str(bad))
 
 
 SB3_MLP_KEYS = {   # ActorCriticPolicy state_dict of MlpPolicy, net_arch=dict(pi=[256,256], vf=[256,256])
