@@ -6,6 +6,7 @@
  *
  *   hs_model_load        <- mujoco.MjModel.from_xml_path(model_path)      custom_env.py:53
  *   hs_model_field       <- MjModel attribute reads (nq, nv, nu, body_mass, ...) custom_env.py:87,59-61
+ *                           (+ "contact_bound": the 4 static worst-case counts of hs_batch_info)
  *   hs_batch_create      <- mujoco.MjData(model) per env                  custom_env.py:54
  *                           x SubprocVecEnv([make_env(...)] * n_envs)     train_sb3.py:203
  *   hs_set_seed          <- VecEnv.seed / np.random.seed(seed) of reset (custom_env.py:99-100)
@@ -129,6 +130,11 @@ typedef struct {
   /* waves of the resident step kernel the device holds at once (2 envs per wave); with more env
    * pairs than this, HS_SCHED_AUTO runs multi-substep calls on the chunk-queue schedule */
   int resident_waves;
+  /* static worst case of one env from the model's collision pair list (most contacts per pair
+   * type x rows per contact, + one row per limited joint / tendon): every pair touching at once
+   * (geometric, unreachable) and every geom on the floor at once (a flat-lying body).  Models
+   * whose floor bound exceeds the wide tier are rejected by hs_batch_create. */
+  int bound_con_all, bound_efc_all, bound_con_floor, bound_efc_floor;
 } hs_batch_info;
 
 hs_model* hs_model_load(const char* xml_path, char* err, int errsz);

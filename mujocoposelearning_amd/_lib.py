@@ -38,7 +38,8 @@ class hs_buffers(C.Structure):
 
 class hs_batch_info(C.Structure):
     _fields_ = [(n, C.c_int) for n in ("n_envs", "precision", "nq", "nv", "nu", "nbody", "obs_dim", "elem_size",
-                                       "resident_con", "resident_efc", "wide_con", "wide_efc", "resident_waves")]
+                                       "resident_con", "resident_efc", "wide_con", "wide_efc", "resident_waves",
+                                       "bound_con_all", "bound_efc_all", "bound_con_floor", "bound_efc_floor")]
 
 
 _LIB = None

@@ -81,6 +81,9 @@ class HsBatch:
         self.resident_capacity = (info.resident_con, info.resident_efc)
         self.wide_capacity = (info.wide_con, info.wide_efc)
         self.resident_waves = info.resident_waves
+        # static worst case (contacts, rows) of one env: every pair touching / every geom on the floor
+        self.contact_bound_all = (info.bound_con_all, info.bound_efc_all)
+        self.contact_bound_floor = (info.bound_con_floor, info.bound_efc_floor)
 
     def queued(self, nsub=None):
         """True when an env step of this batch runs on the chunk-queue schedule (HS_SCHED_AUTO, more

@@ -367,6 +367,11 @@ int hs_batch_get_info(const hs_batch* b, hs_batch_info* out) {
   out->resident_efc = b->precision == HS_FP64 ? hs::MAXEFC_F64 : hs::MAXEFC;
   out->wide_con = hs::MAXCON_WIDE;
   out->wide_efc = hs::MAXEFC_WIDE;
+  const hs::ContactBound cb = hs::contact_bound(h);
+  out->bound_con_all = cb.con_all;
+  out->bound_efc_all = cb.efc_all;
+  out->bound_con_floor = cb.con_floor;
+  out->bound_efc_floor = cb.efc_floor;
   {
     DeviceGuard g(b->device);
     const bool pgs = b->model->host.solver == 1;

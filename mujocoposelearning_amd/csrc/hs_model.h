@@ -37,6 +37,12 @@ constexpr int MAXCON_F64 = 32;
 constexpr int MAXEFC_F64 = 128;
 constexpr int MAXCON_WIDE = 64;    // wide tier (2 contacts per lane)
 constexpr int MAXEFC_WIDE = 256;   // wide tier (8 rows per lane)
+// A flat-lying body -- every non-plane geom against the floor at once, 2 contacts per capsule, 4
+// pyramid rows per condim-3 contact, one row per joint / tendon limit -- always fits the wide tier
+// for any model within the other capacities (mjcf.cpp contact_bound; build_dev_model also checks
+// the model's own count).  Only body-body pile-ups on top of it can overflow (HS_WARN_OVERFLOW).
+static_assert(2 * (MAXGEOM - 1) <= MAXCON_WIDE, "wide tier must hold every geom on the floor");
+static_assert(4 * 2 * (MAXGEOM - 1) + MAXJNT + MAXTEN <= MAXEFC_WIDE, "wide tier rows: every geom on the floor");
 constexpr int MAXLEVEL = 16;
 constexpr int MAXJPB = 3;     // hinge joints per body (kinematics keeps their rotations in registers)
 // solimp on the device: MuJoCo's (d0, dwidth, width, midpoint, power) followed by derived constants

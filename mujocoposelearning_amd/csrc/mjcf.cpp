@@ -936,6 +936,10 @@ int model_field(const HostModel& m, const std::string& name, double* out, int n)
   else if (name == "actuator_gear") Dv(m.actuator_gear);
   else if (name == "actuator_ctrlrange") Dv(m.actuator_ctrlrange);
   else if (name == "actuator_ctrllimited") I(m.actuator_ctrllimited);
+  else if (name == "contact_bound") {
+    const ContactBound cb = contact_bound(m);
+    v = {(double)cb.con_all, (double)cb.efc_all, (double)cb.con_floor, (double)cb.efc_floor};
+  }
   else if (name == "collision_pairs") { for (auto& p : m.pair_geom) { v.push_back(p.first); v.push_back(p.second); } }
   else if (name.rfind("key_", 0) == 0) {
     auto it = m.keyframes.find(name.substr(4));
@@ -957,6 +961,35 @@ void fill_solimp(T (&dst)[SOLIMP], const double* si) {
   dst[7] = (T)(1.0 / std::pow(1 - si[3], si[4] - 1));
 }
 
+ContactBound contact_bound(const HostModel& m) {
+  ContactBound b{0, 0, 0, 0};
+  int nlim = 0;
+  for (int j = 0; j < m.njnt; j++) nlim += (m.jnt_limited[j] && m.jnt_type[j] == JNT_HINGE) ? 1 : 0;
+  for (int t = 0; t < m.ntendon; t++) nlim += m.tendon_limited[t] ? 1 : 0;
+  for (const auto& pr : m.pair_geom) {
+    const int g1 = pr.first, g2 = pr.second, t1 = m.geom_type[g1], t2 = m.geom_type[g2];
+    const bool plane = t1 == GEOM_PLANE || t2 == GEOM_PLANE;
+    const bool caps = t1 == GEOM_CAPSULE || t2 == GEOM_CAPSULE;
+    // narrow phase maxima (collide_pair): plane-capsule and capsule-capsule 2, sphere pairs 1
+    const int ncon = (caps && (plane || (t1 == GEOM_CAPSULE && t2 == GEOM_CAPSULE))) ? 2 : 1;
+    int dim;
+    if (m.geom_priority[g1] != m.geom_priority[g2])
+      dim = m.geom_condim[m.geom_priority[g1] > m.geom_priority[g2] ? g1 : g2];
+    else
+      dim = std::max(m.geom_condim[g1], m.geom_condim[g2]);
+    const int rows = dim == 1 ? 1 : 2 * (dim - 1);       // pyramidal cone: 2 (condim - 1) edges
+    b.con_all += ncon;
+    b.efc_all += ncon * rows;
+    if (plane) {
+      b.con_floor += ncon;
+      b.efc_floor += ncon * rows;
+    }
+  }
+  b.efc_all += nlim;
+  b.efc_floor += nlim;
+  return b;
+}
+
 template <typename T>
 bool build_dev_model(const HostModel& m, DevModel<T>& d, std::string& err) {
   std::memset(&d, 0, sizeof d);
@@ -969,6 +1002,13 @@ bool build_dev_model(const HostModel& m, DevModel<T>& d, std::string& err) {
       !cap("njnt", m.njnt, MAXJNT) || !cap("ngeom", m.ngeom, MAXGEOM) || !cap("ntendon", m.ntendon, MAXTEN) ||
       !cap("nu", m.nu, MAXU) || !cap("npair", (int)m.pair_geom.size(), MAXPAIR))
     return false;
+  {   // every geom resting on the floor at once must fit the wide tier (contacts are dropped only
+      // past it, and only in body-body pile-ups on top of a flat-lying body)
+    const ContactBound cb = contact_bound(m);
+    if (!cap("contacts with every geom on the floor", cb.con_floor, MAXCON_WIDE) ||
+        !cap("constraint rows with every geom on the floor", cb.efc_floor, MAXEFC_WIDE))
+      return false;
+  }
   for (int b = 1; b < m.nbody; b++)
     if (m.body_rootid[b] != m.body_rootid[1]) { err = "engine supports a single kinematic tree under world"; return false; }
   for (int b = 1; b < m.nbody; b++) {   // kernel keeps a body's joint rotations in registers

@@ -45,6 +45,16 @@ bool compile_mjcf_file(const std::string& path, HostModel& out, std::string& err
 // Returns number of values written (or needed, if n is too small), -1 if unknown.
 int model_field(const HostModel& m, const std::string& name, double* out, int n);
 
+// Worst-case contact / constraint-row counts of one env, from the static collision pair list:
+// MuJoCo keeps every contact (custom_env.py:160 mj_step has no per-env cap).  Per pair, the most
+// contacts its narrow phase can return (plane-capsule 2, capsule-capsule 2, the sphere pairs 1);
+// per contact, its rows (condim 1: 1, condim 3 pyramidal: 4); plus one row per limited hinge and
+// per limited tendon (at most one side of a limit is violated at a time).  `all`: every pair
+// touching at once (a geometric bound, far above any reachable state); `floor`: every geom against
+// the plane at once (a humanoid lying flat) -- the engine's wide tier must hold it (build_dev_model).
+struct ContactBound { int con_all, efc_all, con_floor, efc_floor; };
+ContactBound contact_bound(const HostModel& m);
+
 // Build the device layout; returns false (with err) if the model exceeds engine capacity.
 template <typename T>
 bool build_dev_model(const HostModel& m, DevModel<T>& d, std::string& err);
