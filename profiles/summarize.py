@@ -14,17 +14,107 @@ traffic_step_kernel.json keeps one entry per precision (bench.py reads the one i
 import csv
 import json
 import os
+import re
 import statistics
+import struct
+import subprocess
 import sys
+import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STATS_STEPS = 3     # bench.py's stats_of() steps after the timed window
+
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+CODE_OBJECT = os.path.join(ROOT, "build", "obj", "hs_kernels.o")   # the product's kernels (make -C .../csrc)
+
+
+def code_object_resources(obj=CODE_OBJECT):
+    """Per-kernel register / LDS / scratch figures from the gfx950 code object's own metadata
+    (amdhsa.kernels notes of the object's .hip_fatbin offload bundle): the numbers the loader uses.
+    vgpr_count is the unified register count (arch VGPRs + AGPRs); rocprofv3's VGPR_Count /
+    Accum_VGPR_Count columns are granule-rounded allocations and do not split it the same way."""
+    with tempfile.TemporaryDirectory() as td:
+        fat = os.path.join(td, "fat.bin")
+        subprocess.check_call([f"{LLVM}/llvm-objcopy", "--dump-section", f".hip_fatbin={fat}", obj, os.path.join(td, "o")])
+        data = open(fat, "rb").read()
+        out = {}
+        pos = 0
+        while True:
+            pos = data.find(b"__CLANG_OFFLOAD_BUNDLE__", pos)
+            if pos < 0: break
+            n = struct.unpack_from("<Q", data, pos + 24)[0]
+            p = pos + 32
+            for _ in range(n):
+                off, size, idl = struct.unpack_from("<QQQ", data, p); p += 24
+                ident = data[p:p + idl].decode(); p += idl
+                if "gfx950" in ident:
+                    co = os.path.join(td, "co.elf")
+                    open(co, "wb").write(data[pos + off: pos + off + size])
+                    notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], capture_output=True, text=True).stdout
+                    item = None
+                    for line in notes.splitlines():
+                        m = re.match(r"(\s*)(-?)\s*\.(\w+):\s+(.*)$", line)
+                        if not m: continue
+                        ind, dash, k, v = m.groups()
+                        if dash and len(ind) == 2:   # a new entry of amdhsa.kernels
+                            item = {}
+                        if item is None: continue
+                        if k == "name": out[v.strip()] = item
+                        elif k in ("vgpr_count", "agpr_count", "sgpr_count", "private_segment_fixed_size", "group_segment_fixed_size", "vgpr_spill_count", "sgpr_spill_count"):
+                            item[k] = int(v)
+            pos += 24
+        return out
 
 
 def is_step(name):
     # the resident-tier step kernel: one wave per pair (step_kernel<...>) or the chunk-queue schedule
     # (step_kernel_queue<...>, the fp64 engine at 4096 envs)
     return ("step_kernel<" in name or "step_kernel_queue<" in name) and "wide" not in name
+
+
+def resource_lines(kernel_name, out):
+    """Registers from the code object's metadata (authoritative), rocprofv3's columns beside them."""
+    lines = []
+    try:
+        res = code_object_resources()
+        mangled = next((k for k in res if k in kernel_name), None)
+        if mangled is None:   # rocprofv3 prints demangled names: match on the instance's template arguments
+            want = ("step_kernel_queue" if "queue" in kernel_name else "step_kernel") + \
+                   ("Id" if "double" in kernel_name else "If") + "Li27ELb" + ("1" if "true" in kernel_name else "0")
+            mangled = next((k for k in res if want in k and "wide" not in k), None)
+        r = res.get(mangled)
+        if r:
+            out["code_object"] = dict(r, kernel=mangled)
+            lines.append(f"Code object ({mangled[:60]}...): arch VGPR {r['vgpr_count'] - r['agpr_count']} + AGPR "
+                         f"{r['agpr_count']} (unified {r['vgpr_count']}), SGPR {r['sgpr_count']}, VGPRs spilled "
+                         f"{r['vgpr_spill_count']}, SGPRs spilled to VGPR lanes {r['sgpr_spill_count']}, scratch "
+                         f"{r['private_segment_fixed_size']} B/lane, LDS {r['group_segment_fixed_size']} B/workgroup.")
+    except (OSError, subprocess.CalledProcessError, StopIteration) as e:
+        lines.append(f"(code object metadata unavailable: {e})")
+    lines.append(f"rocprofv3 columns (allocation granules, not the split above): VGPR_Count {out['vgpr']}, "
+                 f"Accum_VGPR_Count {out['agpr']}, SGPR {out['sgpr']}, LDS {out['lds_bytes']} B/workgroup, scratch "
+                 f"{out['scratch_bytes_per_lane']} B/lane, grid {out['grid']} threads x wg {out['workgroup']}.")
+    return lines
+
+
+def resources_report(path=None):
+    """profiles/resources_<tag>.md: every step-kernel instance's registers from the code object."""
+    res = code_object_resources()
+    lines = ["# Step-kernel resources from the gfx950 code object metadata (build/obj/hs_kernels.o)", "",
+             "| kernel | arch VGPR | AGPR | unified | VGPR spilled | SGPR | SGPR spills (to VGPR lanes) | scratch B/lane | LDS B/wg |",
+             "|---|---|---|---|---|---|---|---|---|"]
+    for k in sorted(res):
+        if "kernel" not in k:
+            continue
+        r = res[k]
+        lines.append(f"| `{k[:70]}` | {r['vgpr_count'] - r['agpr_count']} | {r['agpr_count']} | {r['vgpr_count']} | "
+                     f"{r['vgpr_spill_count']} | {r['sgpr_count']} | {r['sgpr_spill_count']} | "
+                     f"{r['private_segment_fixed_size']} | {r['group_segment_fixed_size']} |")
+    text = "\n".join(lines) + "\n"
+    if path:
+        open(path, "w").write(text)
+    return text
 
 
 def main(tag="r2a", precision="fp64", n_envs=4096, timed=50, src=None):
@@ -85,9 +175,7 @@ def main(tag="r2a", precision="fp64", n_envs=4096, timed=50, src=None):
               f"kernel r2a); traffic/(algo + hand-off) = {corrected / (algo + 2 * 87 * es * n_envs):.2f}x; "
               f"{corrected / (statistics.mean(win) * 1e-3) / 1e9:.0f} GB/s of the 8 TB/s HBM"]
               if "queue" in row["Kernel_Name"] else []) + ["",
-              "## Resources", "",
-              f"VGPR {out['vgpr']} (+{out['agpr']} AGPR), SGPR {out['sgpr']}, LDS {out['lds_bytes']} B/workgroup, "
-              f"scratch {out['scratch_bytes_per_lane']} B/lane, grid {out['grid']} threads x wg {out['workgroup']}."]
+              "## Resources", ""] + resource_lines(row["Kernel_Name"], out)
     sq = {}
     for sub in ("sq", "sq2"):
         f = os.path.join(src, sub, f"{sub}_counter_collection.csv")
@@ -130,4 +218,7 @@ def main(tag="r2a", precision="fp64", n_envs=4096, timed=50, src=None):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:])
+    if sys.argv[1:2] == ["--resources"]:      # python profiles/summarize.py --resources <tag>
+        print(resources_report(os.path.join(ROOT, "profiles", f"resources_{sys.argv[2]}.md")))
+    else:
+        main(*sys.argv[1:])
