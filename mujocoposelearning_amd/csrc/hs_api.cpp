@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -45,6 +46,35 @@ bool hip_ok(hipError_t e, const char* what) {
   if (e == hipSuccess) return true;
   g_err = std::string(what) + ": " + hipGetErrorString(e);
   return false;
+}
+
+// Uncached device memory (the chunk queue's hand-off rows, claim / exit / epoch words and pair
+// flags) is recycled only as uncached memory: freed blocks go to a per-device list instead of
+// hipFree.  Round-3 finding: after a batch was destroyed, its hipFree'd UNCACHED hand-off rows were
+// handed back out as ordinary memory -- torch tensors of the next batch -- and a few hundred obs rows
+// of that batch intermittently read back stale values (tests/gpu_queue_wide_probe.py: 3 of 3 runs
+// before, none after); keeping UC memory out of the general pool removes that path.
+struct UcBlock { int device; size_t bytes; void* ptr; };
+std::mutex g_uc_mu;
+std::vector<UcBlock> g_uc_free;
+
+bool uc_alloc(int device, size_t bytes, void** out) {
+  {
+    std::lock_guard<std::mutex> lk(g_uc_mu);
+    for (size_t i = 0; i < g_uc_free.size(); i++)
+      if (g_uc_free[i].device == device && g_uc_free[i].bytes >= bytes && g_uc_free[i].bytes <= 2 * bytes + 4096) {
+        *out = g_uc_free[i].ptr;
+        g_uc_free.erase(g_uc_free.begin() + (long)i);
+        return true;
+      }
+  }
+  return hipExtMallocWithFlags(out, bytes, hipDeviceMallocUncached) == hipSuccess;
+}
+
+void uc_release(int device, size_t bytes, void* ptr) {
+  if (!ptr) return;
+  std::lock_guard<std::mutex> lk(g_uc_mu);
+  g_uc_free.push_back({device, bytes, ptr});
 }
 
 struct DeviceGuard {
@@ -322,11 +352,14 @@ hs_batch* hs_batch_create(const hs_model* m, int n_envs, int device, uint64_t se
   if (!hip_ok(hipMalloc(&b->dbg, hs::DBGDIM * 8), "hipMalloc(dbg)") ||
       !hip_ok(hipMalloc((void**)&b->redo, (N + 2) * sizeof(int)), "hipMalloc(redo)") ||
       !hip_ok(hipMalloc((void**)&b->redo_total, sizeof(unsigned long long)), "hipMalloc(redo_total)") ||
-      // chunk-queue hand-off rows and flags: UNCACHED device memory, so a hand-off between waves on
-      // different CUs / XCDs needs no L1 invalidate or L2 write-back (hs_kernels.hip step_pair)
-      !hip_ok(hipExtMallocWithFlags(&b->mid, N * hs::MIDDIM * es, hipDeviceMallocUncached), "hipMalloc(mid)") ||
-      !hip_ok(hipExtMallocWithFlags((void**)&b->qsync, hs::qsync_words((int)N) * sizeof(int), hipDeviceMallocUncached),
-              "hipMalloc(qsync)")) {
+      // chunk-queue hand-off rows, claim counters and pair flags: UNCACHED device memory from the UC
+      // pool above, so a hand-off between waves on different CUs / XCDs needs no L2 write-back or
+      // invalidate (hs_kernels.hip step_pair; a cached version with agent-scope release / acquire
+      // measured 9% slower per fp64 launch: buffer_wbl2 writes back the producer XCD's whole L2)
+      !(uc_alloc(device, N * hs::MIDDIM * es, &b->mid) ? true
+          : (g_err = "hipExtMallocWithFlags(mid, uncached) failed", false)) ||
+      !(uc_alloc(device, hs::qsync_words((int)N) * sizeof(int), (void**)&b->qsync) ? true
+          : (g_err = "hipExtMallocWithFlags(qsync, uncached) failed", false))) {
     hs_batch_destroy(b);
     return nullptr;
   }
@@ -350,8 +383,8 @@ void hs_batch_destroy(hs_batch* b) {
   if (b->dbg) (void)hipFree(b->dbg);
   if (b->redo) (void)hipFree(b->redo);
   if (b->redo_total) (void)hipFree(b->redo_total);
-  if (b->mid) (void)hipFree(b->mid);
-  if (b->qsync) (void)hipFree(b->qsync);
+  if (b->mid) uc_release(b->device, (size_t)b->n * hs::MIDDIM * (b->precision == HS_FP64 ? 8 : 4), b->mid);
+  if (b->qsync) uc_release(b->device, hs::qsync_words(b->n) * sizeof(int), b->qsync);
   delete b;
 }
 

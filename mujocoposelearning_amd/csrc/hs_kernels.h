@@ -13,10 +13,12 @@ constexpr int DBGDIM = 32768;        // stage dump (env 0 only) for parity debug
 // hand-off row of a queued env step (qpos, qvel, qacc_warmstart, time, warning counters)
 constexpr int MID_Q = 0, MID_V = MAXQ, MID_WS = MAXQ + MAXDOF, MID_TIME = MAXQ + 2 * MAXDOF, MID_W = MID_TIME + 1;
 constexpr int MIDDIM = MID_W + 7;
-// chunk-queue sync words (uncached device memory): claim counter, exit counter, per-pair flags
-// (0 idle; s1 = state handed over; -1 = abandoned by a consumer that timed out -- the late producer
-// resets it; every flag is 0 again when a launch ends)
-constexpr int QS_HEAD = 0, QS_EXIT = 1, QS_FLAG = 2;
+// chunk-queue sync words (uncached device memory): claim counter, exit counter, launch epoch,
+// per-pair flags.  A pair's flag holds the tag of the launch whose first chunk last handed its state
+// over (tag = epoch + 1, the epoch advanced by the last wave out of every queued launch), so a flag
+// left over from an earlier launch -- e.g. by a producer that arrived after its consumer timed out
+// -- never matches: no reset store, no returning atomic.
+constexpr int QS_HEAD = 0, QS_EXIT = 1, QS_EPOCH = 2, QS_FLAG = 3;
 constexpr size_t qsync_words(int n_envs) { return QS_FLAG + (size_t)((n_envs + 1) / 2); }
 
 enum StepMode { MODE_ENV_STEP = 0, MODE_RESET = 1, MODE_PHYSICS = 2 };

@@ -294,8 +294,87 @@ __device__ __forceinline__ void cross_force(const T* v, const T* f, T* r) {
 // pivot and a_jk (j > k) back as broadcast ds_reads, so the update is pure FMAs:
 //   A_ij -= (a_ik / a_kk) a_jk.
 
+// fp64: the same two-column elimination with a one-panel lookahead.  Step s factors pivot panel
+// (k, k+1) = (2s, 2s+1) from buffer s % 2, updates the NEXT panel (k+2, k+3) first and publishes it
+// into the other buffer, then updates the trailing columns >= k+4.  The scheduling fence sits
+// between a step's publish and its trailing update, so step s's trailing FMAs share a scheduling
+// region with step s+1's pivot read and reciprocal-square-root chain: the issue-bound updates hide
+// under the latency-bound chain instead of running after it.  Same operations per element (the
+// values are bitwise those of chol_rows_2c).
 template <int NV, typename T>
-__device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb)[2]) {
+__device__ __forceinline__ void chol_rows_la(T (&A)[NV], T& dinv, int sl, T (*cb0)[2], T (*cb1)[2]) {
+  static_assert(NV % 2 == 1, "lookahead variant written for odd NV (humanoid: 27)");
+  {
+    const int sl_p = opaque_v(sl);
+    cb0[sl_p][0] = A[0];
+    cb0[sl_p][1] = A[1];
+  }
+  T pf0 = 0, pf1 = 0;                    // previous step's Schur coefficients (trailing update)
+  static_for<0, NV / 2>([&](auto bc) {
+    constexpr int st = decltype(bc)::value;
+    constexpr int k = 2 * st;
+    T (*cb)[2] = (st & 1) ? cb1 : cb0;
+    T (*pb)[2] = (st & 1) ? cb0 : cb1;   // previous panel's buffer (its trailing columns), next publish
+    const int sl_k = opaque_v(sl);
+    // previous step's trailing update of THIS step's next panel (k+2, k+3) first: it feeds the publish
+    if constexpr (st > 0) {
+      static_for<k + 2, (k + 4 < NV ? k + 4 : NV)>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        A[j] = fma(-pf0, pb[j][0], fma(-pf1, pb[j][1], A[j]));
+      });
+    }
+    T p = cb[k][0], q = cb[k + 1][0], t = cb[k + 1][1];
+    p = p > T(1e-30) ? p : T(1e-30);
+    T r1 = rsqrt_t(p);
+    T l10 = q * r1;
+    T s11 = t - l10 * l10;
+    s11 = s11 > T(1e-30) ? s11 : T(1e-30);
+    T r2 = rsqrt_t(s11);
+    T z0 = A[k] * r1;
+    T z1 = (sl_k == k + 1) ? s11 * r2 : (A[k + 1] - l10 * z0) * r2;
+    T f1 = z1 * r2;
+    T f0 = (z0 - l10 * f1) * r1;
+    A[k] = (sl_k == k) ? p * r1 : z0;
+    A[k + 1] = z1;
+    dinv = (sl_k == k) ? r1 : ((sl_k == k + 1) ? r2 : dinv);
+    // previous step's remaining trailing columns (>= k+4): independent of this step's chain
+    if constexpr (st > 0) {
+      static_for<(k + 4 < NV ? k + 4 : NV), NV>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        A[j] = fma(-pf0, pb[j][0], fma(-pf1, pb[j][1], A[j]));
+      });
+    }
+    // this step's update of the next panel, and its publish (the previous panel's buffer is free:
+    // its last reads were the trailing updates just above)
+    static_for<k + 2, (k + 4 < NV ? k + 4 : NV)>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      A[j] = fma(-f0, cb[j][0], fma(-f1, cb[j][1], A[j]));
+    });
+    pb[sl_k][0] = A[k + 2];
+    pb[sl_k][1] = (k + 3 < NV) ? A[(k + 3 < NV) ? k + 3 : k + 2] : T(0);
+    pf0 = f0;
+    pf1 = f1;
+    SCHED_FENCE();
+  });
+  {   // the last step's trailing columns (>= NV - 1 + 2: none) and the trailing single column
+    constexpr int k = NV - 1;
+    T (*cb)[2] = ((NV / 2) & 1) ? cb1 : cb0;   // published by the last two-column step
+    const int sl_k = opaque_v(sl);
+    T akk = cb[k][0];
+    akk = akk > T(1e-30) ? akk : T(1e-30);
+    T r = rsqrt_t(akk);
+    A[k] = (sl_k == k) ? akk * r : A[k] * r;
+    dinv = (sl_k == k) ? r : dinv;
+  }
+  const int sl_z = opaque_v(sl);
+  static_for<0, NV>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    A[j] = sl_z > j ? A[j] : T(0);
+  });
+}
+
+template <int NV, typename T>
+__device__ __forceinline__ void chol_rows_2c(T (&A)[NV], T& dinv, int sl, T (*cb)[2]) {
   // two columns per LDS round trip: every lane publishes (a_ik, a_i,k+1) as one ds_write and reads
   // the 2x2 pivot block and (a_jk, a_j,k+1) back as broadcasts.  With L_P the pivot block's
   // Cholesky factor (1/L_kk = r1, L_k+1,k = l10, 1/L_k+1,k+1 = r2), row i gets
@@ -342,6 +421,14 @@ __device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb)[2
     constexpr int j = decltype(jc)::value;
     A[j] = sl_z > j ? A[j] : T(0);
   });
+}
+template <int NV, typename T>
+__device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb0)[2], T (*cb1)[2]) {
+#ifndef HS_NO_LOOKAHEAD
+  if constexpr (sizeof(T) == 8 && NV % 2 == 1) chol_rows_la<NV>(A, dinv, sl, cb0, cb1);
+  else
+#endif
+  chol_rows_2c<NV>(A, dinv, sl, cb0);   // fp32: at 256 VGPRs for 2 waves / SIMD, no lookahead
 }
 // solve (L L') x = b (L from chol_rows: strictly lower part, 1/L_ii in dinv); sub-lane i holds b_i;
 // returns x_i.  Forward: at step k every lane subtracts L_ik y_k (zero unless i > k), so lane k's b
@@ -453,7 +540,8 @@ struct Scratch {
     struct { T cdofdot[MAXDOF][6]; T cfrc[MAXBODY][6]; T csub[MAXBODY][6]; } r;   // RNE
     struct { T bvel[MAXBODY][6];                                  // J x mapping (rows, Newton)
              T cfrc[MAXBODY][6], linv[MAXBODY][3], mv[MAXBODY][3];    // full_state (after solve)
-             alignas(16) T cb[MAXDOF][2]; } n;                       // Cholesky column pairs
+             alignas(16) T cb[MAXDOF][2];                             // Cholesky column pairs
+             alignas(16) T cb2[MAXDOF][2]; } n;                      // (second buffer: fp64 lookahead)
   } u;
 };
 
@@ -1441,7 +1529,7 @@ struct Stepper {
       }
       HS_STAMP(clk, 9);
       T hdinv = 0;
-      chol_rows<NV>(H, hdinv, sl, s.u.n.cb);
+      chol_rows<NV>(H, hdinv, sl, s.u.n.cb, s.u.n.cb2);
       HS_STAMP(clk, 15);
       T sdir = -chol_solve<NV>(H, hdinv, g, sl);
       if (sl >= NV) sdir = 0;
@@ -1578,7 +1666,7 @@ struct Stepper {
 #pragma unroll
     for (int j = 0; j < NV; j++) L[j] = Mr[j];
     T dinv = 0;
-    chol_rows<NV>(L, dinv, sl, s.u.n.cb);
+    chol_rows<NV>(L, dinv, sl, s.u.n.cb, s.u.n.cb2);
     // warm start: f = -D (J xws - aref)_-;  per-row b_r = -aref_r, R_r
     if (sl < NV) s.vx[sl] = xws;
     WSYNC();
@@ -1814,7 +1902,7 @@ struct Stepper {
     for (int j = 0; j < NV; j++) He[j] = Mr[j] + ((j == sl) ? h * damp : T(0));
     HS_STAMP(clk, 20);
     T edinv = 0;
-    chol_rows<NV>(He, edinv, sl, s.u.n.cb);
+    chol_rows<NV>(He, edinv, sl, s.u.n.cb, s.u.n.cb2);
     HS_STAMP(clk, 21);
     T a = chol_solve<NV>(He, edinv, fsmooth + fcon, sl);
     HS_STAMP(clk, 17);
@@ -2064,16 +2152,18 @@ __device__ __forceinline__ void commit(MPtr<T> m, KPtr<T> k, const Stepper<T, NV
 // launch that follows re-runs its whole step from the same (untouched) inputs.
 // Queued schedule (launch_step sets p.queue when the pairs outnumber the resident waves): the
 // pair's substeps [s0, s1) only.  A chunk that ends before the last substep hands the state over
-// through b.mid and sets the pair's flag := s1; the last-substep chunk waits for flag == s0 and
-// starts from that row.  b.mid and the flags live in UNCACHED device memory (hs_api.cpp), so the
-// stores are in memory once `s_waitcnt vmcnt(0)` returns and the consumer's loads cannot hit a
-// stale L1 / L2 line: no cache invalidate or write-back on either side.  Every chunk recomputes the whole mj_step
-// pipeline from (qpos, qvel, qacc_warmstart, time), so the hand-off is exact: results are bitwise
-// those of one wave running all substeps.
+// through b.mid and sets the pair's flag := this launch's tag; the last-substep chunk waits for the
+// tag and starts from that row.  b.mid and the flags live in UNCACHED device memory (hs_api.cpp; its
+// blocks are recycled only as uncached memory), so the stores are in memory once `s_waitcnt
+// vmcnt(0)` returns and the consumer's loads cannot hit a stale L1 / L2 line: no cache invalidate or
+// write-back on either side.  Every chunk recomputes the whole mj_step pipeline from (qpos, qvel,
+// qacc_warmstart, time), so the hand-off is exact: results are bitwise those of one wave running all
+// substeps.
 // ghost: this half-wave mirrors env idx (the single-env schedule's upper half) and commits nothing.
 template <typename T, int NV, bool PGS, typename C>
 __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCache<T, C>* pcache, int idx,
-                                          int nidx, const int* list, int s0, int s1, int pair, bool ghost = false) {
+                                          int nidx, const int* list, int s0, int s1, int pair, bool ghost = false,
+                                          int tag = 0) {
   constexpr bool WIDE = C::WIDE;
   const int lane = opaque_v(threadIdx.x);   // (no lane-derived value hoisted out of the chunk-queue loop)
   const bool up = lane >= HL;
@@ -2099,27 +2189,12 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
       int* flag = ka->b.qsync + QS_FLAG + pair;
       int seen = 0;
       if (lane == 0) {   // bounded (~0.5 s): a broken hand-off must not hang the GPU
-        const bool force = pair + 1 == ka->p.dbg_lose_pair1;   // test hook: treat this pair's hand-off as lost
         int w = 0;
-        if (!force)
-          while ((seen = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != s0 && ++w < (1 << 22))
+        if (pair + 1 != ka->p.dbg_lose_pair1)   // test hook: treat this pair's hand-off as lost
+          while ((seen = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != tag && ++w < (1 << 22))
             __builtin_amdgcn_s_sleep(2);
-        if (seen == s0) {
-          __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // consumed: clean for the next launch
-        } else {
-          // Timed out (or forced): mark the pair abandoned (-1) so that a producer arriving late
-          // cleans the flag up itself instead of leaving a stale s0 that the next launch's
-          // consumer would match.  If the producer stored s0 in the meantime, the CAS fails:
-          // consume the flag here (and use the row, unless forced).
-          int expect = 0;
-          if (!__hip_atomic_compare_exchange_strong(flag, &expect, -1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT)) {
-            __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (!force) seen = expect;
-          }
-        }
       }
-      const bool lost = __builtin_amdgcn_readfirstlane(seen) != s0;
+      const bool lost = __builtin_amdgcn_readfirstlane(seen) != tag;
       WSYNC();   // (compiler order: the row loads stay behind the poll)
       const T* r = ka->b.mid + (size_t)env_id * MIDDIM;
       time = r[MID_TIME];
@@ -2201,12 +2276,7 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
         }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the row is in memory before the flag is
-      if (lane == 0) {
-        int* flag = k->b.qsync + QS_FLAG + pair;
-        // -1: the consumer timed out and poisoned the env; leave the flag clean for the next launch
-        if (__hip_atomic_exchange(flag, s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == -1)
-          __hip_atomic_store(flag, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+      if (lane == 0) __hip_atomic_store(k->b.qsync + QS_FLAG + pair, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       HS_FLUSH();
       break;
     }
@@ -2329,13 +2399,17 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !PGS) ? 2 : 1) void step_ker
 // residency can deadlock it.
 template <typename T, int NV, bool PGS>
 __global__ __launch_bounds__(64, 1) void step_kernel_queue(KArgs<T> /* read via kernarg ptr */) {
+  const KPtr<T> ka = (KPtr<T>)__builtin_amdgcn_kernarg_segment_ptr();
+  // this launch's hand-off tag: the epoch only changes after every wave of the launch has left the
+  // claim loop (last wave out, below)
+  const int tag = __builtin_amdgcn_readfirstlane(
+      (__hip_atomic_load(ka->b.qsync + QS_EPOCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0x3fffffff) + 1);
   __shared__ Scratch<T, Resident<T>> smem[2];
   PgsCache<T, Resident<T>>* pcache = nullptr;
   if constexpr (PGS) {
     __shared__ PgsCache<T, Resident<T>> pgs_smem[2];
     pcache = &pgs_smem[threadIdx.x >= HL ? 1 : 0];
   }
-  const KPtr<T> ka = (KPtr<T>)__builtin_amdgcn_kernarg_segment_ptr();
   for (;;) {
     const KPtr<T> k = opaque(ka);       // nothing uniform kept live across items
     const int nsub = k->p.nsub, npairs = (k->nenv + 1) / 2;
@@ -2346,14 +2420,15 @@ __global__ __launch_bounds__(64, 1) void step_kernel_queue(KArgs<T> /* read via 
     const bool last = i >= npairs;
     const int pair = (int)((uint64_t)(last ? i - npairs : i) * (uint32_t)k->p.qmul % (uint32_t)npairs);
     step_pair<T, NV, PGS, Resident<T>>(k, smem, pcache, 2 * pair + (opaque_v(threadIdx.x) >= HL ? 1 : 0), k->nenv,
-                                       nullptr, last ? nsub - 1 : 0, last ? nsub : nsub - 1, pair);
+                                       nullptr, last ? nsub - 1 : 0, last ? nsub : nsub - 1, pair, false, tag);
   }
-  // the last wave out resets the counter for the next launch (every wave has made its final claim;
-  // each pair flag was reset by its last-substep item)
+  // the last wave out resets the counters and advances the epoch for the next launch (every wave has
+  // made its final claim and read this launch's tag)
   int* qs = ka->b.qsync;
   if (threadIdx.x == 0 && atomicAdd(&qs[QS_EXIT], 1) == (int)gridDim.x - 1) {
     qs[QS_HEAD] = 0;
     qs[QS_EXIT] = 0;
+    atomicAdd(&qs[QS_EPOCH], 1);
   }
 }
 

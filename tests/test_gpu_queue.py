@@ -75,8 +75,15 @@ def test_queue_with_wide_tier_reruns_bitwise_equals_direct(model):
     assert reruns[0] == reruns[1], reruns
     assert reruns[0][0] == len(idx)                    # exactly the overflowing envs, in the first step
     assert int(outs[0][-2][:, 3].sum()) == 0           # nothing dropped (re-run, not truncated)
-    for x, y in zip(*outs):
-        assert torch.equal(x, y)
+    names = ["obs0", "reward0", "qpos0", "qpos", "qvel", "ws", "time", "obs", "reward", "warning", "aux"]
+    for name, x, y in zip(names, *outs):
+        if not torch.equal(x, y):
+            d = (x.double() - y.double()).abs().reshape(n, -1)
+            bad = torch.nonzero(d.amax(1) > 0).flatten().cpu().numpy()
+            cols = torch.nonzero(d[bad].amax(0) > 0).flatten().cpu().numpy()
+            raise AssertionError(f"{name}: {bad.size} envs differ (e.g. {bad[:10].tolist()}, lying {np.intersect1d(bad, idx).tolist()}), "
+                                 f"columns {cols[:20].tolist()}, max {float(d.max()):.3e}; warnings "
+                                 f"{outs[0][-2].sum(0).tolist()} / {outs[1][-2].sum(0).tolist()}")
 
 
 def test_forced_lost_handoff_resets_the_pair_and_leaves_the_queue_clean(model):
@@ -175,3 +182,26 @@ def test_single_env_schedule_bitwise_equals_paired(model, prec):
         assert int(outs[0][-4].max()) >= 2                  # auto-resets happened
         for x, y in zip(*outs):
             assert torch.equal(x, y)
+
+
+def test_recreated_queue_batches_keep_obs_consistent(model):
+    """Round-3 regression: a batch created right after a destroyed fp64 queue batch must not see
+    stale data (the destroyed batch's uncached hand-off rows used to return to the general pool and
+    back out as the next batch's tensors; hs_api.cpp now recycles uncached blocks only as uncached
+    memory).  After one step, every env's obs[0:26] is its committed qpos[2:] (custom_env.py:242),
+    for several batches created and destroyed in turn, on both schedules."""
+    import torch
+    n = 4096
+    g = torch.Generator(device="cuda").manual_seed(12)
+    acts = torch.rand(2, n, 21, device="cuda", generator=g) * 2 - 1
+    for rep, sched in enumerate(("auto", "direct", "auto", "direct", "auto")):
+        b = _batch(model, n, seed=rep)
+        b.configure(schedule=sched)
+        b.reset()
+        for k in range(2):
+            b.step(acts[k])
+            obs, q = b.obs.clone(), b.qpos.clone()
+            bad = torch.nonzero((obs[:, :26] != q[:, 2:]).any(1)).flatten()
+            assert bad.numel() == 0, (rep, sched, k, bad[:10].tolist())
+        b.close()
+        del b
