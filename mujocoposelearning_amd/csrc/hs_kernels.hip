@@ -294,87 +294,8 @@ __device__ __forceinline__ void cross_force(const T* v, const T* f, T* r) {
 // pivot and a_jk (j > k) back as broadcast ds_reads, so the update is pure FMAs:
 //   A_ij -= (a_ik / a_kk) a_jk.
 
-// fp64: the same two-column elimination with a one-panel lookahead.  Step s factors pivot panel
-// (k, k+1) = (2s, 2s+1) from buffer s % 2, updates the NEXT panel (k+2, k+3) first and publishes it
-// into the other buffer, then updates the trailing columns >= k+4.  The scheduling fence sits
-// between a step's publish and its trailing update, so step s's trailing FMAs share a scheduling
-// region with step s+1's pivot read and reciprocal-square-root chain: the issue-bound updates hide
-// under the latency-bound chain instead of running after it.  Same operations per element (the
-// values are bitwise those of chol_rows_2c).
 template <int NV, typename T>
-__device__ __forceinline__ void chol_rows_la(T (&A)[NV], T& dinv, int sl, T (*cb0)[2], T (*cb1)[2]) {
-  static_assert(NV % 2 == 1, "lookahead variant written for odd NV (humanoid: 27)");
-  {
-    const int sl_p = opaque_v(sl);
-    cb0[sl_p][0] = A[0];
-    cb0[sl_p][1] = A[1];
-  }
-  T pf0 = 0, pf1 = 0;                    // previous step's Schur coefficients (trailing update)
-  static_for<0, NV / 2>([&](auto bc) {
-    constexpr int st = decltype(bc)::value;
-    constexpr int k = 2 * st;
-    T (*cb)[2] = (st & 1) ? cb1 : cb0;
-    T (*pb)[2] = (st & 1) ? cb0 : cb1;   // previous panel's buffer (its trailing columns), next publish
-    const int sl_k = opaque_v(sl);
-    // previous step's trailing update of THIS step's next panel (k+2, k+3) first: it feeds the publish
-    if constexpr (st > 0) {
-      static_for<k + 2, (k + 4 < NV ? k + 4 : NV)>([&](auto jc) {
-        constexpr int j = decltype(jc)::value;
-        A[j] = fma(-pf0, pb[j][0], fma(-pf1, pb[j][1], A[j]));
-      });
-    }
-    T p = cb[k][0], q = cb[k + 1][0], t = cb[k + 1][1];
-    p = p > T(1e-30) ? p : T(1e-30);
-    T r1 = rsqrt_t(p);
-    T l10 = q * r1;
-    T s11 = t - l10 * l10;
-    s11 = s11 > T(1e-30) ? s11 : T(1e-30);
-    T r2 = rsqrt_t(s11);
-    T z0 = A[k] * r1;
-    T z1 = (sl_k == k + 1) ? s11 * r2 : (A[k + 1] - l10 * z0) * r2;
-    T f1 = z1 * r2;
-    T f0 = (z0 - l10 * f1) * r1;
-    A[k] = (sl_k == k) ? p * r1 : z0;
-    A[k + 1] = z1;
-    dinv = (sl_k == k) ? r1 : ((sl_k == k + 1) ? r2 : dinv);
-    // previous step's remaining trailing columns (>= k+4): independent of this step's chain
-    if constexpr (st > 0) {
-      static_for<(k + 4 < NV ? k + 4 : NV), NV>([&](auto jc) {
-        constexpr int j = decltype(jc)::value;
-        A[j] = fma(-pf0, pb[j][0], fma(-pf1, pb[j][1], A[j]));
-      });
-    }
-    // this step's update of the next panel, and its publish (the previous panel's buffer is free:
-    // its last reads were the trailing updates just above)
-    static_for<k + 2, (k + 4 < NV ? k + 4 : NV)>([&](auto jc) {
-      constexpr int j = decltype(jc)::value;
-      A[j] = fma(-f0, cb[j][0], fma(-f1, cb[j][1], A[j]));
-    });
-    pb[sl_k][0] = A[k + 2];
-    pb[sl_k][1] = (k + 3 < NV) ? A[(k + 3 < NV) ? k + 3 : k + 2] : T(0);
-    pf0 = f0;
-    pf1 = f1;
-    SCHED_FENCE();
-  });
-  {   // the last step's trailing columns (>= NV - 1 + 2: none) and the trailing single column
-    constexpr int k = NV - 1;
-    T (*cb)[2] = ((NV / 2) & 1) ? cb1 : cb0;   // published by the last two-column step
-    const int sl_k = opaque_v(sl);
-    T akk = cb[k][0];
-    akk = akk > T(1e-30) ? akk : T(1e-30);
-    T r = rsqrt_t(akk);
-    A[k] = (sl_k == k) ? akk * r : A[k] * r;
-    dinv = (sl_k == k) ? r : dinv;
-  }
-  const int sl_z = opaque_v(sl);
-  static_for<0, NV>([&](auto jc) {
-    constexpr int j = decltype(jc)::value;
-    A[j] = sl_z > j ? A[j] : T(0);
-  });
-}
-
-template <int NV, typename T>
-__device__ __forceinline__ void chol_rows_2c(T (&A)[NV], T& dinv, int sl, T (*cb)[2]) {
+__device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb)[2]) {
   // two columns per LDS round trip: every lane publishes (a_ik, a_i,k+1) as one ds_write and reads
   // the 2x2 pivot block and (a_jk, a_j,k+1) back as broadcasts.  With L_P the pivot block's
   // Cholesky factor (1/L_kk = r1, L_k+1,k = l10, 1/L_k+1,k+1 = r2), row i gets
@@ -421,14 +342,6 @@ __device__ __forceinline__ void chol_rows_2c(T (&A)[NV], T& dinv, int sl, T (*cb
     constexpr int j = decltype(jc)::value;
     A[j] = sl_z > j ? A[j] : T(0);
   });
-}
-template <int NV, typename T>
-__device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb0)[2], T (*cb1)[2]) {
-#ifndef HS_NO_LOOKAHEAD
-  if constexpr (sizeof(T) == 8 && NV % 2 == 1) chol_rows_la<NV>(A, dinv, sl, cb0, cb1);
-  else
-#endif
-  chol_rows_2c<NV>(A, dinv, sl, cb0);   // fp32: at 256 VGPRs for 2 waves / SIMD, no lookahead
 }
 // solve (L L') x = b (L from chol_rows: strictly lower part, 1/L_ii in dinv); sub-lane i holds b_i;
 // returns x_i.  Forward: at step k every lane subtracts L_ik y_k (zero unless i > k), so lane k's b
@@ -540,8 +453,7 @@ struct Scratch {
     struct { T cdofdot[MAXDOF][6]; T cfrc[MAXBODY][6]; T csub[MAXBODY][6]; } r;   // RNE
     struct { T bvel[MAXBODY][6];                                  // J x mapping (rows, Newton)
              T cfrc[MAXBODY][6], linv[MAXBODY][3], mv[MAXBODY][3];    // full_state (after solve)
-             alignas(16) T cb[MAXDOF][2];                             // Cholesky column pairs
-             alignas(16) T cb2[MAXDOF][2]; } n;                      // (second buffer: fp64 lookahead)
+             alignas(16) T cb[MAXDOF][2]; } n;                       // Cholesky column pairs
   } u;
 };
 
@@ -1529,7 +1441,7 @@ struct Stepper {
       }
       HS_STAMP(clk, 9);
       T hdinv = 0;
-      chol_rows<NV>(H, hdinv, sl, s.u.n.cb, s.u.n.cb2);
+      chol_rows<NV>(H, hdinv, sl, s.u.n.cb);
       HS_STAMP(clk, 15);
       T sdir = -chol_solve<NV>(H, hdinv, g, sl);
       if (sl >= NV) sdir = 0;
@@ -1666,7 +1578,7 @@ struct Stepper {
 #pragma unroll
     for (int j = 0; j < NV; j++) L[j] = Mr[j];
     T dinv = 0;
-    chol_rows<NV>(L, dinv, sl, s.u.n.cb, s.u.n.cb2);
+    chol_rows<NV>(L, dinv, sl, s.u.n.cb);
     // warm start: f = -D (J xws - aref)_-;  per-row b_r = -aref_r, R_r
     if (sl < NV) s.vx[sl] = xws;
     WSYNC();
@@ -1902,7 +1814,7 @@ struct Stepper {
     for (int j = 0; j < NV; j++) He[j] = Mr[j] + ((j == sl) ? h * damp : T(0));
     HS_STAMP(clk, 20);
     T edinv = 0;
-    chol_rows<NV>(He, edinv, sl, s.u.n.cb, s.u.n.cb2);
+    chol_rows<NV>(He, edinv, sl, s.u.n.cb);
     HS_STAMP(clk, 21);
     T a = chol_solve<NV>(He, edinv, fsmooth + fcon, sl);
     HS_STAMP(clk, 17);
@@ -2552,24 +2464,30 @@ hipError_t launch_step(const DevModel<T>* dmodel, int nv, const EnvBuffers<T>& b
   return hipGetLastError();
 }
 
-template hipError_t launch_step<float>(const DevModel<float>*, int, const EnvBuffers<float>&, const float*,
-                                       const uint8_t*, const float*, const float*, const StepParams&, int,
-                                       hipStream_t);
-#ifndef HS_DEV_F32_ONLY
-template hipError_t launch_step<double>(const DevModel<double>*, int, const EnvBuffers<double>&, const float*,
-                                        const uint8_t*, const double*, const double*, const StepParams&, int,
-                                        hipStream_t);
-#endif
-
 template <typename T>
 hipError_t launch_kinematics(const DevModel<T>* dmodel, int nv, const T* qpos, T* out, hipStream_t stream) {
   if (nv != 27) return hipErrorInvalidValue;
   hipLaunchKernelGGL((kin_kernel<T, 27>), dim3(1), dim3(WAVE), 0, stream, (MPtr<T>)dmodel, qpos, out);
   return hipGetLastError();
 }
+// The Makefile compiles this file once per precision (HS_ONLY_F32 / HS_ONLY_F64), so each engine
+// gets its own code-generation flags (the fp64 one without MachineLICM).
+#ifndef HS_ONLY_F64
+template hipError_t launch_step<float>(const DevModel<float>*, int, const EnvBuffers<float>&, const float*,
+                                       const uint8_t*, const float*, const float*, const StepParams&, int,
+                                       hipStream_t);
 template int resident_waves<float>(bool);
-template int resident_waves<double>(bool);
 template hipError_t launch_kinematics<float>(const DevModel<float>*, int, const float*, float*, hipStream_t);
+#endif
+#if !defined(HS_DEV_F32_ONLY) && !defined(HS_ONLY_F32)
+template hipError_t launch_step<double>(const DevModel<double>*, int, const EnvBuffers<double>&, const float*,
+                                        const uint8_t*, const double*, const double*, const StepParams&, int,
+                                        hipStream_t);
+#endif
+
+#if !defined(HS_DEV_F32_ONLY) && !defined(HS_ONLY_F32)
+template int resident_waves<double>(bool);
 template hipError_t launch_kinematics<double>(const DevModel<double>*, int, const double*, double*, hipStream_t);
+#endif
 
 }  // namespace hs

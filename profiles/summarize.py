@@ -26,14 +26,21 @@ STATS_STEPS = 3     # bench.py's stats_of() steps after the timed window
 
 
 LLVM = "/opt/rocm/lib/llvm/bin"
-CODE_OBJECT = os.path.join(ROOT, "build", "obj", "hs_kernels.o")   # the product's kernels (make -C .../csrc)
+CODE_OBJECTS = [os.path.join(ROOT, "build", "obj", f"hs_kernels_{p}.o") for p in ("f32", "f64")]   # make -C .../csrc
 
 
-def code_object_resources(obj=CODE_OBJECT):
+def code_object_resources(objs=None):
     """Per-kernel register / LDS / scratch figures from the gfx950 code object's own metadata
     (amdhsa.kernels notes of the object's .hip_fatbin offload bundle): the numbers the loader uses.
     vgpr_count is the unified register count (arch VGPRs + AGPRs); rocprofv3's VGPR_Count /
     Accum_VGPR_Count columns are granule-rounded allocations and do not split it the same way."""
+    out = {}
+    for obj in objs or CODE_OBJECTS:
+        out.update(_code_object_resources(obj))
+    return out
+
+
+def _code_object_resources(obj):
     with tempfile.TemporaryDirectory() as td:
         fat = os.path.join(td, "fat.bin")
         subprocess.check_call([f"{LLVM}/llvm-objcopy", "--dump-section", f".hip_fatbin={fat}", obj, os.path.join(td, "o")])
@@ -101,7 +108,7 @@ def resource_lines(kernel_name, out):
 def resources_report(path=None):
     """profiles/resources_<tag>.md: every step-kernel instance's registers from the code object."""
     res = code_object_resources()
-    lines = ["# Step-kernel resources from the gfx950 code object metadata (build/obj/hs_kernels.o)", "",
+    lines = ["# Step-kernel resources from the gfx950 code object metadata (build/obj/hs_kernels_{f32,f64}.o)", "",
              "| kernel | arch VGPR | AGPR | unified | VGPR spilled | SGPR | SGPR spills (to VGPR lanes) | scratch B/lane | LDS B/wg |",
              "|---|---|---|---|---|---|---|---|---|"]
     for k in sorted(res):
