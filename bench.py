@@ -176,6 +176,7 @@ def main():
     ap.add_argument("--precision", default="fp64", choices=["fp32", "fp64"],
                     help="headline arithmetic (fp64 = the reference's mjtNum; fp32 is an extra leg)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--schedule", default="auto", help=argparse.SUPPRESS)   # A/B runs (HsBatch.configure)
     ap.add_argument("--no-rollout", action="store_true")
     ap.add_argument("--no-gae", action="store_true")
     ap.add_argument("--train-iters", type=int, default=2, help="PPO iterations of the train mode (0: skip)")
@@ -259,7 +260,7 @@ def main():
         e = HumanoidVecEnv(cfg_x, n_envs=n_x, device=dev_index, precision=precision, seed=seed + 7919 * rank,
                            model=model)
         # sim-only timing writes what a trainer needs; the aux row / ctrl copy only when stats are read
-        e.batch.configure(aux=stats, ctrl=False)
+        e.batch.configure(aux=stats, ctrl=False, schedule=args.schedule)
         e.reset_tensors()
         return e
 

@@ -93,9 +93,11 @@ typedef struct {
  * 1024 envs per GPU); else one wave per env pair when every pair fits on the GPU at once; else (the
  * fp64 engine at 4096 envs) a persistent grid that runs each env step as two chunk items (substeps
  * [0, frame_skip - 1), then the last substep + obs / reward / auto-reset) from a queue.
- * DIRECT: always one wave per pair.  SINGLE: always one wave per env.  Results are bitwise
- * identical whichever schedule runs. */
-enum { HS_SCHED_AUTO = 0, HS_SCHED_DIRECT = 1, HS_SCHED_SINGLE = 2 };
+ * The queue claims the pairs heaviest first by the durations its previous launch measured.
+ * DIRECT: always one wave per pair.  SINGLE: always one wave per env.  FIXED_ORDER: AUTO with the
+ * queue's claims in a fixed permutation (A/B runs, tests).  Results are bitwise identical
+ * whichever schedule runs. */
+enum { HS_SCHED_AUTO = 0, HS_SCHED_DIRECT = 1, HS_SCHED_SINGLE = 2, HS_SCHED_FIXED_ORDER = 3 };
 
 /* Device buffers of a batch (row-major, env-major).  Element type of the T* entries is float
  * (HS_FP32) or double (HS_FP64). */

@@ -18,7 +18,7 @@ HS_REWARD_NONE, HS_REWARD_STAND, HS_REWARD_KNEELING, HS_REWARD_WALK = -1, 0, 1, 
 HS_NWARN = 4
 HS_AUXDIM = 40
 HS_OUT_AUX, HS_OUT_CTRL = 1, 2   # hs_env_config.outputs bits
-HS_SCHED_AUTO, HS_SCHED_DIRECT, HS_SCHED_SINGLE = 0, 1, 2   # hs_env_config.schedule
+HS_SCHED_AUTO, HS_SCHED_DIRECT, HS_SCHED_SINGLE, HS_SCHED_FIXED_ORDER = 0, 1, 2, 3   # hs_env_config.schedule
 DBGDIM = 32768
 
 

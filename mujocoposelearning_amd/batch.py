@@ -90,7 +90,8 @@ class HsBatch:
         env pairs than resident waves, >= 2 substeps; include/hsim.h)."""
         nsub = self.cfg.frame_skip if nsub is None else nsub
         n = max(hi - lo for _, lo, hi in self._groups)
-        return (self.cfg.schedule == _lib.HS_SCHED_AUTO and nsub >= 2 and 0 < self.resident_waves < (n + 1) // 2)
+        return (self.cfg.schedule in (_lib.HS_SCHED_AUTO, _lib.HS_SCHED_FIXED_ORDER) and nsub >= 2
+                and 0 < self.resident_waves < (n + 1) // 2)
 
     def schedule_name(self, nsub=None):
         """The schedule an env step of this batch runs on (the largest group's; hs_kernels.hip
@@ -120,8 +121,9 @@ class HsBatch:
                   schedule=None):
         """``schedule``: "auto" (default: one wave per env when every env fits the resident waves, a
         chunk queue when the env pairs outnumber them, else one wave per env pair; include/hsim.h
-        HS_SCHED_AUTO), "direct" (one wave per env pair) or "single" (one wave per env); results
-        are bitwise identical.
+        HS_SCHED_AUTO), "direct" (one wave per env pair), "single" (one wave per env) or
+        "fixed_order" (auto with the chunk queue's claims in a fixed permutation instead of cost
+        order); results are bitwise identical.
         ``aux`` / ``ctrl``: write the optional aux row (qacc, subtree com, contact / row counts,
         solver iterations) and the data.ctrl copy at every commit (both on by default; data views,
         host rewards and statistics read them, the on-device trainer does not)."""
@@ -132,7 +134,7 @@ class HsBatch:
             c.outputs = (c.outputs & ~_lib.HS_OUT_CTRL) | (_lib.HS_OUT_CTRL if ctrl else 0)
         if schedule is not None:
             c.schedule = {"auto": _lib.HS_SCHED_AUTO, "direct": _lib.HS_SCHED_DIRECT,
-                          "single": _lib.HS_SCHED_SINGLE}[schedule]
+                          "single": _lib.HS_SCHED_SINGLE, "fixed_order": _lib.HS_SCHED_FIXED_ORDER}[schedule]
         if frame_skip is not None:
             c.frame_skip = int(frame_skip)
         if duration is not None:

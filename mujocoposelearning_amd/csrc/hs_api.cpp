@@ -425,7 +425,8 @@ int hs_set_config(hs_batch* b, const hs_env_config* cfg) {
   if (cfg->max_newton < 1) return fail("max_newton must be >= 1");
   if (cfg->reward_id < HS_REWARD_NONE || cfg->reward_id > HS_REWARD_WALK) return fail("unknown reward id");
   if (cfg->outputs & ~(HS_OUT_AUX | HS_OUT_CTRL)) return fail("unknown output bits");
-  if (cfg->schedule != HS_SCHED_AUTO && cfg->schedule != HS_SCHED_DIRECT && cfg->schedule != HS_SCHED_SINGLE)
+  if (cfg->schedule != HS_SCHED_AUTO && cfg->schedule != HS_SCHED_DIRECT && cfg->schedule != HS_SCHED_SINGLE &&
+      cfg->schedule != HS_SCHED_FIXED_ORDER)
     return fail("unknown schedule");
   b->cfg = *cfg;
   return 0;

@@ -19,7 +19,21 @@ constexpr int MIDDIM = MID_W + 7;
 // left over from an earlier launch -- e.g. by a producer that arrived after its consumer timed out
 // -- never matches: no reset store, no returning atomic.
 constexpr int QS_HEAD = 0, QS_EXIT = 1, QS_EPOCH = 2, QS_FLAG = 3;
-constexpr size_t qsync_words(int n_envs) { return QS_FLAG + (size_t)((n_envs + 1) / 2); }
+// Cost-ordered claims: every queued launch measures each pair's duration (first chunk + last
+// substep, 100 MHz realtime clock) and counts the pair into one of QNB buckets of QBIN ticks,
+// heaviest first; the next queued launch claims the pairs bucket by bucket (a counting sort done
+// by the previous launch), so the launch ends on the cheapest last substeps.  After the flags:
+// qcost[npairs] (first-chunk durations), cnt[2][QNB] (bucket counts, by epoch parity: the launch
+// reads cnt[e & 1], counts into cnt[(e + 1) & 1], and its last wave out zeroes cnt[e & 1]),
+// ord[2][QNB][npairs] (the pairs of each bucket).  A launch whose read counts do not sum to npairs
+// (the batch's first queued launch) claims in the fixed multiplicative permutation (p.qmul).
+constexpr int QNB = 32, QBIN = 2500;   // 32 buckets of 25 us
+constexpr size_t qs_cost(int npairs) { return QS_FLAG + (size_t)npairs; }
+constexpr size_t qs_cnt(int npairs, int par) { return QS_FLAG + 2 * (size_t)npairs + (size_t)par * QNB; }
+constexpr size_t qs_ord(int npairs, int par) {
+  return QS_FLAG + 2 * (size_t)npairs + 2 * QNB + (size_t)par * QNB * npairs;
+}
+constexpr size_t qsync_words(int n_envs) { return qs_ord((n_envs + 1) / 2, 2); }
 
 enum StepMode { MODE_ENV_STEP = 0, MODE_RESET = 1, MODE_PHYSICS = 2 };
 enum RewardId { REWARD_NONE = -1, REWARD_STAND = 0, REWARD_KNEELING = 1, REWARD_WALK = 2 };
@@ -72,11 +86,14 @@ struct StepParams {
   int outputs;           // OUT_* bits: optional per-env outputs written at commit
   int schedule;          // HS_SCHED_AUTO (0) / HS_SCHED_DIRECT (1) (hs_env_config.schedule)
   int queue;             // set by launch_step: 1 = chunk-queue schedule (persistent grid), 0 = one wave per pair
-  int qmul;              // chunk-queue claim order: item i -> pair (i * qmul) mod npairs (qmul coprime to npairs)
+  int qmul;              // chunk-queue fallback claim order: item i -> pair (i * qmul) mod npairs (coprime)
+  int qorder;            // chunk queue: 1 = cost-ordered claims (QNB buckets), 0 = the qmul permutation only
   int dbg_lose_pair1;    // test hook (hs_debug_lose_handoff): pair + 1 whose hand-off is treated as lost; 0 = off
   int single;            // set by launch_step: 1 = one env per wave (upper half-wave a ghost), 0 = env pairs
 };
-enum Schedule { SCHED_AUTO = 0, SCHED_DIRECT = 1, SCHED_SINGLE = 2 };   // hs_env_config.schedule
+// hs_env_config.schedule (SCHED_FIXED_ORDER: AUTO with the chunk queue's claims in the fixed
+// permutation instead of cost order -- A/B runs and tests)
+enum Schedule { SCHED_AUTO = 0, SCHED_DIRECT = 1, SCHED_SINGLE = 2, SCHED_FIXED_ORDER = 3 };
 // optional outputs (hs_env_config.outputs): the aux row (qacc, subtree com, ncon, nefc, solver
 // iterations -- data views and stats) and the data.ctrl copy (data views / host rewards)
 enum Outputs { OUT_AUX = 1, OUT_CTRL = 2 };

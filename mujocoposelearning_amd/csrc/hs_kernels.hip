@@ -2305,42 +2305,95 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !PGS) ? 2 : 1) void step_ker
 // the GPU holds at once -- the fp64 engine at 1 wave per SIMD -- for multi-substep calls).  A
 // persistent grid claims items from one counter: first every pair's substeps [0, nsub - 1), then
 // every pair's last substep (+ obs / reward / auto-reset), so the launch ends on short items
-// instead of a second generation of whole env steps; pairs are taken in a fixed
-// multiplicative permutation (p.qmul).  Items are claimed only by running waves and a last-substep
-// item waits only on its own pair's first chunk, claimed npairs items earlier by a running wave: no
-// residency can deadlock it.
+// instead of a second generation of whole env steps.  Pairs are taken heaviest
+// first by the durations the previous queued launch measured (QNB cost buckets, hs_kernels.h), so
+// the launch ends on the cheapest last substeps; the batch's first queued launch uses a fixed
+// multiplicative permutation (p.qmul).  The order only decides which wave runs which pair when:
+// results are bitwise the same in any order.  Items are claimed only by running waves and a
+// last-substep item waits only on its own pair's first chunk, claimed npairs items earlier by a
+// running wave: no residency can deadlock it.
 template <typename T, int NV, bool PGS>
 __global__ __launch_bounds__(64, 1) void step_kernel_queue(KArgs<T> /* read via kernarg ptr */) {
   const KPtr<T> ka = (KPtr<T>)__builtin_amdgcn_kernarg_segment_ptr();
   // this launch's hand-off tag: the epoch only changes after every wave of the launch has left the
   // claim loop (last wave out, below)
-  const int tag = __builtin_amdgcn_readfirstlane(
-      (__hip_atomic_load(ka->b.qsync + QS_EPOCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0x3fffffff) + 1);
+  const uint32_t epoch = __builtin_amdgcn_readfirstlane(
+      __hip_atomic_load(ka->b.qsync + QS_EPOCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const int tag = (int)(epoch & 0x3fffffff) + 1;
   __shared__ Scratch<T, Resident<T>> smem[2];
   PgsCache<T, Resident<T>>* pcache = nullptr;
   if constexpr (PGS) {
     __shared__ PgsCache<T, Resident<T>> pgs_smem[2];
     pcache = &pgs_smem[threadIdx.x >= HL ? 1 : 0];
   }
+  // claim order: prefix sums of the previous launch's bucket counts (qpre[QNB] == npairs: valid)
+  __shared__ int qpre[QNB + 1];
+  {
+    const int npairs = (ka->nenv + 1) / 2, lane = threadIdx.x;
+    int c = (ka->p.qorder && lane < QNB) ? ka->b.qsync[qs_cnt(npairs, epoch & 1) + lane] : 0;
+#pragma unroll
+    for (int d = 1; d < QNB; d <<= 1) {
+      const int y = __shfl_up(c, d);
+      if (lane >= d) c += y;
+    }
+    if (lane < QNB) qpre[lane + 1] = c;
+    if (lane == 0) qpre[0] = 0;
+    WSYNC();
+  }
   for (;;) {
     const KPtr<T> k = opaque(ka);       // nothing uniform kept live across items
     const int nsub = k->p.nsub, npairs = (k->nenv + 1) / 2;
+    int* qs = k->b.qsync;
     int i = 0;
-    if (threadIdx.x == 0) i = atomicAdd(&k->b.qsync[QS_HEAD], 1);
+    if (threadIdx.x == 0) i = atomicAdd(&qs[QS_HEAD], 1);
     i = __builtin_amdgcn_readfirstlane(i);
     if (i >= 2 * npairs) break;
     const bool last = i >= npairs;
-    const int pair = (int)((uint64_t)(last ? i - npairs : i) * (uint32_t)k->p.qmul % (uint32_t)npairs);
+    const int ii = last ? i - npairs : i;
+    int pair;
+    if (qpre[QNB] == npairs) {   // bucket b holds claims [qpre[b], qpre[b + 1])
+      const int lane = opaque_v(threadIdx.x);
+      const bool hit = lane < QNB && qpre[lane] <= ii && ii < qpre[lane + 1];
+      const int b = __builtin_ctzll(__ballot(hit) | (1ull << (QNB - 1)));
+      int p = 0;
+      if (lane == 0) p = qs[qs_ord(npairs, epoch & 1) + (size_t)b * npairs + (ii - qpre[b])];
+      pair = min(max(__builtin_amdgcn_readfirstlane(p), 0), npairs - 1);
+    } else {
+      pair = (int)((uint64_t)ii * (uint32_t)k->p.qmul % (uint32_t)npairs);
+    }
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     step_pair<T, NV, PGS, Resident<T>>(k, smem, pcache, 2 * pair + (opaque_v(threadIdx.x) >= HL ? 1 : 0), k->nenv,
                                        nullptr, last ? nsub - 1 : 0, last ? nsub : nsub - 1, pair, false, tag);
+    // the pair's duration for the next launch's order: the first chunk's is kept in qcost (its
+    // store trails the hand-off, but the last substep reads it ~100 us later; a stale value only
+    // makes the order less exact, never the results different)
+    const uint32_t d = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t0);
+    if (threadIdx.x == 0) {
+      qs = opaque(ka)->b.qsync;
+      if (!last) {
+        qs[qs_cost(npairs) + pair] = (int)d;
+      } else {
+        const uint32_t tot = d + (uint32_t)qs[qs_cost(npairs) + pair];
+        const int b = QNB - 1 - (int)min(tot / (uint32_t)QBIN, (uint32_t)(QNB - 1));
+        const int slot = atomicAdd(&qs[qs_cnt(npairs, (epoch + 1) & 1) + b], 1);
+        qs[qs_ord(npairs, (epoch + 1) & 1) + (size_t)b * npairs + slot] = pair;
+      }
+    }
   }
-  // the last wave out resets the counters and advances the epoch for the next launch (every wave has
-  // made its final claim and read this launch's tag)
+  // the last wave out resets the counters, clears the bucket counts this launch read, and advances
+  // the epoch for the next launch (every wave has made its final claim and read this launch's tag)
   int* qs = ka->b.qsync;
-  if (threadIdx.x == 0 && atomicAdd(&qs[QS_EXIT], 1) == (int)gridDim.x - 1) {
-    qs[QS_HEAD] = 0;
-    qs[QS_EXIT] = 0;
-    atomicAdd(&qs[QS_EPOCH], 1);
+  int lastout = 0;
+  if (threadIdx.x == 0) lastout = atomicAdd(&qs[QS_EXIT], 1) == (int)gridDim.x - 1;
+  if (__builtin_amdgcn_readfirstlane(lastout)) {
+    const int npairs = (ka->nenv + 1) / 2;
+    if (threadIdx.x < QNB) qs[qs_cnt(npairs, epoch & 1) + threadIdx.x] = 0;
+    if (threadIdx.x == 0) {
+      qs[QS_HEAD] = 0;
+      qs[QS_EXIT] = 0;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (threadIdx.x == 0) atomicAdd(&qs[QS_EPOCH], 1);
   }
 }
 
@@ -2428,12 +2481,15 @@ hipError_t launch_step(const DevModel<T>* dmodel, int nv, const EnvBuffers<T>& b
   // engine: 1 wave per SIMD), for multi-substep calls (HS_SCHED_DIRECT: never)
   const int npairs = (nenv + 1) / 2;
   const int resident = resident_waves<T>(p.solver == SOLVER_PGS);
-  args.p.queue = (p.schedule == 0 && b.mid && b.qsync && p.mode != MODE_RESET && p.nsub >= 2 &&
-                  resident > 0 && npairs > resident) ? 1 : 0;
-  // claim order: a fixed multiplicative permutation of the pairs (the same for both chunk kinds, so a
-  // pair's last substep is still claimed npairs items after its first chunk).  Items whose cost is
-  // correlated with the env index -- e.g. env clocks staggered by index, bench.py's window -- are
-  // spread over the launch instead of arriving together at its end.
+  const bool may_queue = p.schedule == SCHED_AUTO || p.schedule == SCHED_FIXED_ORDER;
+  args.p.queue = (may_queue && b.mid && b.qsync && p.mode != MODE_RESET && p.nsub >= 2 && resident > 0 &&
+                  npairs > resident) ? 1 : 0;
+  args.p.qorder = p.schedule == SCHED_AUTO ? 1 : 0;
+  // fallback claim order (first queued launch, SCHED_FIXED_ORDER): a fixed multiplicative
+  // permutation of the pairs (the same for both chunk kinds, so a pair's last substep is still
+  // claimed npairs items after its first chunk).  Items whose cost is correlated with the env index
+  // -- e.g. env clocks staggered by index, bench.py's window -- are spread over the launch instead
+  // of arriving together at its end.
   args.p.qmul = 1;
   if (args.p.queue) {
     auto gcd = [](uint32_t a, uint32_t b) { while (b) { uint32_t t = a % b; a = b; b = t; } return a; };
