@@ -1,6 +1,7 @@
 // hsim C ABI implementation (product).  See include/hsim.h for the reference interfaces replaced.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -30,6 +31,7 @@ struct hs_batch {
   unsigned long long* redo_total = nullptr;  // cumulative wide-tier re-runs
   void* mid = nullptr;                       // chunk-queue hand-off rows [n][MIDDIM] (kernel-managed)
   int* qsync = nullptr;                      // chunk queue claim / exit counters, pair flags (qsync_words)
+  bool newton_rebuild = false;               // HSIM_NEWTON_REBUILD=1 at creation: no incremental factor (A/B)
   hs_env_config cfg{};
   bool ctrl_stale = false;                   // env steps ran with HS_OUT_CTRL off: buf.ctrl is not data.ctrl
   int lose_pair1 = 0;                        // hs_debug_lose_handoff test hook (pair + 1; 0 = off)
@@ -140,6 +142,7 @@ hs::StepParams params_of(const hs_batch* b, int mode, int nsub) {
   p.outputs = b->cfg.outputs;
   p.schedule = b->cfg.schedule;
   p.dbg_lose_pair1 = b->lose_pair1;
+  p.newton_incr = b->newton_rebuild ? 0 : 1;
   return p;
 }
 
@@ -354,8 +357,7 @@ hs_batch* hs_batch_create(const hs_model* m, int n_envs, int device, uint64_t se
       !hip_ok(hipMalloc((void**)&b->redo_total, sizeof(unsigned long long)), "hipMalloc(redo_total)") ||
       // chunk-queue hand-off rows, claim counters and pair flags: UNCACHED device memory from the UC
       // pool above, so a hand-off between waves on different CUs / XCDs needs no L2 write-back or
-      // invalidate (hs_kernels.hip step_pair; a cached version with agent-scope release / acquire
-      // measured 9% slower per fp64 launch: buffer_wbl2 writes back the producer XCD's whole L2)
+      // invalidate (hs_kernels.hip step_pair)
       !(uc_alloc(device, N * hs::MIDDIM * es, &b->mid) ? true
           : (g_err = "hipExtMallocWithFlags(mid, uncached) failed", false)) ||
       !(uc_alloc(device, hs::qsync_words((int)N) * sizeof(int), (void**)&b->qsync) ? true
@@ -363,6 +365,9 @@ hs_batch* hs_batch_create(const hs_model* m, int n_envs, int device, uint64_t se
     hs_batch_destroy(b);
     return nullptr;
   }
+  // HSIM_NEWTON_REBUILD=1: the fp64 Newton rebuilds H every iteration instead of updating its
+  // factor (A/B runs)
+  b->newton_rebuild = getenv("HSIM_NEWTON_REBUILD") && atoi(getenv("HSIM_NEWTON_REBUILD")) != 0;
   ok = precision == HS_FP64 ? init_state<double>(b) : init_state<float>(b);
   if (!ok) { hs_batch_destroy(b); return nullptr; }
   return b;

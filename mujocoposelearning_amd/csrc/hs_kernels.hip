@@ -294,8 +294,10 @@ __device__ __forceinline__ void cross_force(const T* v, const T* f, T* r) {
 // pivot and a_jk (j > k) back as broadcast ds_reads, so the update is pure FMAs:
 //   A_ij -= (a_ik / a_kk) a_jk.
 
-template <int NV, typename T>
-__device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb)[2]) {
+// LDL: return the factor as L D L' instead (unit lower L's strictly lower part in A, dinv = 1/d_i,
+// *diag = d_i): the same elimination, each finished column scaled by its pivot's 1/L_kk on the way.
+template <int NV, typename T, bool LDL = false>
+__device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb)[2], T* diag = nullptr) {
   // two columns per LDS round trip: every lane publishes (a_ik, a_i,k+1) as one ds_write and reads
   // the 2x2 pivot block and (a_jk, a_j,k+1) back as broadcasts.  With L_P the pivot block's
   // Cholesky factor (1/L_kk = r1, L_k+1,k = l10, 1/L_k+1,k+1 = r2), row i gets
@@ -318,9 +320,16 @@ __device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb)[2
     T z1 = (sl_k == k + 1) ? s11 * r2 : (A[k + 1] - l10 * z0) * r2;
     T f1 = z1 * r2;
     T f0 = (z0 - l10 * f1) * r1;
-    A[k] = (sl_k == k) ? p * r1 : z0;
-    A[k + 1] = z1;
-    dinv = (sl_k == k) ? r1 : ((sl_k == k + 1) ? r2 : dinv);
+    if constexpr (LDL) {   // L~_ik = L_ik / L_kk, d = L_kk^2 (the pivots' own entries are zeroed below)
+      A[k] = z0 * r1;
+      A[k + 1] = z1 * r2;
+      dinv = (sl_k == k) ? r1 * r1 : ((sl_k == k + 1) ? r2 * r2 : dinv);
+      *diag = (sl_k == k) ? p : ((sl_k == k + 1) ? s11 : *diag);
+    } else {
+      A[k] = (sl_k == k) ? p * r1 : z0;
+      A[k + 1] = z1;
+      dinv = (sl_k == k) ? r1 : ((sl_k == k + 1) ? r2 : dinv);
+    }
     static_for<k + 2, NV>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
       A[j] = fma(-f0, cb[j][0], fma(-f1, cb[j][1], A[j]));
@@ -334,8 +343,14 @@ __device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb)[2
     T akk = cb[k][0];
     akk = akk > T(1e-30) ? akk : T(1e-30);
     T r = rsqrt_t(akk);
-    A[k] = (sl_k == k) ? akk * r : A[k] * r;
-    dinv = (sl_k == k) ? r : dinv;
+    if constexpr (LDL) {
+      A[k] = A[k] * r * r;
+      dinv = (sl_k == k) ? r * r : dinv;
+      *diag = (sl_k == k) ? akk : *diag;
+    } else {
+      A[k] = (sl_k == k) ? akk * r : A[k] * r;
+      dinv = (sl_k == k) ? r : dinv;
+    }
   }
   const int sl_z = opaque_v(sl);
   static_for<0, NV>([&](auto jc) {
@@ -343,14 +358,49 @@ __device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb)[2
     A[j] = sl_z > j ? A[j] : T(0);
   });
 }
+// Rank-1 update (sgn = +1) or downdate (sgn = -1) of a factor in L D L' form (unit lower L,
+// strictly lower part in A; d_i and 1/d_i on sub-lane i): L D L' + sgn v v' = L~ D~ L~' -- the
+// fp64 Newton's incremental Hessian, as MuJoCo's mju_cholUpdate -- by Gill, Golub, Murray and
+// Saunders' method C1 (no square roots):
+//   p = v_k,  d~_k = d_k + a p^2,  b = a p / d~_k,  a <- a d_k / d~_k;
+//   v_i <- v_i - p L_ik,  L~_ik = L_ik + b v_i          (i > k; a starts at sgn).
+// The chain from column to column is one broadcast of p and one FMA (v), plus the scalar a-chain
+// (one reciprocal); the L~ updates hang off it.  `on` false leaves the half's factor untouched.
+// Returns false on a half whose downdate cancelled more than 3 digits of a pivot (d~_k < 1e-3 d_k):
+// that half's factor is then rebuilt from H.
+template <int NV, typename T>
+__device__ __forceinline__ bool ldl_rank1(T (&A)[NV], T& d, T& dinv, T v, T sgn, bool on, int sl) {
+  bool ok = true;
+  T a = sgn;
+  static_for<0, NV>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    const int sl_k = opaque_v(sl);
+    const T p = bcast<k>(v), dk = bcast<k>(d);
+    const T ap = a * p;
+    const T dn = fma(ap, p, dk);
+    ok = ok && dn > T(1e-3) * dk;
+    const T rdn = recip(dn);
+    const T beta = ap * rdn;
+    a = a * dk * rdn;
+    const T vn = fma(-p, A[k], v);
+    const T ln = fma(beta, vn, A[k]);
+    const bool below = on && sl_k > k, piv = on && sl_k == k;
+    A[k] = below ? ln : A[k];
+    v = below ? vn : v;
+    d = piv ? dn : d;
+    dinv = piv ? rdn : dinv;
+  });
+  return ok || !on;
+}
 // solve (L L') x = b (L from chol_rows: strictly lower part, 1/L_ii in dinv); sub-lane i holds b_i;
 // returns x_i.  Forward: at step k every lane subtracts L_ik y_k (zero unless i > k), so lane k's b
 // stops changing once y_k = b_k / L_kk is broadcast, and y = b / L_ii at the end.
-template <int NV, typename T>
+// UNIT: L D L' form instead (unit lower L, 1/d_i in dinv): forward with L, scale by 1/d, back with L'.
+template <int NV, typename T, bool UNIT = false>
 __device__ __forceinline__ T chol_solve(const T (&L)[NV], T dinv, T b, int sl) {
   static_for<0, NV - 1>([&](auto kc) {      // column NV - 1 has no row below it: skipped
     constexpr int k = decltype(kc)::value;
-    b = fma(-L[k], bcast<k>(b * dinv), b);
+    b = fma(-L[k], bcast<k>(UNIT ? b : b * dinv), b);
   });
   b *= dinv;
   // back substitution x_k = (y_k - sum_{i>k} L_ik x_i) / L_kk in blocks of BS columns, top block
@@ -369,7 +419,7 @@ __device__ __forceinline__ T chol_solve(const T (&L)[NV], T dinv, T b, int sl) {
     });
     static_for<0, hi - lo>([&](auto tc) {
       constexpr int c = hi - 1 - decltype(tc)::value;         // top of the block down
-      T xc = (b - ssum[c - lo]) * dinv;                      // lane c's value is x_c
+      T xc = UNIT ? b - ssum[c - lo] : (b - ssum[c - lo]) * dinv;   // lane c's value is x_c
       x = (sl_k == c) ? xc : x;
       static_for<lo, c>([&](auto dc) {                       // lane c's L_cd x_c to the block's lanes d < c
         constexpr int d = decltype(dc)::value;
@@ -411,6 +461,8 @@ __device__ __forceinline__ T matvec_lds(const T (&A)[NV], const T* v) {
 }
 
 // ------------------------------------------------------------------ per-env LDS scratch
+// dofs of the kernel instance whose Newton factor fits the LDS union (launch_step: nv == 27)
+constexpr int FACNV = 27;
 enum RowKind { RK_JLO = 0, RK_JHI = 1, RK_TLO = 2, RK_THI = 3, RK_CN = 4, RK_P0 = 5 };   // P0..P0+3: pyramid
 __device__ __forceinline__ int rk_kind(int kid) { return kid >> 16; }
 __device__ __forceinline__ int rk_id(int kid) { return kid & 0xffff; }
@@ -446,15 +498,22 @@ struct Scratch {
   T row_f[C::EFC];
   int ncon, nefc, nlim, njl;   // njl: joint-limit rows (tendon rows are [njl, nlim))
   int niter;                   // this env's Newton iterations (the wave's loop runs for the slower env)
+  struct Kin { T xpos[MAXBODY][3]; T xmat[MAXBODY][9]; T xquat[MAXBODY][4]; T xanchor[MAXJNT][3];
+               T xaxis[MAXJNT][3]; T gpos[MAXGEOM][3]; T gax[MAXGEOM][3]; };
+  // the fp64 Newton's L D L' factor between iterations (Stepper::factor_update): row i's unit-lower
+  // entries packed at [i (i - 1) / 2, i (i + 1) / 2), then d[FACNV], 1/d[FACNV].  It aliases the
+  // full-state arrays of `n` (written only after the solve) and the union's slack: no extra LDS.
+  struct Fac { T bvel[MAXBODY][6]; alignas(16) T cb[MAXDOF][2]; T fac[FACNV * (FACNV - 1) / 2 + 2 * FACNV]; };
   union {   // phase-local arrays (aliased)
-    struct { T xpos[MAXBODY][3]; T xmat[MAXBODY][9]; T xquat[MAXBODY][4]; T xanchor[MAXJNT][3];
-             T xaxis[MAXJNT][3]; T gpos[MAXGEOM][3]; T gax[MAXGEOM][3]; } k;   // kinematics + collision
+    Kin k;                                                        // kinematics + collision
     struct { T crb[MAXBODY][10]; T buf[MAXDOF][6]; } c;          // composite rigid body
     struct { T cdofdot[MAXDOF][6]; T cfrc[MAXBODY][6]; T csub[MAXBODY][6]; } r;   // RNE
     struct { T bvel[MAXBODY][6];                                  // J x mapping (rows, Newton)
-             T cfrc[MAXBODY][6], linv[MAXBODY][3], mv[MAXBODY][3];    // full_state (after solve)
-             alignas(16) T cb[MAXDOF][2]; } n;                       // Cholesky column pairs
+             alignas(16) T cb[MAXDOF][2];                         // Cholesky column pairs
+             T cfrc[MAXBODY][6], linv[MAXBODY][3], mv[MAXBODY][3]; } n;   // full_state (after solve)
+    Fac nf;
   } u;
+  static_assert(sizeof(Fac) <= sizeof(Kin), "the Newton factor slot must fit the union without growing it");
 };
 
 // PGS solver scratch (the <option solver="PGS"> kernel instance only; the Newton instance never
@@ -778,7 +837,7 @@ __device__ __forceinline__ T jtf_lane(MPtr<T> m, const Scratch<T, C>& s, int sl,
 // Built only with -DHS_TIMING (libhsim_timing.so): s_memtime stamps accumulated per phase,
 // summed over waves into dbg[8000 + slot].  The product build compiles them out.
 #ifdef HS_TIMING
-constexpr int NSLOT = 26;
+constexpr int NSLOT = 27;
 struct PhaseClock {
   uint64_t acc[NSLOT] = {0};
   uint64_t prev = 0, t0 = 0, rt0 = 0;   // rt0: s_memrealtime (100 MHz, one clock for all XCDs)
@@ -843,6 +902,25 @@ struct Stepper {
 
   __device__ Stepper(MPtr<T> mm, Scratch<T, C>& ss, int lane)
       : m(mm), s(ss), sl(lane & (HL - 1)), nb(mm->nbody), up(lane >= HL) {}
+
+  // Incremental factor (development build -DHS_NEWTON_INCR, fp64 only): Newton iterations after the
+  // first update the previous iteration's L D L' factor by rank-1 terms for the rows whose active
+  // state changed (at most NUPD per half; factor_update) instead of rebuilding H and factoring it,
+  // as MuJoCo's Newton does.  Measured slower on MI355X and left out of the product (DESIGN.md 3.2:
+  // the updates are serial 27-column chains, and the extra live state costs the queue kernel its
+  // last registers).
+#ifdef HS_NEWTON_INCR
+  static constexpr bool INCR = sizeof(T) == 8 && NV <= FACNV;
+#else
+  static constexpr bool INCR = false;
+#endif
+#ifndef HS_NUPD
+  static constexpr int NUPD = 4;
+#else
+  static constexpr int NUPD = HS_NUPD;
+#endif
+  // the launch arguments (every step-kernel instance takes its KArgs at kernarg offset 0)
+  __device__ __forceinline__ static KPtr<T> kargs() { return (KPtr<T>)__builtin_amdgcn_kernarg_segment_ptr(); }
 
   // start of a pipeline phase: nothing lane-invariant is carried over from the previous phase
   __device__ __forceinline__ void phase_begin() {
@@ -1343,6 +1421,7 @@ struct Stepper {
     HS_STAMP(clk, 6);
     bool done = false;      // this half-wave's solver has converged
     int it = 0;
+    int fmask = 0;          // (INCR) rows q = 0..RPL-1 of this lane active in the saved factor
     if (sl == 0) s.niter = maxit;   // per env: the iteration at which this half converged
     for (; it < maxit; it++) {
       m = opaque(m);
@@ -1364,8 +1443,15 @@ struct Stepper {
       done = done || conv;
       HS_STAMP(clk, 8);
       if (__ballot(!done) == 0) break;       // both envs of the wave converged
-      // Hessian lower rows: M + contact (tree form) + joint limits (diag) + dense rank-1 rows
       T H[NV];
+      T hdinv = 0, hdiag = 0;
+      bool full = true;     // this half builds H and factors it (else: its saved factor, updated)
+      if constexpr (INCR) {
+        if (it > 0 && opaque(kargs())->p.newton_incr) full = !factor_update(H, hdiag, hdinv, act, vr, fmask);
+        HS_STAMP(clk, 26);
+      }
+      if (full) {
+      // Hessian lower rows: M + contact (tree form) + joint limits (diag) + dense rank-1 rows
       {
         T aug[6] = {0, 0, 0, 0, 0, 0};
         T dadd = 0;
@@ -1440,10 +1526,16 @@ struct Stepper {
         }
       }
       HS_STAMP(clk, 9);
-      T hdinv = 0;
-      chol_rows<NV>(H, hdinv, sl, s.u.n.cb);
+      chol_rows<NV, T, INCR>(H, hdinv, sl, s.u.n.cb, &hdiag);   // (INCR: as L D L')
       HS_STAMP(clk, 15);
-      T sdir = -chol_solve<NV>(H, hdinv, g, sl);
+      }
+      T sdir = -chol_solve<NV, T, INCR>(H, hdinv, g, sl);
+      if constexpr (INCR) {   // the factor and its active set, for the next iteration's update
+        fmask = 0;
+#pragma unroll
+        for (int q = 0; q < C::RPL; q++) fmask |= act[q] ? (1 << q) : 0;
+        fac_store(H, hdiag, hdinv);
+      }
       if (sl >= NV) sdir = 0;
       HS_STAMP(clk, 10);
       // exact line search along sdir (piecewise-quadratic cost)
@@ -1526,6 +1618,77 @@ struct Stepper {
     qacc = x;
     WSYNC();
     HS_STAMP(clk, 12);
+  }
+
+  // Incremental factor (fp64 Newton, iterations after the first; MuJoCo's Newton updates its
+  // Cholesky factor the same way, mju_cholUpdate): this half's L D L' factor of the previous
+  // iteration, saved in LDS (fac_store), updated by sqrt(D_r) J_r for every row r whose active state
+  // changed since it was factored -- rows that became active first (updates), then rows that left
+  // (downdates).  Returns false on a half with more than NUPD changed rows or a failed downdate:
+  // that half rebuilds H and factors it instead.
+  __device__ __forceinline__ bool factor_update(T (&H)[NV], T& hdiag, T& hdinv, const bool (&act)[C::RPL],
+                                                const bool (&vr)[C::RPL], int fmask) {
+    uint32_t ad[C::RPL], rm[C::RPL];
+    int cnt = 0;
+#pragma unroll
+    for (int q = 0; q < C::RPL; q++) {
+      const bool f = (fmask >> q) & 1;
+      ad[q] = hballot(act[q] && !f, up);
+      rm[q] = hballot(vr[q] && !act[q] && f, up);
+      cnt += __popc(ad[q]) + __popc(rm[q]);
+    }
+    const bool inc = cnt <= NUPD;
+    if (__ballot(inc) == 0) return false;
+    fac_load(H, hdiag, hdinv);
+    bool ok = true;
+    for (;;) {   // max(changed rows of either half) rounds, wave-uniform control
+      int r = -1;
+      bool add = false;
+#pragma unroll
+      for (int q = C::RPL - 1; q >= 0; q--)
+        if (rm[q]) r = HL * q + __builtin_ctz(rm[q]);
+#pragma unroll
+      for (int q = C::RPL - 1; q >= 0; q--)
+        if (ad[q]) { r = HL * q + __builtin_ctz(ad[q]); add = true; }
+      if (!inc) r = -1;
+      if (__ballot(r >= 0) == 0) break;
+      T v = 0;
+      if (r >= 0) {
+#pragma unroll
+        for (int q = 0; q < C::RPL; q++) {   // consume the row
+          if (q == r / HL) {
+            if (add) ad[q] &= ad[q] - 1u;
+            else rm[q] &= rm[q] - 1u;
+          }
+        }
+        v = sqrt(s.row_D[r]) * row_J_lane(r);
+      }
+      ok = ldl_rank1<NV>(H, hdiag, hdinv, v, add ? T(1) : T(-1), r >= 0, sl) && ok;
+    }
+    return inc && ok;
+  }
+  // the factor between Newton iterations: row sl's unit-lower entries packed in LDS (Scratch::Fac)
+  __device__ __forceinline__ void fac_store(const T (&H)[NV], T d, T dinv) {
+    T* f = s.u.nf.fac;
+    const int i = opaque_v(sl), base = i * (i - 1) / 2;
+    static_for<0, NV - 1>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      if (j < i && i < NV) f[base + j] = H[j];
+    });
+    if (i < NV) {
+      f[FACNV * (FACNV - 1) / 2 + i] = d;
+      f[FACNV * (FACNV - 1) / 2 + FACNV + i] = dinv;
+    }
+  }
+  __device__ __forceinline__ void fac_load(T (&H)[NV], T& d, T& dinv) {
+    const T* f = s.u.nf.fac;
+    const int i = opaque_v(sl), base = i * (i - 1) / 2;
+    static_for<0, NV>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      H[j] = (j < i && i < NV) ? f[base + j] : T(0);
+    });
+    d = i < NV ? f[FACNV * (FACNV - 1) / 2 + i] : T(1);
+    dinv = i < NV ? f[FACNV * (FACNV - 1) / 2 + FACNV + i] : T(1);
   }
 
   // lane (dof) j's entry of constraint row r's Jacobian (the same per-row Jacobians row_Jx applies

@@ -16,7 +16,7 @@ NAMES = ["load", "kinematics", "mass_matrix", "vel+rne", "collision", "rows+aref
          "newton:rowf+aggr", "newton:gradient", "newton:hessian", "newton:solve", "newton:ls loop",
          "newton:final frc", "euler:integrate", "obs+writeback", "newton:chol", "newton:ls J s rows",
          "euler:solve", "newton:ls M s", "newton:ls map_vx", "euler:pre", "euler:chol", "pre-obs (loop top)",
-         "obs write", "step_count/energy sum", "reward"]
+         "obs write", "step_count/energy sum", "reward", "newton:factor update"]
 NS = len(NAMES)
 
 
