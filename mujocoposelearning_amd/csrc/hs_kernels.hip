@@ -55,6 +55,16 @@ using Wide = Cap<MAXCON_WIDE, MAXEFC_WIDE, true>;
 // scheduling fence: keeps the machine scheduler from hoisting loads across iterations of fully
 // unrolled loops (which otherwise inflates VGPR pressure far past the occupancy target)
 #define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+// per-loop scheduling fences (development A/B knobs; 1 = fenced)
+#ifndef HS_FENCE_CHOL
+#define HS_FENCE_CHOL 1
+#endif
+#ifndef HS_FENCE_CRB
+#define HS_FENCE_CRB 1
+#endif
+#ifndef HS_FENCE_HESS
+#define HS_FENCE_HESS 1
+#endif
 
 // single-wave workgroup: LDS ops of a wave execute in order, so a compiler-only barrier suffices to
 // keep LDS accesses from moving across phase boundaries (no s_barrier, and no s_waitcnt that a
@@ -334,7 +344,7 @@ __device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb)[2
       constexpr int j = decltype(jc)::value;
       A[j] = fma(-f0, cb[j][0], fma(-f1, cb[j][1], A[j]));
     });
-    SCHED_FENCE();
+    if constexpr (HS_FENCE_CHOL == 1 || (HS_FENCE_CHOL == 2 && (k / 2) % 2 == 1)) SCHED_FENCE();
   });
   if constexpr (NV % 2 == 1) {         // trailing single column
     constexpr int k = NV - 1;
@@ -914,6 +924,19 @@ struct Stepper {
 #else
   static constexpr bool INCR = false;
 #endif
+  // the Newton factor as L D L' (unit lower L): the same elimination, but the triangular solves lose
+  // one dependent multiply per column (fp64 0.740 -> 0.731 ms per configs[1] launch; the Euler
+  // factorization and the fp32 engine measured the same either way and stay L L').
+  // HS_NEWTON_LDL: bit 0 the fp32 engine, bit 1 the fp64 engine.
+#ifndef HS_NEWTON_LDL
+#define HS_NEWTON_LDL 2
+#endif
+  static constexpr bool LDLF = INCR || ((sizeof(T) == 8 ? 2 : 1) & HS_NEWTON_LDL) != 0;
+#ifdef HS_EULER_LDL
+  static constexpr bool LDLE = true;
+#else
+  static constexpr bool LDLE = false;
+#endif
 #ifndef HS_NUPD
   static constexpr int NUPD = 4;
 #else
@@ -1172,7 +1195,7 @@ struct Stepper {
       for (int k = 0; k < 6; k++) { cj[k] = s.cdof[j][k]; bj[k] = s.u.c.buf[j][k]; }
       T v = (j <= sl) ? dot6(cj, bf) : dot6(cd, bj);
       Mr[j] = rel ? v + ((j == sl) ? arm : T(0)) : T(0);
-      SCHED_FENCE();
+      if constexpr (HS_FENCE_CRB) SCHED_FENCE();
     }
     WSYNC();
   }
@@ -1480,7 +1503,7 @@ struct Stepper {
           T cj[6];
           for (int k = 0; k < 6; k++) cj[k] = s.cdof[j][k];
           H[j] = Mr[j] + (bit(anci, j) ? dot6(cj, aug) : T(0)) + ((j == sl) ? dadd : T(0));
-          SCHED_FENCE();
+          if constexpr (HS_FENCE_HESS) SCHED_FENCE();
         }
         // dense rank-1 rows (tendon limits, body-body contacts): only the rows flagged in
         // dense_mask; the loop runs max(#rows of either half) times (wave-uniform control)
@@ -1526,10 +1549,10 @@ struct Stepper {
         }
       }
       HS_STAMP(clk, 9);
-      chol_rows<NV, T, INCR>(H, hdinv, sl, s.u.n.cb, &hdiag);   // (INCR: as L D L')
+      chol_rows<NV, T, LDLF>(H, hdinv, sl, s.u.n.cb, &hdiag);   // (LDLF: as L D L')
       HS_STAMP(clk, 15);
       }
-      T sdir = -chol_solve<NV, T, INCR>(H, hdinv, g, sl);
+      T sdir = -chol_solve<NV, T, LDLF>(H, hdinv, g, sl);
       if constexpr (INCR) {   // the factor and its active set, for the next iteration's update
         fmask = 0;
 #pragma unroll
@@ -1976,10 +1999,10 @@ struct Stepper {
 #pragma unroll
     for (int j = 0; j < NV; j++) He[j] = Mr[j] + ((j == sl) ? h * damp : T(0));
     HS_STAMP(clk, 20);
-    T edinv = 0;
-    chol_rows<NV>(He, edinv, sl, s.u.n.cb);
+    T edinv = 0, ediag = 0;
+    chol_rows<NV, T, LDLE>(He, edinv, sl, s.u.n.cb, &ediag);
     HS_STAMP(clk, 21);
-    T a = chol_solve<NV>(He, edinv, fsmooth + fcon, sl);
+    T a = chol_solve<NV, T, LDLE>(He, edinv, fsmooth + fcon, sl);
     HS_STAMP(clk, 17);
     if (sl < NV) s.qvel[sl] += h * a;
     WSYNC();
