@@ -352,12 +352,13 @@ __device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb)[2
     cb[sl_k][0] = A[k];
     T akk = cb[k][0];
     akk = akk > T(1e-30) ? akk : T(1e-30);
-    T r = rsqrt_t(akk);
     if constexpr (LDL) {
+      const T r = rsqrt_t(akk);
       A[k] = A[k] * r * r;
       dinv = (sl_k == k) ? r * r : dinv;
       *diag = (sl_k == k) ? akk : *diag;
     } else {
+      const T r = rsqrt_t(akk);
       A[k] = (sl_k == k) ? akk * r : A[k] * r;
       dinv = (sl_k == k) ? r : dinv;
     }
@@ -416,7 +417,13 @@ __device__ __forceinline__ T chol_solve(const T (&L)[NV], T dinv, T b, int sl) {
   // back substitution x_k = (y_k - sum_{i>k} L_ik x_i) / L_kk in blocks of BS columns, top block
   // first: the sums over the rows below the block are BS independent half-wave sums (their latencies
   // overlap), the block's own rows follow as a short chain of broadcasts of L_ik x_i from lane i
-  constexpr int BS = 3;
+  // (block size A/B, fp64 configs[1] ms per launch: BS 1 0.726, 2 0.728, 3 0.731, 4 0.738,
+  // 5 0.747; fp32: BS 2 0.424 vs 3 0.426, BS 1 within noise of 2)
+#ifndef HS_SOLVE_BS
+  constexpr int BS = sizeof(T) == 8 ? 1 : 2;
+#else
+  constexpr int BS = HS_SOLVE_BS;
+#endif
   T x = 0;
   static_for<0, (NV + BS - 1) / BS>([&](auto bc) {
     constexpr int hi = NV - BS * decltype(bc)::value;        // block = columns [lo, hi)
