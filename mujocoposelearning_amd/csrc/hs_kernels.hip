@@ -65,6 +65,13 @@ using Wide = Cap<MAXCON_WIDE, MAXEFC_WIDE, true>;
 #ifndef HS_FENCE_HESS
 #define HS_FENCE_HESS 1
 #endif
+// columns per scheduling group in the Hessian / CRB row loops (A/B, fp64 configs[1] ms per launch:
+// Hessian 2 columns 0.720 vs 1 column 0.724, 3 spill; CRB 2 or 3 columns: no change)
+// (the fp32 engine at 2 waves per SIMD has no registers for a second column: 148 B/lane of scratch)
+#ifndef HS_CRB_G
+#define HS_CRB_G 1
+#endif
+constexpr int CRB_G = HS_CRB_G;
 
 // single-wave workgroup: LDS ops of a wave execute in order, so a compiler-only barrier suffices to
 // keep LDS accesses from moving across phase boundaries (no s_barrier, and no s_waitcnt that a
@@ -854,7 +861,7 @@ __device__ __forceinline__ T jtf_lane(MPtr<T> m, const Scratch<T, C>& s, int sl,
 // Built only with -DHS_TIMING (libhsim_timing.so): s_memtime stamps accumulated per phase,
 // summed over waves into dbg[8000 + slot].  The product build compiles them out.
 #ifdef HS_TIMING
-constexpr int NSLOT = 27;
+constexpr int NSLOT = 29;
 struct PhaseClock {
   uint64_t acc[NSLOT] = {0};
   uint64_t prev = 0, t0 = 0, rt0 = 0;   // rt0: s_memrealtime (100 MHz, one clock for all XCDs)
@@ -1194,16 +1201,37 @@ struct Stepper {
       arm = m->dof_armature[sl];
     }
     WSYNC();
+    // CRB_G columns per scheduling group (one exposed LDS round trip per group, as in the Hessian)
+    if constexpr (CRB_G == 1) {
 #pragma unroll
-    for (int j = 0; j < NV; j++) {
-      uint32_t ancj = m->dof_ancmask[j];
-      bool rel = (sl < NV) && (bit(anci, j) || bit(ancj, sl));
-      T cj[6], bj[6];
-      for (int k = 0; k < 6; k++) { cj[k] = s.cdof[j][k]; bj[k] = s.u.c.buf[j][k]; }
-      T v = (j <= sl) ? dot6(cj, bf) : dot6(cd, bj);
-      Mr[j] = rel ? v + ((j == sl) ? arm : T(0)) : T(0);
+      for (int j = 0; j < NV; j++) {
+        uint32_t ancj = m->dof_ancmask[j];
+        bool rel = (sl < NV) && (bit(anci, j) || bit(ancj, sl));
+        T cj[6], bj[6];
+        for (int k = 0; k < 6; k++) { cj[k] = s.cdof[j][k]; bj[k] = s.u.c.buf[j][k]; }
+        T v = (j <= sl) ? dot6(cj, bf) : dot6(cd, bj);
+        Mr[j] = rel ? v + ((j == sl) ? arm : T(0)) : T(0);
+        if constexpr (HS_FENCE_CRB) SCHED_FENCE();
+      }
+    } else static_for<0, (NV + CRB_G - 1) / CRB_G>([&](auto gc) {
+      constexpr int j0 = decltype(gc)::value * CRB_G;
+      T cj[CRB_G][6], bj[CRB_G][6];
+      static_for<0, CRB_G>([&](auto tc) {
+        constexpr int t = decltype(tc)::value;
+        if constexpr (j0 + t < NV)
+          for (int k = 0; k < 6; k++) { cj[t][k] = s.cdof[j0 + t][k]; bj[t][k] = s.u.c.buf[j0 + t][k]; }
+      });
+      static_for<0, CRB_G>([&](auto tc) {
+        constexpr int t = decltype(tc)::value, j = j0 + t;
+        if constexpr (j < NV) {
+          const uint32_t ancj = m->dof_ancmask[j];
+          const bool rel = (sl < NV) && (bit(anci, j) || bit(ancj, sl));
+          const T v = (j <= sl) ? dot6(cj[t], bf) : dot6(cd, bj[t]);
+          Mr[j] = rel ? v + ((j == sl) ? arm : T(0)) : T(0);
+        }
+      });
       if constexpr (HS_FENCE_CRB) SCHED_FENCE();
-    }
+    });
     WSYNC();
   }
 
@@ -1505,13 +1533,37 @@ struct Stepper {
           if (lo >= 0 && s.row_f[lo] != T(0)) dadd += s.row_D[lo];
           if (hi >= 0 && s.row_f[hi] != T(0)) dadd += s.row_D[hi];
         }
+        HS_STAMP(clk, 27);
+        // HESS_G columns per scheduling group: their cdof rows are read from LDS together, so one
+        // LDS round trip is exposed per group instead of per column
+#ifdef HS_HESS_G
+        constexpr int HESS_G = HS_HESS_G;
+#else
+        constexpr int HESS_G = sizeof(T) == 8 ? 2 : 1;
+#endif
+        if constexpr (HESS_G == 1) {
 #pragma unroll
-        for (int j = 0; j < NV; j++) {
-          T cj[6];
-          for (int k = 0; k < 6; k++) cj[k] = s.cdof[j][k];
-          H[j] = Mr[j] + (bit(anci, j) ? dot6(cj, aug) : T(0)) + ((j == sl) ? dadd : T(0));
+          for (int j = 0; j < NV; j++) {
+            T cj[6];
+            for (int k = 0; k < 6; k++) cj[k] = s.cdof[j][k];
+            H[j] = Mr[j] + (bit(anci, j) ? dot6(cj, aug) : T(0)) + ((j == sl) ? dadd : T(0));
+            if constexpr (HS_FENCE_HESS) SCHED_FENCE();
+          }
+        } else static_for<0, (NV + HESS_G - 1) / HESS_G>([&](auto gc) {
+          constexpr int j0 = decltype(gc)::value * HESS_G;
+          T cj[HESS_G][6];
+          static_for<0, HESS_G>([&](auto tc) {
+            constexpr int t = decltype(tc)::value;
+            if constexpr (j0 + t < NV)
+              for (int k = 0; k < 6; k++) cj[t][k] = s.cdof[j0 + t][k];
+          });
+          static_for<0, HESS_G>([&](auto tc) {
+            constexpr int t = decltype(tc)::value, j = j0 + t;
+            if constexpr (j < NV) H[j] = Mr[j] + (bit(anci, j) ? dot6(cj[t], aug) : T(0)) + ((j == sl) ? dadd : T(0));
+          });
           if constexpr (HS_FENCE_HESS) SCHED_FENCE();
-        }
+        });
+        HS_STAMP(clk, 28);
         // dense rank-1 rows (tendon limits, body-body contacts): only the rows flagged in
         // dense_mask; the loop runs max(#rows of either half) times (wave-uniform control)
         uint32_t dm[C::RPL];

@@ -13,10 +13,10 @@ from mujocoposelearning_amd.batch import HsBatch  # noqa: E402
 from mujocoposelearning_amd.model import HsModel  # noqa: E402
 
 NAMES = ["load", "kinematics", "mass_matrix", "vel+rne", "collision", "rows+aref", "newton:init Jx",
-         "newton:rowf+aggr", "newton:gradient", "newton:hessian", "newton:solve", "newton:ls loop",
+         "newton:rowf+aggr", "newton:gradient", "newton:hess dense rows", "newton:solve", "newton:ls loop",
          "newton:final frc", "euler:integrate", "obs+writeback", "newton:chol", "newton:ls J s rows",
          "euler:solve", "newton:ls M s", "newton:ls map_vx", "euler:pre", "euler:chol", "pre-obs (loop top)",
-         "obs write", "step_count/energy sum", "reward", "newton:factor update"]
+         "obs write", "step_count/energy sum", "reward", "newton:factor update", "newton:hess contacts", "newton:hess M+tree rows"]
 NS = len(NAMES)
 
 
