@@ -55,6 +55,21 @@ using Wide = Cap<MAXCON_WIDE, MAXEFC_WIDE, true>;
 // scheduling fence: keeps the machine scheduler from hoisting loads across iterations of fully
 // unrolled loops (which otherwise inflates VGPR pressure far past the occupancy target)
 #define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+// Cholesky pivot block by DPP broadcast instead of LDS read-back, per precision (bit 0 the fp32
+// engine, bit 1 the fp64 engine).  A/B, ms per configs[1] launch: fp64 0.720 -> 0.714 (with the
+// normal-range sqrt below 0.701); fp32 0.423 -> 0.433 (2 waves per SIMD hide the LDS round trip,
+// and the extra VALU ops cost issue slots): fp64 only.
+#ifndef HS_CHOL_DPP
+#define HS_CHOL_DPP 2
+#endif
+// fp64 1/sqrt without the denormal / class handling of the library sqrt (development A/B knob)
+#ifndef HS_SQRT_FAST
+#define HS_SQRT_FAST 2
+#endif
+// M·v with two accumulators (development A/B knob)
+#ifndef HS_MATVEC_SPLIT
+#define HS_MATVEC_SPLIT 0
+#endif
 // per-loop scheduling fences (development A/B knobs; 1 = fenced)
 #ifndef HS_FENCE_CHOL
 #define HS_FENCE_CHOL 1
@@ -254,12 +269,50 @@ __device__ __forceinline__ double recip(double x) {
   e = fma(-x, y, 1.0);
   return fma(y, e, y);
 }
-// fp64 1/sqrt(x): the exact sqrt, then recip() instead of the IEEE divide sequence (within ~1 ulp of
-// the correctly rounded value; fewer dependent ops on the Cholesky pivots' chain: 0.900 -> 0.890 ms
-// per fp64 launch).  (Measured alternative: v_rsq_f64 + two Newton steps in place of the sqrt is
-// SLOWER -- 305k vs 298k cycles per env substep.)
+// fp64 1/sqrt(x), x >= 1e-30 at every call site (the Cholesky pivots are clamped to it, the
+// normalizations branch below it), so no denormal scaling or zero / infinity class check:
+//   HS_SQRT_FAST 2 (product): v_rsq_f64, one Goldschmidt step (h ~ 1/(2 sqrt x)), one Newton step on
+//     y = 2h -- within ~1 ulp, 7 dependent operations;
+//   1: the library's sqrt sequence without its scaling / class check, then recip() (13);
+//   0: recip(sqrt(x)) (18).
+// A/B, fp64 ms per configs[1] launch (with the DPP pivots of chol_rows): 0 0.714, 1 0.701, 2 0.690.
+// (Round 2 measured a v_rsq_f64 + two-Newton-step variant slower, 305k vs 298k cycles per env
+// substep, under the default machine scheduler.)
+#if HS_SQRT_FAST
+// sqrt for x in the normal range (every caller clamps x >= 1e-30): the compiler's sqrt sequence
+// (v_rsq_f64, one Goldschmidt step, two Newton corrections) without its denormal scaling and its
+// zero / infinity class check -- the same arithmetic for these x, five fewer dependent operations
+__device__ __forceinline__ double sqrt_normal(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = 0.5 * y;
+  const double r = fma(-h, g, 0.5);
+  g = fma(g, r, g);
+  h = fma(h, r, h);
+  double d = fma(-g, g, x);
+  g = fma(d, h, g);
+  d = fma(-g, g, x);
+  return fma(d, h, g);
+}
+#if HS_SQRT_FAST >= 2
+// 1/sqrt(x) directly: v_rsq_f64, one Goldschmidt step (h ~ 1/(2 sqrt x)), one Newton step on y = 2h
+template <>
+__device__ __forceinline__ double rsqrt_t<double>(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y, h = 0.5 * y;
+  const double r = fma(-h, g, 0.5);
+  h = fma(h, r, h);
+  const double y1 = h + h;
+  const double e = fma(-(x * y1), y1, 1.0);
+  return fma(h, e, y1);
+}
+#else
+template <>
+__device__ __forceinline__ double rsqrt_t<double>(double x) { return recip(sqrt_normal(x)); }
+#endif
+#else
 template <>
 __device__ __forceinline__ double rsqrt_t<double>(double x) { return recip(sqrt(x)); }
+#endif
 template <typename T>
 __device__ __forceinline__ T normalize3(T* v) {
   const T n2 = dot3(v, v);
@@ -315,6 +368,7 @@ __device__ __forceinline__ void cross_force(const T* v, const T* f, T* r) {
 // *diag = d_i): the same elimination, each finished column scaled by its pivot's 1/L_kk on the way.
 template <int NV, typename T, bool LDL = false>
 __device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb)[2], T* diag = nullptr) {
+  constexpr bool CDPP = (HS_CHOL_DPP & (sizeof(T) == 8 ? 2 : 1)) != 0;
   // two columns per LDS round trip: every lane publishes (a_ik, a_i,k+1) as one ds_write and reads
   // the 2x2 pivot block and (a_jk, a_j,k+1) back as broadcasts.  With L_P the pivot block's
   // Cholesky factor (1/L_kk = r1, L_k+1,k = l10, 1/L_k+1,k+1 = r2), row i gets
@@ -326,7 +380,16 @@ __device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb)[2
     const int sl_k = opaque_v(sl);     // fresh compare per step (no 64-bit mask kept live)
     cb[sl_k][0] = A[k];
     cb[sl_k][1] = A[k + 1];
-    T p = cb[k][0], q = cb[k + 1][0], t = cb[k + 1][1];
+    T p, q, t;
+    if constexpr (CDPP) {   // the pivot block by DPP broadcast from lanes k, k+1: the LDS round trip
+      p = bcast<k>(A[k]);   // of the column publish leaves the pivot chain (the trailing update still
+      q = bcast<k + 1>(A[k]);   // reads a_jk from LDS)
+      t = bcast<k + 1>(A[k + 1]);
+    } else {
+      p = cb[k][0];
+      q = cb[k + 1][0];
+      t = cb[k + 1][1];
+    }
     p = p > T(1e-30) ? p : T(1e-30);
     T r1 = rsqrt_t(p);
     T l10 = q * r1;
@@ -356,8 +419,13 @@ __device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb)[2
   if constexpr (NV % 2 == 1) {         // trailing single column
     constexpr int k = NV - 1;
     const int sl_k = opaque_v(sl);
-    cb[sl_k][0] = A[k];
-    T akk = cb[k][0];
+    T akk;
+    if constexpr (CDPP) {
+      akk = bcast<k>(A[k]);
+    } else {
+      cb[sl_k][0] = A[k];
+      akk = cb[k][0];
+    }
     akk = akk > T(1e-30) ? akk : T(1e-30);
     if constexpr (LDL) {
       const T r = rsqrt_t(akk);
@@ -414,13 +482,37 @@ __device__ __forceinline__ bool ldl_rank1(T (&A)[NV], T& d, T& dinv, T v, T sgn,
 // returns x_i.  Forward: at step k every lane subtracts L_ik y_k (zero unless i > k), so lane k's b
 // stops changing once y_k = b_k / L_kk is broadcast, and y = b / L_ii at the end.
 // UNIT: L D L' form instead (unit lower L, 1/d_i in dinv): forward with L, scale by 1/d, back with L'.
+// fac (optional): an LDS block of NV (NV - 1) / 2 values for a column-oriented back substitution.
+// Every lane publishes its row of L there (packed, row i at i (i - 1) / 2), and step c broadcasts the
+// finished x_c from lane c while every lane j < c subtracts L_cj x_c, read from LDS off the chain:
+// one broadcast and one FMA per column instead of a half-wave sum.
 template <int NV, typename T, bool UNIT = false>
-__device__ __forceinline__ T chol_solve(const T (&L)[NV], T dinv, T b, int sl) {
+__device__ __forceinline__ T chol_solve(const T (&L)[NV], T dinv, T b, int sl, T* fac = nullptr) {
   static_for<0, NV - 1>([&](auto kc) {      // column NV - 1 has no row below it: skipped
     constexpr int k = decltype(kc)::value;
     b = fma(-L[k], bcast<k>(UNIT ? b : b * dinv), b);
   });
   b *= dinv;
+  if (fac) {
+    const int sl_w = opaque_v(sl);
+    const int base = sl_w * (sl_w - 1) / 2;
+    static_for<0, NV - 1>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      if (j < sl_w && sl_w < NV) fac[base + j] = L[j];
+    });
+    WSYNC();
+    // L' x = y (UNIT: y = D^-1 z already); lane c's x is final when column c's turn comes
+    T x = b;
+    static_for<0, NV - 1>([&](auto tc) {
+      constexpr int c = NV - 1 - decltype(tc)::value;          // NV - 1 .. 1
+      const int sl_c = opaque_v(sl);
+      const T l = fac[c * (c - 1) / 2 + (sl_c < c ? sl_c : 0)];
+      const T xc = bcast<c>(UNIT ? x : x * dinv);
+      x = sl_c < c ? fma(-l, xc, x) : x;
+    });
+    WSYNC();
+    return UNIT ? x : x * dinv;
+  }
   // back substitution x_k = (y_k - sum_{i>k} L_ik x_i) / L_kk in blocks of BS columns, top block
   // first: the sums over the rows below the block are BS independent half-wave sums (their latencies
   // overlap), the block's own rows follow as a short chain of broadcasts of L_ik x_i from lane i
@@ -476,12 +568,23 @@ __device__ __forceinline__ T chol_fwd(const T (&L)[NV], T dinv, T b, int sl) {
 // (A v)_i for a row-per-lane matrix and a vector in LDS (broadcast ds_reads)
 template <int NV, typename T>
 __device__ __forceinline__ T matvec_lds(const T (&A)[NV], const T* v) {
+#if HS_MATVEC_SPLIT
+  // two interleaved accumulators (half the dependent FMA chain; the sum's rounding order differs)
+  T acc0 = 0, acc1 = 0;
+  static_for<0, NV>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    if constexpr (j % 2 == 0) acc0 = fma(A[j], v[j], acc0);
+    else acc1 = fma(A[j], v[j], acc1);
+  });
+  return acc0 + acc1;
+#else
   T acc = 0;
   static_for<0, NV>([&](auto jc) {
     constexpr int j = decltype(jc)::value;
     acc = fma(A[j], v[j], acc);
   });
   return acc;
+#endif
 }
 
 // ------------------------------------------------------------------ per-env LDS scratch
@@ -946,6 +1049,12 @@ struct Stepper {
 #define HS_NEWTON_LDL 2
 #endif
   static constexpr bool LDLF = INCR || ((sizeof(T) == 8 ? 2 : 1) & HS_NEWTON_LDL) != 0;
+  // column-oriented back substitution through LDS in the Newton solve (chol_solve), per precision
+  // (bit 0 the fp32 engine, bit 1 the fp64 engine)
+#ifndef HS_BACK_LDS
+#define HS_BACK_LDS 0
+#endif
+  static constexpr bool BACK_LDS = ((sizeof(T) == 8 ? 2 : 1) & HS_BACK_LDS) != 0;
 #ifdef HS_EULER_LDL
   static constexpr bool LDLE = true;
 #else
@@ -1611,7 +1720,7 @@ struct Stepper {
       chol_rows<NV, T, LDLF>(H, hdinv, sl, s.u.n.cb, &hdiag);   // (LDLF: as L D L')
       HS_STAMP(clk, 15);
       }
-      T sdir = -chol_solve<NV, T, LDLF>(H, hdinv, g, sl);
+      T sdir = -chol_solve<NV, T, LDLF>(H, hdinv, g, sl, (BACK_LDS && !INCR) ? s.u.nf.fac : nullptr);
       if constexpr (INCR) {   // the factor and its active set, for the next iteration's update
         fmask = 0;
 #pragma unroll
