@@ -165,6 +165,41 @@ __device__ __forceinline__ uint32_t hballot(bool p, bool upper) {
   uint64_t m = __ballot(p);
   return upper ? (uint32_t)(m >> 32) : (uint32_t)m;
 }
+// f(j, ld(j)) for each set bit j of mk, ascending (the chain / subtree sums).  HS_BITS_AHEAD (per
+// precision: bit 0 fp32, bit 1 fp64; development A/B knob): the loads of the next bit's operands are
+// issued before the current bit's arithmetic, so one LDS round trip overlaps the FMAs (the same
+// operations in the same order).  Measured slower in both engines (fp64 0.697 vs 0.691 ms, fp32 0.411
+// vs 0.408 ms per configs[1] launch): off.
+#ifndef HS_BITS_AHEAD
+#define HS_BITS_AHEAD 0
+#endif
+template <typename T, typename LD, typename F>
+__device__ __forceinline__ void for_bits(uint32_t mk, LD&& ld, F&& f) {
+  if constexpr ((HS_BITS_AHEAD & (sizeof(T) == 8 ? 2 : 1)) != 0) {
+    if (mk == 0u) return;
+    int j = __builtin_ctz(mk);
+    mk &= mk - 1u;
+    auto cur = ld(j);
+    for (; mk; mk &= mk - 1u) {
+      const int jn = __builtin_ctz(mk);
+      auto nxt = ld(jn);
+      f(j, cur);
+      cur = nxt;
+      j = jn;
+    }
+    f(j, cur);
+  } else {
+    for (; mk; mk &= mk - 1u) {
+      const int j = __builtin_ctz(mk);
+      f(j, ld(j));
+    }
+  }
+}
+template <typename T, int N>
+struct Vals { T v[N]; };
+template <typename T, int N>
+struct ValsX { T x; T v[N]; };
+
 // Hide a (uniform) pointer's value from the optimiser.  The model pointer is const __restrict__,
 // so without this LICM hoists every per-lane model load (m->dof_bodyid[sl], ...) out of the
 // substep / Newton loops and keeps each one live in a VGPR for the whole kernel.
@@ -482,37 +517,13 @@ __device__ __forceinline__ bool ldl_rank1(T (&A)[NV], T& d, T& dinv, T v, T sgn,
 // returns x_i.  Forward: at step k every lane subtracts L_ik y_k (zero unless i > k), so lane k's b
 // stops changing once y_k = b_k / L_kk is broadcast, and y = b / L_ii at the end.
 // UNIT: L D L' form instead (unit lower L, 1/d_i in dinv): forward with L, scale by 1/d, back with L'.
-// fac (optional): an LDS block of NV (NV - 1) / 2 values for a column-oriented back substitution.
-// Every lane publishes its row of L there (packed, row i at i (i - 1) / 2), and step c broadcasts the
-// finished x_c from lane c while every lane j < c subtracts L_cj x_c, read from LDS off the chain:
-// one broadcast and one FMA per column instead of a half-wave sum.
 template <int NV, typename T, bool UNIT = false>
-__device__ __forceinline__ T chol_solve(const T (&L)[NV], T dinv, T b, int sl, T* fac = nullptr) {
+__device__ __forceinline__ T chol_solve(const T (&L)[NV], T dinv, T b, int sl) {
   static_for<0, NV - 1>([&](auto kc) {      // column NV - 1 has no row below it: skipped
     constexpr int k = decltype(kc)::value;
     b = fma(-L[k], bcast<k>(UNIT ? b : b * dinv), b);
   });
   b *= dinv;
-  if (fac) {
-    const int sl_w = opaque_v(sl);
-    const int base = sl_w * (sl_w - 1) / 2;
-    static_for<0, NV - 1>([&](auto jc) {
-      constexpr int j = decltype(jc)::value;
-      if (j < sl_w && sl_w < NV) fac[base + j] = L[j];
-    });
-    WSYNC();
-    // L' x = y (UNIT: y = D^-1 z already); lane c's x is final when column c's turn comes
-    T x = b;
-    static_for<0, NV - 1>([&](auto tc) {
-      constexpr int c = NV - 1 - decltype(tc)::value;          // NV - 1 .. 1
-      const int sl_c = opaque_v(sl);
-      const T l = fac[c * (c - 1) / 2 + (sl_c < c ? sl_c : 0)];
-      const T xc = bcast<c>(UNIT ? x : x * dinv);
-      x = sl_c < c ? fma(-l, xc, x) : x;
-    });
-    WSYNC();
-    return UNIT ? x : x * dinv;
-  }
   // back substitution x_k = (y_k - sum_{i>k} L_ik x_i) / L_kk in blocks of BS columns, top block
   // first: the sums over the rows below the block are BS independent half-wave sums (their latencies
   // overlap), the block's own rows follow as a short chain of broadcasts of L_ik x_i from lane i
@@ -825,12 +836,11 @@ __device__ __forceinline__ void map_vx(Scratch<T, C>& s, int sl, int nb, uint32_
     T v[6] = {0, 0, 0, 0, 0, 0};
     // the chain's dofs only, ascending: the same sum as over all dofs (the skipped terms are exact
     // zeros), ~half the fp64 FMAs (fp64 0.866 -> 0.812 ms per launch)
-    for (uint32_t mk = ch; mk; mk &= mk - 1u) {
-      const int j = __builtin_ctz(mk);
-      const T xj = s.vx[j];
+    for_bits<T>(ch, [&](int j) { ValsX<T, 6> r; r.x = s.vx[j]; for (int k = 0; k < 6; k++) r.v[k] = s.cdof[j][k]; return r; },
+                [&](int, const ValsX<T, 6>& r) {
 #pragma unroll
-      for (int k = 0; k < 6; k++) v[k] = fma(s.cdof[j][k], xj, v[k]);
-    }
+                  for (int k = 0; k < 6; k++) v[k] = fma(r.v[k], r.x, v[k]);
+                });
     for (int k = 0; k < 6; k++) s.u.n.bvel[sl][k] = v[k];
   }
   WSYNC();
@@ -1049,12 +1059,6 @@ struct Stepper {
 #define HS_NEWTON_LDL 2
 #endif
   static constexpr bool LDLF = INCR || ((sizeof(T) == 8 ? 2 : 1) & HS_NEWTON_LDL) != 0;
-  // column-oriented back substitution through LDS in the Newton solve (chol_solve), per precision
-  // (bit 0 the fp32 engine, bit 1 the fp64 engine)
-#ifndef HS_BACK_LDS
-#define HS_BACK_LDS 0
-#endif
-  static constexpr bool BACK_LDS = ((sizeof(T) == 8 ? 2 : 1) & HS_BACK_LDS) != 0;
 #ifdef HS_EULER_LDL
   static constexpr bool LDLE = true;
 #else
@@ -1293,10 +1297,8 @@ struct Stepper {
     if (sl > 0 && sl < nb) {
       const uint32_t dm = m->body_descmask[sl] & ~1u & ((nb < 32 ? (1u << nb) : 0u) - 1u);
       T a[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-      for (uint32_t mk = dm; mk; mk &= mk - 1u) {   // the subtree's bodies only, ascending
-        const int c = __builtin_ctz(mk);
-        for (int k = 0; k < 10; k++) a[k] += s.cinert[c][k];
-      }
+      for_bits<T>(dm, [&](int c) { Vals<T, 10> r; for (int k = 0; k < 10; k++) r.v[k] = s.cinert[c][k]; return r; },
+                  [&](int, const Vals<T, 10>& r) { for (int k = 0; k < 10; k++) a[k] += r.v[k]; });   // the subtree's bodies, ascending
       for (int k = 0; k < 10; k++) s.u.c.crb[sl][k] = a[k];
     }
     WSYNC();
@@ -1351,22 +1353,16 @@ struct Stepper {
       T v[6] = {0, 0, 0, 0, 0, 0};
       if (sl > 0) {
         const uint32_t ch = m->body_chainmask[sl];
-        for (uint32_t mk = ch; mk; mk &= mk - 1u) {   // the chain's dofs only, ascending
-          const int j = __builtin_ctz(mk);
-          const T q = s.qvel[j];
-          for (int k = 0; k < 6; k++) v[k] = fma(s.cdof[j][k], q, v[k]);
-        }
+        for_bits<T>(ch, [&](int j) { ValsX<T, 6> r; r.x = s.qvel[j]; for (int k = 0; k < 6; k++) r.v[k] = s.cdof[j][k]; return r; },
+                    [&](int, const ValsX<T, 6>& r) { for (int k = 0; k < 6; k++) v[k] = fma(r.v[k], r.x, v[k]); });   // the chain's dofs, ascending
       }
       for (int k = 0; k < 6; k++) s.cvel[sl][k] = v[k];
     }
     if (sl < NV) {
       const uint32_t dm = m->dof_dotmask[sl];
       T v[6] = {0, 0, 0, 0, 0, 0}, cdd[6];
-      for (uint32_t mk = dm; mk; mk &= mk - 1u) {   // ascending, set bits only
-        const int j = __builtin_ctz(mk);
-        const T q = s.qvel[j];
-        for (int k = 0; k < 6; k++) v[k] = fma(s.cdof[j][k], q, v[k]);
-      }
+      for_bits<T>(dm, [&](int j) { ValsX<T, 6> r; r.x = s.qvel[j]; for (int k = 0; k < 6; k++) r.v[k] = s.cdof[j][k]; return r; },
+                  [&](int, const ValsX<T, 6>& r) { for (int k = 0; k < 6; k++) v[k] = fma(r.v[k], r.x, v[k]); });   // ascending, set bits only
       cross_motion(v, cd, cdd);
       for (int k = 0; k < 6; k++) s.u.r.cdofdot[sl][k] = cdd[k];
     }
@@ -1374,11 +1370,8 @@ struct Stepper {
     if (sl > 0 && sl < nb) {   // RNE: cacc, cfrc_body
       const uint32_t ch = m->body_chainmask[sl];
       T a[6] = {0, 0, 0, -m->gravity[0], -m->gravity[1], -m->gravity[2]};
-      for (uint32_t mk = ch; mk; mk &= mk - 1u) {   // the chain's dofs only, ascending
-        const int j = __builtin_ctz(mk);
-        const T q = s.qvel[j];
-        for (int k = 0; k < 6; k++) a[k] = fma(s.u.r.cdofdot[j][k], q, a[k]);
-      }
+      for_bits<T>(ch, [&](int j) { ValsX<T, 6> r; r.x = s.qvel[j]; for (int k = 0; k < 6; k++) r.v[k] = s.u.r.cdofdot[j][k]; return r; },
+                  [&](int, const ValsX<T, 6>& r) { for (int k = 0; k < 6; k++) a[k] = fma(r.v[k], r.x, a[k]); });   // the chain's dofs, ascending
       T f[6], t[6], t2[6];
       mul_inert(s.cinert[sl], a, f);
       mul_inert(s.cinert[sl], s.cvel[sl], t);
@@ -1389,10 +1382,8 @@ struct Stepper {
     if (sl > 0 && sl < nb) {   // subtree sums of cfrc_body
       const uint32_t dm = m->body_descmask[sl] & ~1u & ((nb < 32 ? (1u << nb) : 0u) - 1u);
       T a[6] = {0, 0, 0, 0, 0, 0};
-      for (uint32_t mk = dm; mk; mk &= mk - 1u) {   // the subtree's bodies only, ascending
-        const int c = __builtin_ctz(mk);
-        for (int k = 0; k < 6; k++) a[k] += s.u.r.cfrc[c][k];
-      }
+      for_bits<T>(dm, [&](int c) { Vals<T, 6> r; for (int k = 0; k < 6; k++) r.v[k] = s.u.r.cfrc[c][k]; return r; },
+                  [&](int, const Vals<T, 6>& r) { for (int k = 0; k < 6; k++) a[k] += r.v[k]; });   // the subtree's bodies, ascending
       for (int k = 0; k < 6; k++) s.u.r.csub[sl][k] = a[k];
     }
     WSYNC();
@@ -1720,7 +1711,7 @@ struct Stepper {
       chol_rows<NV, T, LDLF>(H, hdinv, sl, s.u.n.cb, &hdiag);   // (LDLF: as L D L')
       HS_STAMP(clk, 15);
       }
-      T sdir = -chol_solve<NV, T, LDLF>(H, hdinv, g, sl, (BACK_LDS && !INCR) ? s.u.nf.fac : nullptr);
+      T sdir = -chol_solve<NV, T, LDLF>(H, hdinv, g, sl);
       if constexpr (INCR) {   // the factor and its active set, for the next iteration's update
         fmask = 0;
 #pragma unroll
