@@ -66,6 +66,22 @@ using Wide = Cap<MAXCON_WIDE, MAXEFC_WIDE, true>;
 #ifndef HS_SQRT_FAST
 #define HS_SQRT_FAST 2
 #endif
+// CRB and Newton-Hessian rows software-pipelined: the next column (group)'s LDS reads are issued
+// before the current one's arithmetic, behind the per-column scheduling fence, so each LDS round trip
+// overlaps the previous column's FMAs (A/B, fp64 ms per configs[1] launch: 0.681 -> CRB 0.674,
+// Hessian 0.661, both 0.659; the fp64 queue kernel drops from 510 to 482 unified registers)
+#ifndef HS_CRB_AHEAD
+#define HS_CRB_AHEAD 1
+#endif
+#ifndef HS_HESS_AHEAD
+#define HS_HESS_AHEAD 1
+#endif
+// fp64 Cholesky (DPP pivots): trailing-column LDS reads issued before the pivot math, behind a
+// scheduling fence (the machine scheduler otherwise sinks the column publish and its read-back below
+// the pivot chain, exposing the LDS round trip): 0.691 -> 0.682 ms per fp64 configs[1] launch
+#ifndef HS_CHOL_EARLY
+#define HS_CHOL_EARLY 1
+#endif
 // M·v with two accumulators (development A/B knob)
 #ifndef HS_MATVEC_SPLIT
 #define HS_MATVEC_SPLIT 0
@@ -417,15 +433,30 @@ __device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb)[2
     cb[sl_k][1] = A[k + 1];
     T p, q, t;
     if constexpr (CDPP) {   // the pivot block by DPP broadcast from lanes k, k+1: the LDS round trip
-      p = bcast<k>(A[k]);   // of the column publish leaves the pivot chain (the trailing update still
-      q = bcast<k + 1>(A[k]);   // reads a_jk from LDS)
+      // of the column publish leaves the pivot chain (the trailing update still reads a_jk from LDS);
+      // the pivot is clamped before the broadcast (an FMA result: no NaN canonicalization for v_max)
+      p = bcast<k>(A[k] > T(1e-30) ? A[k] : T(1e-30));
+      q = bcast<k + 1>(A[k]);
       t = bcast<k + 1>(A[k + 1]);
     } else {
       p = cb[k][0];
       q = cb[k + 1][0];
       t = cb[k + 1][1];
+      p = p > T(1e-30) ? p : T(1e-30);
     }
-    p = p > T(1e-30) ? p : T(1e-30);
+#if HS_CHOL_EARLY
+    // the trailing columns' broadcast reads issued before the pivot math (fenced), so their LDS round
+    // trip overlaps the pivot chain instead of following it
+    T cj[NV][2];
+    if constexpr (CDPP) {
+      static_for<k + 2, NV>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        cj[j][0] = cb[j][0];
+        cj[j][1] = cb[j][1];
+      });
+      SCHED_FENCE();
+    }
+#endif
     T r1 = rsqrt_t(p);
     T l10 = q * r1;
     T s11 = t - l10 * l10;
@@ -447,6 +478,10 @@ __device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb)[2
     }
     static_for<k + 2, NV>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
+#if HS_CHOL_EARLY
+      if constexpr (CDPP) A[j] = fma(-f0, cj[j][0], fma(-f1, cj[j][1], A[j]));
+      else
+#endif
       A[j] = fma(-f0, cb[j][0], fma(-f1, cb[j][1], A[j]));
     });
     if constexpr (HS_FENCE_CHOL == 1 || (HS_FENCE_CHOL == 2 && (k / 2) % 2 == 1)) SCHED_FENCE();
@@ -1313,7 +1348,25 @@ struct Stepper {
     }
     WSYNC();
     // CRB_G columns per scheduling group (one exposed LDS round trip per group, as in the Hessian)
-    if constexpr (CRB_G == 1) {
+    if constexpr (HS_CRB_AHEAD) {
+      // software-pipelined: column j+1's cdof / buf rows are read before column j's arithmetic
+      T cb2[2][12];
+      auto load = [&](auto jc, T (&dst)[12]) {
+        constexpr int j = decltype(jc)::value;
+        for (int k = 0; k < 6; k++) { dst[k] = s.cdof[j][k]; dst[6 + k] = s.u.c.buf[j][k]; }
+      };
+      load(std::integral_constant<int, 0>{}, cb2[0]);
+      static_for<0, NV>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        if constexpr (j + 1 < NV) load(std::integral_constant<int, j + 1>{}, cb2[(j + 1) & 1]);
+        SCHED_FENCE();
+        const uint32_t ancj = m->dof_ancmask[j];
+        const bool rel = (sl < NV) && (bit(anci, j) || bit(ancj, sl));
+        const T* cj = cb2[j & 1];
+        const T v = (j <= sl) ? dot6(cj, bf) : dot6(cd, cj + 6);
+        Mr[j] = rel ? v + ((j == sl) ? arm : T(0)) : T(0);
+      });
+    } else if constexpr (CRB_G == 1) {
 #pragma unroll
       for (int j = 0; j < NV; j++) {
         uint32_t ancj = m->dof_ancmask[j];
@@ -1649,6 +1702,30 @@ struct Stepper {
             H[j] = Mr[j] + (bit(anci, j) ? dot6(cj, aug) : T(0)) + ((j == sl) ? dadd : T(0));
             if constexpr (HS_FENCE_HESS) SCHED_FENCE();
           }
+        } else if constexpr (HS_HESS_AHEAD) {
+          // software-pipelined: group g+1's cdof rows are read before group g's arithmetic (fenced),
+          // so each group's LDS round trip overlaps the previous group's FMAs
+          constexpr int NG = (NV + HESS_G - 1) / HESS_G;
+          T cbuf[2][HESS_G][6];
+          auto load = [&](auto gc, T (&dst)[HESS_G][6]) {
+            constexpr int j0 = decltype(gc)::value * HESS_G;
+            static_for<0, HESS_G>([&](auto tc) {
+              constexpr int t = decltype(tc)::value;
+              if constexpr (j0 + t < NV)
+                for (int k = 0; k < 6; k++) dst[t][k] = s.cdof[j0 + t][k];
+            });
+          };
+          load(std::integral_constant<int, 0>{}, cbuf[0]);
+          static_for<0, NG>([&](auto gc) {
+            constexpr int g = decltype(gc)::value, j0 = g * HESS_G;
+            if constexpr (g + 1 < NG) load(std::integral_constant<int, g + 1>{}, cbuf[(g + 1) & 1]);
+            SCHED_FENCE();
+            static_for<0, HESS_G>([&](auto tc) {
+              constexpr int t = decltype(tc)::value, j = j0 + t;
+              if constexpr (j < NV)
+                H[j] = Mr[j] + (bit(anci, j) ? dot6(cbuf[g & 1][t], aug) : T(0)) + ((j == sl) ? dadd : T(0));
+            });
+          });
         } else static_for<0, (NV + HESS_G - 1) / HESS_G>([&](auto gc) {
           constexpr int j0 = decltype(gc)::value * HESS_G;
           T cj[HESS_G][6];
