@@ -62,6 +62,14 @@ using Wide = Cap<MAXCON_WIDE, MAXEFC_WIDE, true>;
 #ifndef HS_CHOL_DPP
 #define HS_CHOL_DPP 2
 #endif
+// contact aggregates over a contact's rows as straight-line code (A/B knob)
+#ifndef HS_AGGR_STATIC
+#define HS_AGGR_STATIC 0
+#endif
+// fp64 1/x as rcp + one cubic correction instead of two Newton steps (A/B knob)
+#ifndef HS_RECIP3
+#define HS_RECIP3 0
+#endif
 // fp64 1/sqrt without the denormal / class handling of the library sqrt (development A/B knob)
 #ifndef HS_SQRT_FAST
 #define HS_SQRT_FAST 2
@@ -315,10 +323,16 @@ __device__ __forceinline__ float rsqrt_t<float>(float x) { return __builtin_amdg
 __device__ __forceinline__ float recip(float x) { return 1.0f / x; }
 __device__ __forceinline__ double recip(double x) {
   double y = __builtin_amdgcn_rcp(x);
+#if HS_RECIP3
+  // y (1 + e + e^2) with e = 1 - x y: relative error cubed in one step (4 dependent operations)
+  const double e = fma(-x, y, 1.0);
+  return fma(fma(e, e, e), y, y);
+#else
   double e = fma(-x, y, 1.0);
   y = fma(y, e, y);
   e = fma(-x, y, 1.0);
   return fma(y, e, y);
+#endif
 }
 // fp64 1/sqrt(x), x >= 1e-30 at every call site (the Cholesky pivots are clamped to it, the
 // normalizations branch below it), so no denormal scaling or zero / infinity class check:
@@ -945,6 +959,39 @@ __device__ __forceinline__ void contact_aggregates(MPtr<T> m, Scratch<T, C>& s, 
       int adr = s.con_adr[c];
       int nr = (s.con_bb[c] >> 16) == 1 ? 1 : 4;
       T U[6] = {0, 0, 0, 0, 0, 0}, F[3] = {0, 0, 0};
+#if HS_AGGR_STATIC
+      // straight-line over the (at most 4) rows: every LDS operand is read up front (one round trip),
+      // then the same sums in the same order as the row loop below
+      const bool pyr = nr == 4;
+      T f4[4], D4[4], nn[3], t1[3], t2[3];
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const bool on = q == 0 || pyr;
+        f4[q] = on ? s.row_f[adr + q] : T(0);
+        D4[q] = on ? s.row_D[adr + q] : T(0);
+      }
+      for (int k = 0; k < 3; k++) { nn[k] = s.con_n[c][k]; t1[k] = s.con_t1[c][k]; }
+      const T mu = s.con_mu[c];
+      cross3(nn, t1, t2);
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const T f = f4[q];
+        if (f != T(0)) {
+          T u[3];
+          if (!pyr) {
+            for (int k = 0; k < 3; k++) u[k] = nn[k];
+          } else {
+            const T sg = (q & 1) ? -mu : mu;
+            for (int k = 0; k < 3; k++) u[k] = nn[k] + sg * ((q >> 1) ? t2[k] : t1[k]);
+          }
+          const T D = D4[q];
+          U[0] += D * u[0] * u[0]; U[1] += D * u[1] * u[1]; U[2] += D * u[2] * u[2];
+          U[3] += D * u[0] * u[1]; U[4] += D * u[0] * u[2]; U[5] += D * u[1] * u[2];
+          for (int k = 0; k < 3; k++) F[k] += f * u[k];
+        }
+      }
+      if (false)
+#endif
       for (int q = 0; q < nr; q++) {
         int r = adr + q;
         T f = s.row_f[r];
