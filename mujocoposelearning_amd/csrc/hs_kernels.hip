@@ -200,9 +200,9 @@ __device__ __forceinline__ uint32_t hballot(bool p, bool upper) {
 #ifndef HS_BITS_AHEAD
 #define HS_BITS_AHEAD 0
 #endif
-template <typename T, typename LD, typename F>
+template <typename T, bool AHEAD = (HS_BITS_AHEAD & (sizeof(T) == 8 ? 2 : 1)) != 0, typename LD, typename F>
 __device__ __forceinline__ void for_bits(uint32_t mk, LD&& ld, F&& f) {
-  if constexpr ((HS_BITS_AHEAD & (sizeof(T) == 8 ? 2 : 1)) != 0) {
+  if constexpr (AHEAD) {
     if (mk == 0u) return;
     int j = __builtin_ctz(mk);
     mk &= mk - 1u;
@@ -1024,11 +1024,49 @@ __device__ __forceinline__ void for_active_contacts(const uint32_t* act, F&& f) 
     for (uint32_t mk = act[w]; mk; mk &= mk - 1u) f(w * HL + __builtin_ctz(mk));
 }
 
+// the same with every per-contact LDS operand read by ld(c) in one batch (one round trip per
+// contact instead of a read, a branch on it and dependent reads; HS_CONTACT_FLAT) and the next
+// contact's reads issued before the current contact's arithmetic (HS_CONTACT_AHEAD): J'f and the
+// Hessian's contact terms.  A/B, fp64 ms per configs[1] launch: 0.635 -> flat 0.634 -> + ahead 0.632.
+#ifndef HS_CONTACT_AHEAD
+#define HS_CONTACT_AHEAD 1
+#endif
+template <typename T, typename C, typename LD, typename F>
+__device__ __forceinline__ void for_active_contacts_ld(const uint32_t* act, LD&& ld, F&& f) {
+#pragma unroll
+  for (int w = 0; w < (C::CON + HL - 1) / HL; w++)
+    for_bits<T, HS_CONTACT_AHEAD != 0>(
+        act[w], [&](int j) { return ld(w * HL + j); }, [&](int j, const auto& v) { f(w * HL + j, v); });
+}
+#ifndef HS_CONTACT_FLAT
+#define HS_CONTACT_FLAT 1
+#endif
+
 // (J' f)_i for dof sub-lane i (contacts via point Jacobians, joint limits via the dof's
 // limit-row slots, tendon limits via rows [njl, nlim))
 template <typename T, typename C>
 __device__ __forceinline__ T jtf_lane(MPtr<T> m, const Scratch<T, C>& s, int sl, const T* cd) {
   T acc = 0;
+#if HS_CONTACT_FLAT
+  struct CV { uint32_t m1, m2; T p[3], f[3]; };
+  for_active_contacts_ld<T, C>(s.con_act, [&](int c) {
+    CV v;
+    v.m1 = s.con_m1[c]; v.m2 = s.con_m2[c];
+    for (int k = 0; k < 3; k++) { v.p[k] = s.con_pos[c][k]; v.f[k] = s.con_F[c][k]; }
+    return v;
+  }, [&](int, const CV& v) {
+    const int in2 = bit(v.m2, sl), in1 = bit(v.m1, sl);
+    if (in1 != in2) {
+      T r[3] = {v.p[0] - s.com[0], v.p[1] - s.com[1], v.p[2] - s.com[2]};
+      T w[3];
+      cross3(cd, r, w);
+      T jp[3] = {cd[3] + w[0], cd[4] + w[1], cd[5] + w[2]};
+      T x = dot3(jp, v.f);
+      acc += in2 ? x : -x;
+    }
+  });
+  if (false)
+#endif
   for_active_contacts<C>(s.con_act, [&](int c) {
     int in2 = bit(s.con_m2[c], sl), in1 = bit(s.con_m1[c], sl);
     if (in1 != in2) {
@@ -1716,6 +1754,29 @@ struct Stepper {
       {
         T aug[6] = {0, 0, 0, 0, 0, 0};
         T dadd = 0;
+#if HS_CONTACT_FLAT
+        struct CU { uint32_t m1, m2; T p[3], U[6]; };
+        for_active_contacts_ld<T, C>(s.con_act, [&](int c) {
+          CU v;
+          v.m1 = s.con_m1[c]; v.m2 = s.con_m2[c];
+          for (int k = 0; k < 3; k++) v.p[k] = s.con_pos[c][k];
+          for (int k = 0; k < 6; k++) v.U[k] = s.con_U[c][k];
+          return v;
+        }, [&](int, const CU& v) {   // (contacts with U = 0 add exact zeros)
+          if (v.m1 != 0u || !bit(v.m2, sl)) return;   // body-body: dense rank-1 rows below
+          T r[3] = {v.p[0] - s.com[0], v.p[1] - s.com[1], v.p[2] - s.com[2]};
+          T w[3];
+          cross3(cd, r, w);
+          T jp[3] = {cd[3] + w[0], cd[4] + w[1], cd[5] + w[2]};
+          const T* U = v.U;
+          T z[3] = {U[0] * jp[0] + U[3] * jp[1] + U[4] * jp[2], U[3] * jp[0] + U[1] * jp[1] + U[5] * jp[2],
+                    U[4] * jp[0] + U[5] * jp[1] + U[2] * jp[2]};
+          T rz[3];
+          cross3(r, z, rz);
+          for (int k = 0; k < 3; k++) { aug[k] += rz[k]; aug[3 + k] += z[k]; }
+        });
+        if (false)
+#endif
         for_active_contacts<C>(s.con_act, [&](int c) {   // (contacts with U = 0 add exact zeros)
           if (s.con_m1[c] != 0u) return;           // body-body: dense rank-1 rows below
           if (!bit(s.con_m2[c], sl)) return;
