@@ -882,26 +882,8 @@ template <typename T>
 __device__ __forceinline__ uint32_t chain_mask(MPtr<T> m, int sl, int nb) {
   return (sl > 0 && sl < nb) ? m->body_chainmask[sl] : 0u;
 }
-#ifndef HS_MAPVX_EARLY
-#define HS_MAPVX_EARLY 0
-#endif
 template <int NV, typename T, typename C>
 __device__ __forceinline__ void map_vx(Scratch<T, C>& s, int sl, int nb, uint32_t ch) {
-#if HS_MAPVX_EARLY
-  // the contact lane's operands (body ids, lever arm, frame) read before the body loop, so only the
-  // bodies' velocities are left to wait for after it (resident tier: one contact slot per lane)
-  constexpr bool EARLY = C::CON <= HL;
-  uint32_t bbE = 0;
-  T rE[3], nE[3], t1E[3];
-  if constexpr (EARLY) {
-    if (sl < s.ncon) {
-      bbE = s.con_bb[sl];
-      for (int k = 0; k < 3; k++) { rE[k] = s.con_pos[sl][k] - s.com[k]; nE[k] = s.con_n[sl][k]; t1E[k] = s.con_t1[sl][k]; }
-    }
-  }
-#else
-  constexpr bool EARLY = false;
-#endif
   if (sl < nb) {   // body spatial velocity = sum over the body's dof chain of cdof_j x_j
     T v[6] = {0, 0, 0, 0, 0, 0};
     // the chain's dofs only, ascending: the same sum as over all dofs (the skipped terms are exact
@@ -914,26 +896,6 @@ __device__ __forceinline__ void map_vx(Scratch<T, C>& s, int sl, int nb, uint32_
     for (int k = 0; k < 6; k++) s.u.n.bvel[sl][k] = v[k];
   }
   WSYNC();
-#if HS_MAPVX_EARLY
-  if constexpr (EARLY) {
-    if (sl < s.ncon) {
-      const int b1 = bbE & 0xff, b2 = (bbE >> 8) & 0xff;
-      T w[3], v1[3], v2[3];
-      cross3(s.u.n.bvel[b2], rE, w);
-      for (int k = 0; k < 3; k++) v2[k] = s.u.n.bvel[b2][3 + k] + w[k];
-      cross3(s.u.n.bvel[b1], rE, w);
-      for (int k = 0; k < 3; k++) v1[k] = s.u.n.bvel[b1][3 + k] + w[k];
-      T dv[3] = {v2[0] - v1[0], v2[1] - v1[1], v2[2] - v1[2]};
-      T t2[3];
-      cross3(nE, t1E, t2);
-      s.con_v[sl][0] = dot3(nE, dv);
-      s.con_v[sl][1] = dot3(t1E, dv);
-      s.con_v[sl][2] = dot3(t2, dv);
-    }
-    WSYNC();
-    return;
-  }
-#endif
 #pragma unroll
   for (int cs = 0; cs < C::CON; cs += HL) {   // contact slots of this lane (one per lane in the resident tier)
     const int c = cs + sl;
