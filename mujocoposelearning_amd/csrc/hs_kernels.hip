@@ -87,11 +87,12 @@ using Wide = Cap<MAXCON_WIDE, MAXEFC_WIDE, true>;
 #ifndef HS_HESS_AHEAD
 #define HS_HESS_AHEAD 1
 #endif
-// fp64 Cholesky (DPP pivots): trailing-column LDS reads issued before the pivot math, behind a
+// Cholesky, per precision (bit 0 fp32, bit 1 fp64): trailing-column LDS reads issued before the pivot math, behind a
 // scheduling fence (the machine scheduler otherwise sinks the column publish and its read-back below
-// the pivot chain, exposing the LDS round trip): 0.691 -> 0.682 ms per fp64 configs[1] launch
+// the pivot chain, exposing the LDS round trip): 0.691 -> 0.682 ms per fp64 configs[1] launch; fp32
+// (pivots from LDS too, so one round trip instead of two): 0.390 -> 0.387 ms
 #ifndef HS_CHOL_EARLY
-#define HS_CHOL_EARLY 1
+#define HS_CHOL_EARLY 3
 #endif
 // M·v with two accumulators (development A/B knob)
 #ifndef HS_MATVEC_SPLIT
@@ -437,6 +438,7 @@ __device__ __forceinline__ void cross_force(const T* v, const T* f, T* r) {
 template <int NV, typename T, bool LDL = false>
 __device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb)[2], T* diag = nullptr) {
   constexpr bool CDPP = (HS_CHOL_DPP & (sizeof(T) == 8 ? 2 : 1)) != 0;
+  constexpr bool CEARLY = (HS_CHOL_EARLY & (sizeof(T) == 8 ? 2 : 1)) != 0;
   // two columns per LDS round trip: every lane publishes (a_ik, a_i,k+1) as one ds_write and reads
   // the 2x2 pivot block and (a_jk, a_j,k+1) back as broadcasts.  With L_P the pivot block's
   // Cholesky factor (1/L_kk = r1, L_k+1,k = l10, 1/L_k+1,k+1 = r2), row i gets
@@ -465,7 +467,7 @@ __device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb)[2
     // the trailing columns' broadcast reads issued before the pivot math (fenced), so their LDS round
     // trip overlaps the pivot chain instead of following it
     T cj[NV][2];
-    if constexpr (CDPP) {
+    if constexpr (CEARLY) {
       static_for<k + 2, NV>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
         cj[j][0] = cb[j][0];
@@ -496,7 +498,7 @@ __device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb)[2
     static_for<k + 2, NV>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
 #if HS_CHOL_EARLY
-      if constexpr (CDPP) A[j] = fma(-f0, cj[j][0], fma(-f1, cj[j][1], A[j]));
+      if constexpr (CEARLY) A[j] = fma(-f0, cj[j][0], fma(-f1, cj[j][1], A[j]));
       else
 #endif
       A[j] = fma(-f0, cb[j][0], fma(-f1, cb[j][1], A[j]));
