@@ -50,6 +50,18 @@ bool hip_ok(hipError_t e, const char* what) {
   return false;
 }
 
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
 // Uncached device memory (the chunk queue's hand-off rows, claim / exit / epoch words and pair
 // flags) is recycled only as uncached memory: freed blocks go to a per-device list instead of
 // hipFree.  Round-3 finding: after a batch was destroyed, its hipFree'd UNCACHED hand-off rows were
@@ -73,23 +85,21 @@ bool uc_alloc(int device, size_t bytes, void** out) {
   return hipExtMallocWithFlags(out, bytes, hipDeviceMallocUncached) == hipSuccess;
 }
 
+// The free list is bounded: past kUcKeep blocks the oldest block goes back to the runtime (the
+// stale-obs path above needs a UC block to be handed out again as cached memory while this process
+// still steps batches; a bounded list keeps the common create/destroy cycles inside the pool).
+constexpr size_t kUcKeep = 64;
 void uc_release(int device, size_t bytes, void* ptr) {
   if (!ptr) return;
   std::lock_guard<std::mutex> lk(g_uc_mu);
   g_uc_free.push_back({device, bytes, ptr});
+  if (g_uc_free.size() > kUcKeep) {
+    DeviceGuard g(g_uc_free.front().device);
+    (void)hipDeviceSynchronize();
+    (void)hipFree(g_uc_free.front().ptr);
+    g_uc_free.erase(g_uc_free.begin());
+  }
 }
-
-struct DeviceGuard {
-  int prev = -1;
-  explicit DeviceGuard(int dev) {
-    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-    if (prev != dev) (void)hipSetDevice(dev);
-  }
-  ~DeviceGuard() {
-    int cur;
-    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-  }
-};
 
 int obs_dim_of(const hs::HostModel& m) { return (m.nq - 2) + m.nv + 10 * m.nbody + 6 * m.nbody + m.nv; }
 
@@ -203,7 +213,10 @@ bool init_state(hs_batch* b) {
          (!b->buf.terminal_total_reward || hip_ok(hipMemset(b->buf.terminal_total_reward, 0, (size_t)N * es), "init")) &&
          hip_ok(hipMemset(b->redo, 0, (size_t)(N + 2) * sizeof(int)), "init") &&
          hip_ok(hipMemset(b->redo_total, 0, sizeof(unsigned long long)), "init") &&
-         hip_ok(hipMemset(b->qsync, 0, hs::qsync_words(N) * sizeof(int)), "init");
+         hip_ok(hipMemset(b->qsync, 0, hs::qsync_words(N) * sizeof(int)), "init") &&
+         // a recycled UC block holds another batch's rows: a lost hand-off reads this row's warning
+         // counters and time (hs_kernels.hip step_pair), so they start at 0, not at stale bits
+         hip_ok(hipMemset(b->mid, 0, (size_t)N * hs::MIDDIM * es), "init");
 }
 
 template <typename T>
@@ -459,7 +472,8 @@ int hs_step(hs_batch* b, const float* actions, void* stream) {
   if (!actions) return fail("hs_step: actions must not be NULL");
   if (!b) return fail("null batch");
   int rc = launch(b, hs::MODE_ENV_STEP, actions, nullptr, b->ar_qpos_noise, b->ar_qvel_noise, b->cfg.frame_skip, stream);
-  if (rc == 0 && !(b->cfg.outputs & HS_OUT_CTRL)) b->ctrl_stale = true;
+  // a step with the ctrl copy on rewrites every env's data.ctrl (commit), one with it off leaves it stale
+  if (rc == 0) b->ctrl_stale = !(b->cfg.outputs & HS_OUT_CTRL);
   return rc;
 }
 
@@ -494,11 +508,12 @@ int hs_state_io(hs_batch* b, int dir, double* qpos, double* qvel, double* qacc_w
   if (dir != 0 && dir != 1) return fail("dir must be 0 (get) or 1 (set)");
   if (dir == 0 && ctrl && b->ctrl_stale)
     return fail("hs_state_io: ctrl requested, but env steps ran with HS_OUT_CTRL off (the ctrl buffer is stale)");
-  if (dir == 1 && ctrl) b->ctrl_stale = false;
   DeviceGuard g(b->device);
   if (!hip_ok(hipDeviceSynchronize(), "sync")) return -1;
-  return b->precision == HS_FP64 ? state_io<double>(b, dir, qpos, qvel, qacc_warmstart, time, ctrl)
-                                 : state_io<float>(b, dir, qpos, qvel, qacc_warmstart, time, ctrl);
+  int rc = b->precision == HS_FP64 ? state_io<double>(b, dir, qpos, qvel, qacc_warmstart, time, ctrl)
+                                   : state_io<float>(b, dir, qpos, qvel, qacc_warmstart, time, ctrl);
+  if (rc == 0 && dir == 1 && ctrl) b->ctrl_stale = false;   // only once the new ctrl is on the device
+  return rc;
 }
 
 int hs_kinematics(hs_batch* b, int env, const double* qpos, double* xpos, double* xmat, double* geom_xpos,

@@ -16,7 +16,9 @@ from pathlib import Path
 
 import numpy as np
 
+from . import _lib
 from . import reward_functions as _rf
+from ._lib import HsimError
 from .batch import HsBatch
 from .model import HsModel
 from .render import Renderer, write_video
@@ -24,6 +26,27 @@ from .spaces import Box, Env
 
 CLIP_OBSERVATION_VALUE = np.inf   # custom_env.py:9
 ACTION_CLIP_VALUE = 1             # custom_env.py:10
+
+
+def subtree_com_from_cinert(cinert, com0, parent):
+    """Per-body subtree COM (MuJoCo mj_comPos) from one forward pass's cinert.
+
+    cinert[b] = [I(6), m_b (xipos_b - com0) (3), m_b] with com0 the root subtree's COM, so
+    subtree_com[b] = com0 + sum_{c in subtree(b)} m_c d_c / sum m_c (children have larger ids
+    than their parents, so one backward pass accumulates the subtrees).  A massless subtree gets
+    com0 (MuJoCo: the body's xipos; no such body in the supported model class carries joints)."""
+    cinert = np.asarray(cinert, np.float64)
+    nb = cinert.shape[0]
+    md = cinert[:, 6:9].copy()
+    mass = cinert[:, 9].copy()
+    for b in range(nb - 1, 0, -1):
+        p = int(parent[b])
+        md[p] += md[b]
+        mass[p] += mass[b]
+    out = np.empty((nb, 3))
+    for b in range(nb):
+        out[b] = com0 + (md[b] / mass[b] if mass[b] > 1e-15 else 0.0)
+    return out
 
 
 class HsData:
@@ -83,14 +106,13 @@ class HsData:
 
     @property
     def subtree_com(self):
-        """Row 0 (and every body of the single kinematic tree's root) = whole-model COM of the last
-        forward pass; other rows are not computed by the engine (NaN)."""
-        m = self._env.model
-        out = np.full((m.nbody, 3), np.nan)
-        com = self._b().aux[self._env._idx, 32:35].double().cpu().numpy()
-        out[0] = com
-        out[1] = com
-        return out
+        """MjData.subtree_com of the last forward pass, every body (mj_comPos): rebuilt from the
+        same pass's cinert (obs rows, custom_env.py:240) and the root COM (aux row)."""
+        b = self._b()
+        if not (b.cfg.outputs & _lib.HS_OUT_AUX):
+            raise HsimError("data.subtree_com needs the aux output (HsBatch.configure(aux=True))")
+        com0 = b.aux[self._env._idx, 32:35].double().cpu().numpy()
+        return subtree_com_from_cinert(self.cinert, com0, self._env._body_parent)
 
     @property
     def subtree_linvel(self):
@@ -145,6 +167,7 @@ class HumanoidEnv(Env):
             self.total_reward = 0.0
             device, precision, max_newton, full_state = 0, 'fp64', 100, False
         self.model = HsModel(self.model_path)
+        self._body_parent = self.model.field("body_parentid").astype(int)
         self._batch = HsBatch(self.model, 1, device=device, precision=precision, full_state=full_state)
         self._idx = 0
         self.data = HsData(self)

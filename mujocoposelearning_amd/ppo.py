@@ -195,6 +195,18 @@ def gae(rewards, values, dones, last_values, last_dones, gamma, lam):
     return adv, adv + values
 
 
+def minibatch_weights(counts, rank, n_steps, n_minibatches):
+    """Gradient weight of each of rank ``rank``'s minibatches in the world-plan of
+    PPO._plan_minibatches: rank r splits its n_steps * counts[r] samples into n_minibatches
+    chunks at (j * M_r) // n_minibatches, and minibatch j's weight is its chunk's share of the
+    global minibatch j (the sum over ranks), so the all-reduced sum is the global mean."""
+    nmb = n_minibatches
+    def size(c, j):
+        m = n_steps * c
+        return ((j + 1) * m) // nmb - (j * m) // nmb
+    return [size(counts[rank], j) / sum(size(c, j) for c in counts) for j in range(nmb)]
+
+
 class PPO:
     """PPO over a device vec-env (HumanoidVecEnv's fast path).
 
@@ -392,7 +404,7 @@ class PPO:
           M_r / M_total before the sum, so uneven shards count per sample.
         """
         world, T, bs = self.world_size, self.n_steps, self.batch_size
-        if world > 1 or self.sync_grads:
+        if self.sync_grads:      # independent trainers (sync_grads=False) plan locally, no collective
             import torch.distributed as dist
             counts = torch.zeros(world, dtype=torch.int64, device=self._comm_device())
             counts[self.rank] = n_local
@@ -405,7 +417,7 @@ class PPO:
         self.env_counts = counts
         self.n_envs_global = sum(counts)
         M = T * n_local
-        if world == 1:
+        if world == 1 or not self.sync_grads:
             self.n_minibatches = -(-M // bs)
             self._mb_bounds = [min(s, M) for s in range(0, M + bs, bs)][: self.n_minibatches + 1]
             self._mb_bounds[-1] = M
@@ -417,7 +429,12 @@ class PPO:
             self._mb_bounds = [(j * M) // self.n_minibatches for j in range(self.n_minibatches + 1)]
         sizes = {b - a for a, b in zip(self._mb_bounds, self._mb_bounds[1:])}
         self._chunk = sizes.pop() if len(sizes) == 1 else None     # uniform minibatch size (graphable)
-        self.grad_weight = (T * n_local) / (T * self.n_envs_global) if self.sync_grads else 1.0
+        # minibatch j's gradient is weighted by this rank's share of the global minibatch j,
+        # s_r(j) / sum_r' s_r'(j) (every rank's chunk sizes follow from the agreed counts), so the
+        # summed bucket is the mean over the global minibatch for even and uneven shards alike
+        self._mb_weight = (minibatch_weights(counts, self.rank, T, self.n_minibatches)
+                           if self.sync_grads and world > 1 else [1.0] * self.n_minibatches)
+        self.grad_weight = self._mb_weight[0]
 
     def _agree_stop(self, stop):
         """Every rank leaves learn() at the same iteration (a callback may stop one rank only)."""
@@ -482,7 +499,8 @@ class PPO:
         stats = []
         for epoch in range(self.n_epochs):
             perm = torch.randperm(M, device=self.device)
-            for s, e in zip(self._mb_bounds, self._mb_bounds[1:]):
+            for j, (s, e) in enumerate(zip(self._mb_bounds, self._mb_bounds[1:])):
+                self.grad_weight = self._mb_weight[j]
                 loss, pg, vf = self._minibatch_loss(obs, act, old_logp, adv, ret, perm[s:e])
                 self.opt.zero_grad(set_to_none=True)
                 loss.backward()
@@ -520,8 +538,9 @@ class PPO:
         src = (b["obs"].view(M, -1), b["act"].view(M, -1), b["logp"].view(-1), self._g_adv, self._g_ret)
         params = list(self.policy.parameters())
 
-        sync, w = self.sync_grads, float(self.grad_weight)
+        sync = self.sync_grads
         self._g_flat = torch.zeros(sum(p.numel() for p in params), dtype=torch.float32, device=dev) if sync else None
+        self._g_w = torch.full((1,), float(self._mb_weight[0]), dtype=torch.float32, device=dev)
 
         def g1_body():
             loss, pg, vf = self._minibatch_loss(*src, self._g_idx)
@@ -529,7 +548,7 @@ class PPO:
             self._g_stats.add_(torch.stack([pg.detach(), vf.detach()]))
             if sync:                     # the weighted gradient bucket the eager all-reduce sends
                 torch.cat([p.grad.reshape(-1) for p in params], out=self._g_flat)
-                self._g_flat.mul_(w)
+                self._g_flat.mul_(self._g_w)     # minibatch weight, refreshed before each replay
 
         def g2_body():
             if sync:                     # summed bucket back into the .grad tensors
@@ -592,8 +611,10 @@ class PPO:
         n = 0
         for epoch in range(self.n_epochs):
             perm = torch.randperm(M, device=self.device)
-            for s, e in zip(self._mb_bounds, self._mb_bounds[1:]):
+            for j, (s, e) in enumerate(zip(self._mb_bounds, self._mb_bounds[1:])):
                 self._g_idx.copy_(perm[s:e])
+                if self.sync_grads:
+                    self._g_w.fill_(self._mb_weight[j])
                 g1.replay()
                 if self.sync_grads:
                     self._allreduce_flat(self._g_flat)

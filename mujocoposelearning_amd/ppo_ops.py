@@ -23,7 +23,7 @@ class _SplitKLinearFn(torch.autograd.Function):
     """y = x W^T + b whose weight gradient is computed as S batched [out x rows] x [rows x in]
     products summed over S, instead of one GEMM with a K = batch-size reduction.  The library's
     kernel for a 256 x 32768 x 352 weight gradient runs at a few TFLOP/s (one long reduction on few
-    tiles); split into 16 slices it fills the chip (tests/gpu_mlp_probe.py: minibatch fwd+bwd
+    tiles); split into 16 slices it fills the chip (tools/probes/gpu_mlp_probe.py: minibatch fwd+bwd
     1.45 -> 0.97 ms at 32768 samples)."""
 
     @staticmethod

@@ -24,7 +24,9 @@ import copy
 
 import numpy as np
 
+from . import _lib
 from . import reward_functions as _rf
+from ._lib import HsimError
 from .batch import HsBatch
 from .model import HsModel
 from .spaces import Box
@@ -323,12 +325,16 @@ class _HostViews:
 
     def __init__(self, batch, model):
         self.m = model
+        need = _lib.HS_OUT_AUX | _lib.HS_OUT_CTRL
+        if (batch.cfg.outputs & need) != need:
+            raise HsimError("host reward views need the aux row and the ctrl copy (HsBatch.configure(aux=True, ctrl=True))")
         self.qpos = batch.qpos.double().cpu().numpy()
         self.qvel = batch.qvel.double().cpu().numpy()
         self.ctrl = batch.ctrl.double().cpu().numpy()
         self.time = batch.time.double().cpu().numpy()
         self.obs = batch.obs.double().cpu().numpy()
         self.com = batch.aux[:, 32:35].double().cpu().numpy()
+        self.parent = None
         fs = batch.full_state
         self.cfrc = batch.cfrc_ext.double().cpu().numpy() if fs else None
         self.linv = batch.subtree_linvel.double().cpu().numpy() if fs else None
@@ -338,11 +344,14 @@ class _HostViews:
         m = self.m
         o2 = (m.nq - 2) + m.nv
         o3, o4 = o2 + 10 * m.nbody, o2 + 16 * m.nbody
-        com = np.full((m.nbody, 3), np.nan)
-        com[0] = com[1] = self.com[i]
+        from .env import subtree_com_from_cinert
+        if self.parent is None:
+            self.parent = m.field("body_parentid").astype(int)
+        cinert = self.obs[i, o2:o3].reshape(m.nbody, 10)
+        com = subtree_com_from_cinert(cinert, self.com[i], self.parent)
         return SimpleNamespace(
             qpos=self.qpos[i], qvel=self.qvel[i], ctrl=self.ctrl[i], time=float(self.time[i]),
-            cinert=self.obs[i, o2:o3].reshape(m.nbody, 10), cvel=self.obs[i, o3:o4].reshape(m.nbody, 6),
+            cinert=cinert, cvel=self.obs[i, o3:o4].reshape(m.nbody, 6),
             qfrc_actuator=self.obs[i, o4:o4 + m.nv], subtree_com=com,
             cfrc_ext=self.cfrc[i] if self.cfrc is not None else np.zeros((m.nbody, 6)),
             subtree_linvel=self.linv[i] if self.linv is not None else np.zeros((m.nbody, 3)))

@@ -107,3 +107,27 @@ def test_worker_reset_streams_golden():
         for k in range(3):
             assert np.array_equal(r.uniform(low=-0.01, high=0.01, size=28), g[f"stream_pos_{100 + i}_{k}"])
             assert np.array_equal(r.uniform(low=-0.01, high=0.01, size=27), g[f"stream_vel_{100 + i}_{k}"])
+
+
+def test_subtree_com_from_cinert_matches_oracle_every_body():
+    """HsData.subtree_com (every body, MuJoCo mj_comPos) is rebuilt from the forward pass's cinert
+    and the root COM; against the oracle's own per-body subtree_com on random poses."""
+    from mujocoposelearning_amd.env import subtree_com_from_cinert
+    from oracle.oracle import Oracle
+    from mujocoposelearning_amd.model import HUMANOID_XML
+    o = Oracle(HUMANOID_XML)
+    nb = o.M["nbody"]
+    parent = np.array(o.M["body_parentid"][:nb], int)
+    rng = np.random.default_rng(3)
+    for _ in range(5):
+        q = o.M["qpos0"].copy()
+        q[:3] += rng.uniform(-0.5, 0.5, 3)
+        quat = rng.normal(size=4)
+        q[3:7] = quat / np.linalg.norm(quat)
+        q[7:] += rng.uniform(-0.5, 0.5, q.size - 7)
+        o.qpos[:] = q
+        o.forward()
+        ref = o.get("subtree_com")
+        got = subtree_com_from_cinert(o.get("cinert"), ref[0], parent)
+        assert got.shape == ref.shape == (nb, 3)
+        assert np.abs(got - ref).max() < 1e-12

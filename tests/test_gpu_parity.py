@@ -213,6 +213,10 @@ def test_reset_noise_host_supplied_matches_oracle_env(model):
     assert (term, trunc) == (rterm, rtrunc) == (False, False)
     assert set(info) == {"reward_components", "height", "step_count", "truncated", "truncation_info", "terminated",
                          "total_reward"}
+    # the plug-in data view's subtree_com: every body, as MuJoCo's mj_comPos fills it
+    com, rcom = env.data.subtree_com, ref.sim.get("subtree_com")
+    assert com.shape == rcom.shape == (17, 3) and np.isfinite(com).all()
+    assert np.abs(com - rcom).max() <= 1e-9
     env.close()
 
 

@@ -148,6 +148,13 @@ def test_physics_step_refuses_stale_ctrl(model):
     b.set_state(ctrl=0.5)                                # rewriting ctrl makes it valid again
     b.physics_step(None, 1)
     assert np.allclose(b.get_state()["ctrl"], 0.5)
+    # ctrl copy off for a step, back on for the next: that step rewrites data.ctrl, so it is valid
+    b.configure(ctrl=False)
+    b.step(torch.zeros(4, 21, device=b.device))
+    b.configure(ctrl=True)
+    b.step(torch.full((4, 21), 0.25, device=b.device))
+    assert np.allclose(b.get_state()["ctrl"], 0.25)
+    b.physics_step(None, 1)
 
 
 @pytest.mark.parametrize("prec", ["fp64", "fp32"])

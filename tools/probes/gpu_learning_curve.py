@@ -1,0 +1,45 @@
+"""Learning-curve sanity of the on-device PPO (SB3 is not importable, so the trainer
+is judged by the stand reward rising).  bench.py's train config: 4096 envs, n_steps 32,
+batch 32768, 4 epochs, lr 3e-4, MLP[256,256] ReLU.
+python tools/probes/gpu_learning_curve.py [iters] [stand|kneeling] [fp32|fp64] [seed]"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from mujocoposelearning_amd.model import HsModel  # noqa: E402
+from mujocoposelearning_amd.ppo import PPO  # noqa: E402
+from mujocoposelearning_amd.vec_env import HumanoidVecEnv  # noqa: E402
+
+XML = os.path.join(ROOT, "mujocoposelearning_amd", "assets", "humanoid.xml")
+
+
+def main(iters=400, reward="stand", precision="fp32", seed=0):
+    env = HumanoidVecEnv({"model_path": XML, "duration": 10.0, "reward_config": {"type": reward}, "frame_skip": 3},
+                         n_envs=4096, model=HsModel(XML), seed=seed, precision=precision)
+    ppo = PPO(env, n_steps=32, batch_size=32768, n_epochs=4, learning_rate=3e-4, seed=seed,
+              policy_kwargs={"activation_fn": "ReLU", "net_arch": {"pi": [256, 256], "vf": [256, 256]}})
+    t0 = time.perf_counter()
+    rows = []
+    for it in range(1, iters + 1):
+        adv, ret = ppo.collect_rollouts()
+        r_step = float(ppo.buf["rew"].mean())
+        h = float(ppo.buf["obs"][..., 0].mean())          # obs[0] = qpos[2], the torso height
+        st = ppo.train(adv, ret)
+        if it % max(1, iters // 20) == 0 or it == 1:
+            ep = float(np.mean(ppo.ep_returns[-200:])) if ppo.ep_returns else float("nan")
+            rows.append((it, ppo.num_timesteps, r_step, h, ep, st["value_loss"], time.perf_counter() - t0))
+            print(f"iter {it:4d} steps {ppo.num_timesteps / 1e6:6.1f}M  mean step reward {r_step:.4f}  "
+                  f"mean height {h:.3f}  ep return (last 200) {ep:8.2f}  vf loss {st['value_loss']:.4f}  "
+                  f"{time.perf_counter() - t0:6.1f}s", flush=True)
+    env.close()
+    return rows
+
+
+if __name__ == "__main__":
+    main(int(sys.argv[1]) if len(sys.argv) > 1 else 400, sys.argv[2] if len(sys.argv) > 2 else "stand",
+         sys.argv[3] if len(sys.argv) > 3 else "fp32", int(sys.argv[4]) if len(sys.argv) > 4 else 0)
