@@ -37,6 +37,13 @@ enum { ST_KIN = 0, ST_COM, ST_TENDON, ST_CRB, ST_COLLISION, ST_CONSTRAINT, ST_CO
 #define MINIMP 0.0001
 #define MAXIMP 0.9999
 
+/* Known-WRONG physics switches for the reference-trajectory power test (oracle/trajfit.py), 0 =
+ * the restatement.  1: pyramidal R without MuJoCo's 2 mu^2 / impratio scale; 2: Euler without the
+ * implicit damping (H = M instead of M + h B); 4: friction mixed by min instead of max;
+ * 8: Newton stopped by MuJoCo's tolerance rule (scale * improvement or scale * |grad| below
+ * opt.tolerance) instead of at the exact active set -- not wrong, a sensitivity check. */
+int orc_variant = 0;
+
 int orc_sizeof_model(void) { return (int)sizeof(OrcModel); }
 int orc_sizeof_data(void) { return (int)sizeof(OrcData); }
 
@@ -398,7 +405,9 @@ static void contact_param(const OrcModel* m, OrcContact* c, int g1, int g2) {
     memcpy(c->solimp, m->geom_solimp[g], sizeof c->solimp);
   } else {
     c->dim = m->geom_condim[g1] > m->geom_condim[g2] ? m->geom_condim[g1] : m->geom_condim[g2];
-    for (int k = 0; k < 3; k++) fr[k] = fmax(m->geom_friction[g1][k], m->geom_friction[g2][k]);
+    for (int k = 0; k < 3; k++)
+      fr[k] = (orc_variant & 4) ? fmin(m->geom_friction[g1][k], m->geom_friction[g2][k])
+                                : fmax(m->geom_friction[g1][k], m->geom_friction[g2][k]);
     double s1 = m->geom_solmix[g1], s2 = m->geom_solmix[g2], mix;
     if (s1 >= MINVAL && s2 >= MINVAL) mix = s1 / (s1 + s2);
     else if (s1 < MINVAL && s2 < MINVAL) mix = 0.5;
@@ -576,7 +585,7 @@ static void make_constraint(const OrcModel* m, OrcData* d) {
        * scaled by 1 the inferred pre-step velocities leave the reset-noise box, only factors in
        * [1.95, 2.15] keep all 27 inside it. */
       double mu = d->contact[id].friction[0];
-      d->efc_R[r] *= 2 * mu * mu / m->impratio;
+      if (!(orc_variant & 1)) d->efc_R[r] *= 2 * mu * mu / m->impratio;
     }
     d->efc_D[r] = 1 / d->efc_R[r];
   }
@@ -765,6 +774,16 @@ static void solve_newton(const OrcModel* m, OrcData* d) {
     double improvement = cost - newcost;
     cost = newcost;
     if (same || scale * improvement < 1e-16) { it++; break; }
+    if (orc_variant & 8) {                        /* MuJoCo's stop: improvement or gradient below tol */
+      double g2 = 0;
+      for (int i = 0; i < nv; i++) {
+        double t = 0;
+        for (int k = 0; k < nv; k++) t += d->qM[i][k] * (x[k] - d->qacc_smooth[k]);
+        for (int r = 0; r < ne; r++) if (jar[r] < 0) t += d->efc_D[r] * jar[r] * d->efc_J[r][i];
+        g2 += t * t;
+      }
+      if (scale * improvement < m->tolerance || scale * sqrt(g2) < m->tolerance) { it++; break; }
+    }
   }
   d->solver_niter = it;
   memcpy(d->qacc, x, sizeof(double) * nv);
@@ -881,7 +900,8 @@ static void euler(const OrcModel* m, OrcData* d) {
   double h = m->timestep, f[OMAXV], a[OMAXV];
   static double H[OMAXV][OMAXV], L[OMAXV][OMAXV];
   memcpy(H, d->qM, sizeof H);
-  for (int i = 0; i < nv; i++) H[i][i] += h * m->dof_damping[i];
+  if (!(orc_variant & 2))
+    for (int i = 0; i < nv; i++) H[i][i] += h * m->dof_damping[i];
   for (int i = 0; i < nv; i++) f[i] = d->qfrc_smooth[i] + d->qfrc_constraint[i];
   chol(L, H, nv);
   chol_solve(a, L, f, nv);

@@ -398,3 +398,33 @@ def test_pgs_stopping_rule_and_option_parsing(tmp_path):
     bad.write_text(src.replace('<option timestep="0.005"/>', '<option timestep="0.005" solver="CG"/>'))
     with pytest.raises(ValueError, match="solver"):
         compile_mjcf(str(bad))
+
+
+def test_newton_tolerance_stop_gives_the_exact_trajectory():
+    """MuJoCo's Newton also stops when scale*improvement or scale*|grad| falls below opt.tolerance
+    (1e-8); the oracle (and the kernel) stop at the exact active set.  With the exact line search the
+    tolerance rule never fires first: the oracle run with it (orc_variant bit 8) is bitwise the same
+    over 300 substeps of random torques with contacts.  (MuJoCo's own line search is inexact; that
+    part of its iteration is not restated.)"""
+    from oracle import trajfit as T
+    from oracle.oracle import Oracle
+    M = T.make_model(XML)
+    a, b = Oracle(M=M), Oracle(M=M)
+    rng = np.random.default_rng(0)
+    noise = rng.uniform(-0.01, 0.01, 27)
+    for o in (a, b):
+        o.reset_data()
+        o.qpos[2] = 1.282
+        o.qvel[:] = noise
+    try:
+        for n in range(300):
+            if n % 3 == 0:
+                u = rng.uniform(-1, 1, 21)
+            T.set_variant(0)
+            a.step(u, 1)
+            T.set_variant(8)
+            b.step(u, 1)
+            assert np.array_equal(a.qpos, b.qpos) and np.array_equal(a.qvel, b.qvel), n
+    finally:
+        T.set_variant(0)
+    assert a.d.ncon > 0 or np.abs(a.qpos[2]) < 1.0      # it reached the floor

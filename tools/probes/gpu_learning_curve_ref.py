@@ -1,0 +1,65 @@
+"""Learning curve under the reference's own PPO hyperparameters (README.md:23-53): lr 5e-5,
+n_steps 2048 x 8 envs = 16 384 samples per rollout, batch 128, 10 epochs, gamma 0.99, lambda 0.95,
+clip 0.2, ent_coef 0.002, MLP[256,256] ReLU, 'stand', frame_skip 3, duration 10 s
+(train_sb3.py:183-200), 20 M env steps.  The 16 384 samples per rollout are spread over more envs
+(``--envs`` x ``--n-steps``, default 128 x 128) so a run fits one GPU call; pass ``--envs 8
+--n-steps 2048`` for the literal layout.  fp64 env (the reference's arithmetic).
+
+python tools/probes/gpu_learning_curve_ref.py --seed 0 [--envs 128 --n-steps 128 --steps 20e6]
+Prints one progress line per ``--every`` iterations: env steps, SB3's ep_rew_mean over the last 100
+episodes (every stand episode runs 667 steps: termination is time >= duration, custom_env.py), the
+fraction of the rollout's steps with the torso above 1.0 m ("upright") and the mean torso height."""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from mujocoposelearning_amd.model import HUMANOID_XML, HsModel  # noqa: E402
+from mujocoposelearning_amd.ppo import PPO  # noqa: E402
+from mujocoposelearning_amd.train import env_config_from_kwargs  # noqa: E402
+from mujocoposelearning_amd.vec_env import HumanoidVecEnv  # noqa: E402
+
+PPO_KWARGS = dict(learning_rate=5e-5, batch_size=128, n_epochs=10, gamma=0.99, gae_lambda=0.95, clip_range=0.2,
+                  ent_coef=0.002, policy_kwargs={"activation_fn": "ReLU", "net_arch": {"pi": [256, 256], "vf": [256, 256]}})
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--envs", type=int, default=128)
+    ap.add_argument("--n-steps", type=int, default=128)
+    ap.add_argument("--steps", type=float, default=20e6)
+    ap.add_argument("--precision", default="fp64")
+    ap.add_argument("--reward", default="stand")
+    ap.add_argument("--every", type=int, default=20)
+    a = ap.parse_args()
+    cfg = env_config_from_kwargs({"reward_function": a.reward, "frame_skip": 3}, HUMANOID_XML)
+    env = HumanoidVecEnv(cfg, n_envs=a.envs, model=HsModel(HUMANOID_XML), seed=a.seed, precision=a.precision)
+    env.batch.configure(aux=False, ctrl=False)
+    ppo = PPO(env, n_steps=a.n_steps, seed=a.seed, **PPO_KWARGS)
+    t0 = time.perf_counter()
+    it = 0
+    while ppo.num_timesteps < a.steps:
+        adv, ret = ppo.collect_rollouts()
+        h = ppo.buf["obs"][..., 0]                     # obs[0] = qpos[2], the torso height
+        upright = float((h > 1.0).float().mean())
+        hmean = float(h.mean())
+        st = ppo.train(adv, ret)
+        it += 1
+        if it % a.every == 0 or ppo.num_timesteps >= a.steps:
+            ep = float(np.mean(ppo.ep_returns[-100:])) if ppo.ep_returns else float("nan")
+            print(f"seed {a.seed} iter {it:5d} steps {ppo.num_timesteps / 1e6:7.3f}M ep_rew_mean {ep:8.2f} "
+                  f"episodes {len(ppo.ep_returns):6d} upright {upright:.3f} height {hmean:.3f} "
+                  f"vf_loss {st['value_loss']:.3f} log_std {float(ppo.policy.log_std.mean()):.3f} "
+                  f"{time.perf_counter() - t0:7.1f}s", flush=True)
+    env.close()
+
+
+if __name__ == "__main__":
+    torch.backends.cuda.matmul.allow_tf32 = False
+    main()
