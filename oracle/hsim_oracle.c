@@ -29,8 +29,15 @@
 #ifndef ORC_NSTAGE
 #define ORC_STAGE(k) ((void)0)
 #endif
+/* solver sub-phases, separated only in the precision-emulating build (oracle/precemu.h) */
+#ifdef ORC_PREC_SUBSTAGES
+#define ORC_SUBSTAGE(k) ORC_STAGE(k)
+#else
+#define ORC_SUBSTAGE(k) ((void)0)
+#endif
 enum { ST_KIN = 0, ST_COM, ST_TENDON, ST_CRB, ST_COLLISION, ST_CONSTRAINT, ST_COMVEL, ST_PASSIVE, ST_REFERENCE,
-       ST_RNE, ST_ACTUATION, ST_SMOOTH, ST_SOLVER, ST_EULER, ST_OTHER };
+       ST_RNE, ST_ACTUATION, ST_SMOOTH, ST_SOLVER, ST_EULER, ST_OTHER, ST_SOLVER_HESS, ST_SOLVER_CHOL,
+       ST_SOLVER_LS };
 
 #define MINVAL 1e-15
 #define MAXVAL 1e10
@@ -749,26 +756,33 @@ static void solve_newton(const OrcModel* m, OrcData* d) {
       for (int k = 0; k < nv; k++) t += d->qM[i][k] * (x[k] - d->qacc_smooth[k]);
       g[i] = t;
     }
+    ORC_SUBSTAGE(ST_SOLVER_HESS);
     memcpy(H, d->qM, sizeof H);
     for (int r = 0; r < ne; r++) {
       if (!act[r]) continue;
       double Dr = d->efc_D[r], *Jr = d->efc_J[r];
       for (int i = 0; i < nv; i++) {
+        ORC_SUBSTAGE(ST_SOLVER);
         g[i] += Dr * jar[r] * Jr[i];
+        ORC_SUBSTAGE(ST_SOLVER_HESS);
         if (Jr[i] == 0) continue;
         for (int k = 0; k <= i; k++) H[i][k] += Dr * Jr[i] * Jr[k];
       }
     }
     for (int i = 0; i < nv; i++) for (int k = i + 1; k < nv; k++) H[i][k] = H[k][i];
+    ORC_SUBSTAGE(ST_SOLVER);
     double gn = 0;
     for (int i = 0; i < nv; i++) gn += g[i] * g[i];
     if (scale * sqrt(gn) < 1e-14) break;
+    ORC_SUBSTAGE(ST_SOLVER_CHOL);
     if (chol(L, H, nv)) break;
     chol_solve(s, L, g, nv);
     for (int i = 0; i < nv; i++) s[i] = -s[i];
+    ORC_SUBSTAGE(ST_SOLVER_LS);
     double alpha = line_search(m, d, x, s, jar, Js);
     for (int i = 0; i < nv; i++) x[i] += alpha * s[i];
     double newcost = eval_cost(m, d, x, jar);
+    ORC_SUBSTAGE(ST_SOLVER);
     int same = 1;
     for (int r = 0; r < ne; r++) if ((jar[r] < 0) != act[r]) { same = 0; break; }
     double improvement = cost - newcost;

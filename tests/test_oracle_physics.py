@@ -428,3 +428,63 @@ def test_newton_tolerance_stop_gives_the_exact_trajectory():
     finally:
         T.set_variant(0)
     assert a.d.ncon > 0 or np.abs(a.qpos[2]) < 1.0      # it reached the floor
+
+
+def test_fp32_state_storage_alone_breaks_the_1e4_bound_through_contact_flips():
+    """Why the fp32 engine cannot hold the north star's < 1e-4 over 1000 substeps:
+    the fp64 oracle with NOTHING but its state rounded to fp32 after every substep (exact arithmetic
+    otherwise) already drifts to ~2e-4 by smooth amplification of that rounding, and then a resting
+    contact at distance ~0 (a capsule end-point at -1.7e-6) is in one run's contact set and not the
+    other's: from that substep on the runs differ by > 1e-3.  Zero tape, the initial state of
+    tools/probes/parity_report.py seed 1 (first flip at substep 375)."""
+    from oracle.oracle import Oracle
+    _oracle = lambda: Oracle(XML)  # noqa: E731
+    o = _oracle()
+    rng = np.random.default_rng(1)
+    q = o.M["qpos0"].copy()
+    q[2], q[3:7] = 1.282, [1, 0, 0, 0]
+    q += rng.uniform(-0.01, 0.01, 28) * np.r_[1, 1, 0.1, 0, 0, 0, 0, np.ones(21)]
+    v = rng.uniform(-0.01, 0.01, 27)
+    a, b = _oracle(), _oracle()
+    a.qpos[:], a.qvel[:] = q, v
+    b.qpos[:], b.qvel[:] = q.astype(np.float32), v.astype(np.float32)
+    first_flip, before, worst = None, 0.0, 0.0
+    for s in range(1000):
+        a.step(np.zeros(21), 1)
+        b.step(np.zeros(21), 1)
+        b.qpos[:] = b.qpos.astype(np.float32)
+        b.qvel[:] = b.qvel.astype(np.float32)
+        d = float(np.abs(a.qpos - b.qpos).max())
+        if first_flip is None and (a.d.ncon, a.d.nefc) != (b.d.ncon, b.d.nefc):
+            first_flip = s
+        if first_flip is None:
+            before = max(before, d)
+        worst = max(worst, d)
+    assert first_flip is not None
+    assert before < 1e-3           # fp32-storage round-off, amplified smoothly, until the flip
+    assert worst > 1e-3 and worst > 10 * before      # ... and a jump past the north star's bound
+
+
+def test_precision_emulation_build_mask0_is_the_oracle_bitwise():
+    """oracle/precision.py (the restatement with chosen stages rounded to fp32) with no stage
+    selected steps bitwise like the plain build, so its per-stage results isolate rounding."""
+    from oracle import precision as P
+    from oracle.oracle import Oracle
+    a, b = Oracle(XML), P.PrecOracle(XML)
+    rng = np.random.default_rng(2)
+    v = rng.uniform(-0.5, 0.5, 27)
+    for o in (a, b):
+        o.qpos[2] = 1.25
+        o.qvel[:] = v
+    P.set_mask(0)
+    for _ in range(60):
+        u = rng.uniform(-1, 1, 21)
+        a.step(u, 1)
+        b.step(u, 1)
+    assert np.array_equal(a.qpos, b.qpos) and np.array_equal(a.qvel, b.qvel)
+    P.set_mask(P.ALL)
+    b.step(u, 1)
+    a.step(u, 1)
+    P.set_mask(0)
+    d = np.abs(a.qvel - b.qvel).max()
+    assert 0 < d < 1e-2 * (1 + np.abs(a.qvel).max())       # fp32 arithmetic: close, not equal

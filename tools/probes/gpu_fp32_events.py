@@ -1,0 +1,64 @@
+"""Where the fp32 engine leaves the fp64 oracle on the zero tape: step the GPU fp32
+engine and the fp64 oracle side by side (seeds 0-2 of tools/probes/parity_report.py, 1000 substeps),
+and print every substep where |dqpos| grows by > 3x or the contact / row counts differ (GPU aux row
+vs oracle), up to the first jump above 1e-4.  Also the fp64 oracle with its state rounded to fp32
+after every substep (an fp32-STORAGE engine with exact arithmetic) for comparison.
+
+python tools/probes/gpu_fp32_events.py > gpurun_out/fp32_events.md
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import torch  # noqa: E402
+
+from mujocoposelearning_amd.batch import HsBatch  # noqa: E402
+from mujocoposelearning_amd.model import HsModel  # noqa: E402
+from oracle.oracle import Oracle  # noqa: E402
+from parity_report import XML, initial  # noqa: E402
+
+
+def main():
+    model = HsModel(XML)
+    for seed in (0, 1, 2):
+        o = Oracle(XML)
+        q, v, _ = initial(o, seed)
+        o.qpos[:] = q
+        o.qvel[:] = v
+        s32 = Oracle(XML)
+        s32.qpos[:] = q.astype(np.float32)
+        s32.qvel[:] = v.astype(np.float32)
+        b = HsBatch(model, 1, precision="fp32")
+        b.set_state(qpos=q, qvel=v, time=0.0, qacc_warmstart=0.0)
+        zero = torch.zeros(1, 21, device=b.device)
+        print(f"\n## seed {seed}\n\n| substep | GPU fp32 max dqpos | GPU ncon / nefc | oracle ncon / nefc | fp32-storage oracle max dqpos |")
+        print("|---|---|---|---|---|")
+        prev, worst, stor = 0.0, 0.0, 0.0
+        reported = 0
+        for s in range(1000):
+            b.physics_step(zero, 1)
+            o.step(np.zeros(21), 1)
+            s32.step(np.zeros(21), 1)
+            s32.qpos[:] = s32.qpos.astype(np.float32)
+            s32.qvel[:] = s32.qvel.astype(np.float32)
+            gq = b.qpos[0].double().cpu().numpy()
+            aux = b.aux[0].double().cpu().numpy()
+            d = float(np.abs(gq - o.qpos).max())
+            stor = max(stor, float(np.abs(s32.qpos - o.qpos).max()))
+            gc, ge = int(aux[35]), int(aux[36])
+            flip = (gc, ge) != (o.d.ncon, o.d.nefc)
+            if (d > 3 * prev + 1e-9 or flip) and reported < 40 and worst <= 1e-4:
+                print(f"| {s} | {d:.2e} | {gc} / {ge} | {o.d.ncon} / {o.d.nefc} | {stor:.1e} |", flush=True)
+                reported += 1
+            prev = max(prev, d)
+            worst = max(worst, d)
+        print(f"\nseed {seed}: GPU fp32 max |dqpos| over 1000 substeps {worst:.2e}; fp32-storage oracle {stor:.2e}")
+        b.close()
+
+
+if __name__ == "__main__":
+    main()
