@@ -90,8 +90,6 @@ struct StepParams {
   int qorder;            // chunk queue: 1 = cost-ordered claims (QNB buckets), 0 = the qmul permutation only
   int dbg_lose_pair1;    // test hook (hs_debug_lose_handoff): pair + 1 whose hand-off is treated as lost; 0 = off
   int single;            // set by launch_step: 1 = one env per wave (upper half-wave a ghost), 0 = env pairs
-  int newton_incr;       // fp64 Newton: 1 = incremental factor after the first iteration, 0 = rebuild H every
-                         // iteration (HSIM_NEWTON_REBUILD=1 at batch creation: A/B runs)
 };
 // hs_env_config.schedule (SCHED_FIXED_ORDER: AUTO with the chunk queue's claims in the fixed
 // permutation instead of cost order -- A/B runs and tests)

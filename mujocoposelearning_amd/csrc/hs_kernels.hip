@@ -59,62 +59,25 @@ using Wide = Cap<MAXCON_WIDE, MAXEFC_WIDE, true>;
 // engine, bit 1 the fp64 engine).  A/B, ms per configs[1] launch: fp64 0.720 -> 0.714 (with the
 // normal-range sqrt below 0.701); fp32 0.423 -> 0.433 (2 waves per SIMD hide the LDS round trip,
 // and the extra VALU ops cost issue slots): fp64 only.
-#ifndef HS_CHOL_DPP
-#define HS_CHOL_DPP 2
-#endif
 // contact aggregates over a contact's rows as straight-line code: all LDS operands read up front
 // instead of a row loop whose every iteration waits on its own reads (fp64 0.662 -> 0.634 ms per
 // configs[1] launch)
-#ifndef HS_AGGR_STATIC
-#define HS_AGGR_STATIC 1
-#endif
 // fp64 1/x as rcp + one cubic correction (e + e^2) instead of two Newton steps: 4 dependent
 // operations instead of 5, the same ~1 ulp (0.662 -> 0.656 ms)
-#ifndef HS_RECIP3
-#define HS_RECIP3 1
-#endif
 // fp64 1/sqrt without the denormal / class handling of the library sqrt (development A/B knob)
-#ifndef HS_SQRT_FAST
-#define HS_SQRT_FAST 2
-#endif
 // CRB and Newton-Hessian rows software-pipelined: the next column (group)'s LDS reads are issued
 // before the current one's arithmetic, behind the per-column scheduling fence, so each LDS round trip
 // overlaps the previous column's FMAs (A/B, fp64 ms per configs[1] launch: 0.681 -> CRB 0.674,
 // Hessian 0.661, both 0.659; the fp64 queue kernel drops from 510 to 482 unified registers)
-#ifndef HS_CRB_AHEAD
-#define HS_CRB_AHEAD 1
-#endif
-#ifndef HS_HESS_AHEAD
-#define HS_HESS_AHEAD 1
-#endif
 // Cholesky, per precision (bit 0 fp32, bit 1 fp64): trailing-column LDS reads issued before the pivot math, behind a
 // scheduling fence (the machine scheduler otherwise sinks the column publish and its read-back below
 // the pivot chain, exposing the LDS round trip): 0.691 -> 0.682 ms per fp64 configs[1] launch; fp32
 // (pivots from LDS too, so one round trip instead of two): 0.390 -> 0.387 ms
-#ifndef HS_CHOL_EARLY
-#define HS_CHOL_EARLY 3
-#endif
-// M·v with two accumulators (development A/B knob)
-#ifndef HS_MATVEC_SPLIT
-#define HS_MATVEC_SPLIT 0
-#endif
-// per-loop scheduling fences (development A/B knobs; 1 = fenced)
-#ifndef HS_FENCE_CHOL
-#define HS_FENCE_CHOL 1
-#endif
-#ifndef HS_FENCE_CRB
-#define HS_FENCE_CRB 1
-#endif
-#ifndef HS_FENCE_HESS
-#define HS_FENCE_HESS 1
-#endif
+// M·v with two accumulators: no change.  Removing the per-loop scheduling fences
+// costs 1136 / 564 B/lane of scratch (Cholesky / CRB).
 // columns per scheduling group in the Hessian / CRB row loops (A/B, fp64 configs[1] ms per launch:
 // Hessian 2 columns 0.720 vs 1 column 0.724, 3 spill; CRB 2 or 3 columns: no change)
 // (the fp32 engine at 2 waves per SIMD has no registers for a second column: 148 B/lane of scratch)
-#ifndef HS_CRB_G
-#define HS_CRB_G 1
-#endif
-constexpr int CRB_G = HS_CRB_G;
 
 // single-wave workgroup: LDS ops of a wave execute in order, so a compiler-only barrier suffices to
 // keep LDS accesses from moving across phase boundaries (no s_barrier, and no s_waitcnt that a
@@ -193,15 +156,12 @@ __device__ __forceinline__ uint32_t hballot(bool p, bool upper) {
   uint64_t m = __ballot(p);
   return upper ? (uint32_t)(m >> 32) : (uint32_t)m;
 }
-// f(j, ld(j)) for each set bit j of mk, ascending (the chain / subtree sums).  HS_BITS_AHEAD (per
-// precision: bit 0 fp32, bit 1 fp64; development A/B knob): the loads of the next bit's operands are
-// issued before the current bit's arithmetic, so one LDS round trip overlaps the FMAs (the same
-// operations in the same order).  Measured slower in both engines (fp64 0.697 vs 0.691 ms, fp32 0.411
-// vs 0.408 ms per configs[1] launch): off.
-#ifndef HS_BITS_AHEAD
-#define HS_BITS_AHEAD 0
-#endif
-template <typename T, bool AHEAD = (HS_BITS_AHEAD & (sizeof(T) == 8 ? 2 : 1)) != 0, typename LD, typename F>
+// f(j, ld(j)) for each set bit j of mk, ascending (the chain / subtree sums).  AHEAD: the loads of the
+// next bit's operands are issued before the current bit's arithmetic, so one LDS round trip overlaps
+// the FMAs (the same operations in the same order) -- the contact loops take it; for the chain /
+// subtree sums it measured slower in both engines (fp64 0.697 vs 0.691 ms, fp32 0.411 vs 0.408 ms
+// per configs[1] launch).
+template <typename T, bool AHEAD = false, typename LD, typename F>
 __device__ __forceinline__ void for_bits(uint32_t mk, LD&& ld, F&& f) {
   if constexpr (AHEAD) {
     if (mk == 0u) return;
@@ -327,43 +287,17 @@ __device__ __forceinline__ float rsqrt_t<float>(float x) { return __builtin_amdg
 __device__ __forceinline__ float recip(float x) { return 1.0f / x; }
 __device__ __forceinline__ double recip(double x) {
   double y = __builtin_amdgcn_rcp(x);
-#if HS_RECIP3
   // y (1 + e + e^2) with e = 1 - x y: relative error cubed in one step (4 dependent operations)
   const double e = fma(-x, y, 1.0);
   return fma(fma(e, e, e), y, y);
-#else
-  double e = fma(-x, y, 1.0);
-  y = fma(y, e, y);
-  e = fma(-x, y, 1.0);
-  return fma(y, e, y);
-#endif
 }
 // fp64 1/sqrt(x), x >= 1e-30 at every call site (the Cholesky pivots are clamped to it, the
 // normalizations branch below it), so no denormal scaling or zero / infinity class check:
-//   HS_SQRT_FAST 2 (product): v_rsq_f64, one Goldschmidt step (h ~ 1/(2 sqrt x)), one Newton step on
-//     y = 2h -- within ~1 ulp, 7 dependent operations;
-//   1: the library's sqrt sequence without its scaling / class check, then recip() (13);
-//   0: recip(sqrt(x)) (18).
-// A/B, fp64 ms per configs[1] launch (with the DPP pivots of chol_rows): 0 0.714, 1 0.701, 2 0.690.
-// (Round 2 measured a v_rsq_f64 + two-Newton-step variant slower, 305k vs 298k cycles per env
-// substep, under the default machine scheduler.)
-#if HS_SQRT_FAST
-// sqrt for x in the normal range (every caller clamps x >= 1e-30): the compiler's sqrt sequence
-// (v_rsq_f64, one Goldschmidt step, two Newton corrections) without its denormal scaling and its
-// zero / infinity class check -- the same arithmetic for these x, five fewer dependent operations
-__device__ __forceinline__ double sqrt_normal(double x) {
-  double y = __builtin_amdgcn_rsq(x);
-  double g = x * y, h = 0.5 * y;
-  const double r = fma(-h, g, 0.5);
-  g = fma(g, r, g);
-  h = fma(h, r, h);
-  double d = fma(-g, g, x);
-  g = fma(d, h, g);
-  d = fma(-g, g, x);
-  return fma(d, h, g);
-}
-#if HS_SQRT_FAST >= 2
-// 1/sqrt(x) directly: v_rsq_f64, one Goldschmidt step (h ~ 1/(2 sqrt x)), one Newton step on y = 2h
+// v_rsq_f64, one Goldschmidt step (h ~ 1/(2 sqrt x)), one Newton step on y = 2h -- within ~1 ulp,
+// 7 dependent operations.  A/B, fp64 ms per configs[1] launch (with the DPP pivots of chol_rows):
+// recip(sqrt(x)) (18 operations) 0.714, the library sqrt sequence without its scaling / class check
+// then recip() (13) 0.701, this 0.690.  (Round 2 measured a v_rsq_f64 + two-Newton-step variant
+// slower, 305k vs 298k cycles per env substep, under the default machine scheduler.)
 template <>
 __device__ __forceinline__ double rsqrt_t<double>(double x) {
   const double y = __builtin_amdgcn_rsq(x);
@@ -374,14 +308,6 @@ __device__ __forceinline__ double rsqrt_t<double>(double x) {
   const double e = fma(-(x * y1), y1, 1.0);
   return fma(h, e, y1);
 }
-#else
-template <>
-__device__ __forceinline__ double rsqrt_t<double>(double x) { return recip(sqrt_normal(x)); }
-#endif
-#else
-template <>
-__device__ __forceinline__ double rsqrt_t<double>(double x) { return recip(sqrt(x)); }
-#endif
 template <typename T>
 __device__ __forceinline__ T normalize3(T* v) {
   const T n2 = dot3(v, v);
@@ -437,8 +363,7 @@ __device__ __forceinline__ void cross_force(const T* v, const T* f, T* r) {
 // *diag = d_i): the same elimination, each finished column scaled by its pivot's 1/L_kk on the way.
 template <int NV, typename T, bool LDL = false>
 __device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb)[2], T* diag = nullptr) {
-  constexpr bool CDPP = (HS_CHOL_DPP & (sizeof(T) == 8 ? 2 : 1)) != 0;
-  constexpr bool CEARLY = (HS_CHOL_EARLY & (sizeof(T) == 8 ? 2 : 1)) != 0;
+  constexpr bool CDPP = sizeof(T) == 8;   // pivot block by DPP: the fp64 engine only (see above)
   // two columns per LDS round trip: every lane publishes (a_ik, a_i,k+1) as one ds_write and reads
   // the 2x2 pivot block and (a_jk, a_j,k+1) back as broadcasts.  With L_P the pivot block's
   // Cholesky factor (1/L_kk = r1, L_k+1,k = l10, 1/L_k+1,k+1 = r2), row i gets
@@ -463,19 +388,15 @@ __device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb)[2
       t = cb[k + 1][1];
       p = p > T(1e-30) ? p : T(1e-30);
     }
-#if HS_CHOL_EARLY
     // the trailing columns' broadcast reads issued before the pivot math (fenced), so their LDS round
     // trip overlaps the pivot chain instead of following it
     T cj[NV][2];
-    if constexpr (CEARLY) {
-      static_for<k + 2, NV>([&](auto jc) {
-        constexpr int j = decltype(jc)::value;
-        cj[j][0] = cb[j][0];
-        cj[j][1] = cb[j][1];
-      });
-      SCHED_FENCE();
-    }
-#endif
+    static_for<k + 2, NV>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      cj[j][0] = cb[j][0];
+      cj[j][1] = cb[j][1];
+    });
+    SCHED_FENCE();
     T r1 = rsqrt_t(p);
     T l10 = q * r1;
     T s11 = t - l10 * l10;
@@ -497,13 +418,9 @@ __device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb)[2
     }
     static_for<k + 2, NV>([&](auto jc) {
       constexpr int j = decltype(jc)::value;
-#if HS_CHOL_EARLY
-      if constexpr (CEARLY) A[j] = fma(-f0, cj[j][0], fma(-f1, cj[j][1], A[j]));
-      else
-#endif
-      A[j] = fma(-f0, cb[j][0], fma(-f1, cb[j][1], A[j]));
+      A[j] = fma(-f0, cj[j][0], fma(-f1, cj[j][1], A[j]));
     });
-    if constexpr (HS_FENCE_CHOL == 1 || (HS_FENCE_CHOL == 2 && (k / 2) % 2 == 1)) SCHED_FENCE();
+    SCHED_FENCE();
   });
   if constexpr (NV % 2 == 1) {         // trailing single column
     constexpr int k = NV - 1;
@@ -533,40 +450,6 @@ __device__ __forceinline__ void chol_rows(T (&A)[NV], T& dinv, int sl, T (*cb)[2
     A[j] = sl_z > j ? A[j] : T(0);
   });
 }
-// Rank-1 update (sgn = +1) or downdate (sgn = -1) of a factor in L D L' form (unit lower L,
-// strictly lower part in A; d_i and 1/d_i on sub-lane i): L D L' + sgn v v' = L~ D~ L~' -- the
-// fp64 Newton's incremental Hessian, as MuJoCo's mju_cholUpdate -- by Gill, Golub, Murray and
-// Saunders' method C1 (no square roots):
-//   p = v_k,  d~_k = d_k + a p^2,  b = a p / d~_k,  a <- a d_k / d~_k;
-//   v_i <- v_i - p L_ik,  L~_ik = L_ik + b v_i          (i > k; a starts at sgn).
-// The chain from column to column is one broadcast of p and one FMA (v), plus the scalar a-chain
-// (one reciprocal); the L~ updates hang off it.  `on` false leaves the half's factor untouched.
-// Returns false on a half whose downdate cancelled more than 3 digits of a pivot (d~_k < 1e-3 d_k):
-// that half's factor is then rebuilt from H.
-template <int NV, typename T>
-__device__ __forceinline__ bool ldl_rank1(T (&A)[NV], T& d, T& dinv, T v, T sgn, bool on, int sl) {
-  bool ok = true;
-  T a = sgn;
-  static_for<0, NV>([&](auto kc) {
-    constexpr int k = decltype(kc)::value;
-    const int sl_k = opaque_v(sl);
-    const T p = bcast<k>(v), dk = bcast<k>(d);
-    const T ap = a * p;
-    const T dn = fma(ap, p, dk);
-    ok = ok && dn > T(1e-3) * dk;
-    const T rdn = recip(dn);
-    const T beta = ap * rdn;
-    a = a * dk * rdn;
-    const T vn = fma(-p, A[k], v);
-    const T ln = fma(beta, vn, A[k]);
-    const bool below = on && sl_k > k, piv = on && sl_k == k;
-    A[k] = below ? ln : A[k];
-    v = below ? vn : v;
-    d = piv ? dn : d;
-    dinv = piv ? rdn : dinv;
-  });
-  return ok || !on;
-}
 // solve (L L') x = b (L from chol_rows: strictly lower part, 1/L_ii in dinv); sub-lane i holds b_i;
 // returns x_i.  Forward: at step k every lane subtracts L_ik y_k (zero unless i > k), so lane k's b
 // stops changing once y_k = b_k / L_kk is broadcast, and y = b / L_ii at the end.
@@ -583,11 +466,7 @@ __device__ __forceinline__ T chol_solve(const T (&L)[NV], T dinv, T b, int sl) {
   // overlap), the block's own rows follow as a short chain of broadcasts of L_ik x_i from lane i
   // (block size A/B, fp64 configs[1] ms per launch: BS 1 0.726, 2 0.728, 3 0.731, 4 0.738,
   // 5 0.747; fp32: BS 2 0.424 vs 3 0.426, BS 1 within noise of 2)
-#ifndef HS_SOLVE_BS
   constexpr int BS = sizeof(T) == 8 ? 1 : 2;
-#else
-  constexpr int BS = HS_SOLVE_BS;
-#endif
   T x = 0;
   static_for<0, (NV + BS - 1) / BS>([&](auto bc) {
     constexpr int hi = NV - BS * decltype(bc)::value;        // block = columns [lo, hi)
@@ -633,28 +512,15 @@ __device__ __forceinline__ T chol_fwd(const T (&L)[NV], T dinv, T b, int sl) {
 // (A v)_i for a row-per-lane matrix and a vector in LDS (broadcast ds_reads)
 template <int NV, typename T>
 __device__ __forceinline__ T matvec_lds(const T (&A)[NV], const T* v) {
-#if HS_MATVEC_SPLIT
-  // two interleaved accumulators (half the dependent FMA chain; the sum's rounding order differs)
-  T acc0 = 0, acc1 = 0;
-  static_for<0, NV>([&](auto jc) {
-    constexpr int j = decltype(jc)::value;
-    if constexpr (j % 2 == 0) acc0 = fma(A[j], v[j], acc0);
-    else acc1 = fma(A[j], v[j], acc1);
-  });
-  return acc0 + acc1;
-#else
   T acc = 0;
   static_for<0, NV>([&](auto jc) {
     constexpr int j = decltype(jc)::value;
     acc = fma(A[j], v[j], acc);
   });
   return acc;
-#endif
 }
 
 // ------------------------------------------------------------------ per-env LDS scratch
-// dofs of the kernel instance whose Newton factor fits the LDS union (launch_step: nv == 27)
-constexpr int FACNV = 27;
 enum RowKind { RK_JLO = 0, RK_JHI = 1, RK_TLO = 2, RK_THI = 3, RK_CN = 4, RK_P0 = 5 };   // P0..P0+3: pyramid
 __device__ __forceinline__ int rk_kind(int kid) { return kid >> 16; }
 __device__ __forceinline__ int rk_id(int kid) { return kid & 0xffff; }
@@ -692,10 +558,6 @@ struct Scratch {
   int niter;                   // this env's Newton iterations (the wave's loop runs for the slower env)
   struct Kin { T xpos[MAXBODY][3]; T xmat[MAXBODY][9]; T xquat[MAXBODY][4]; T xanchor[MAXJNT][3];
                T xaxis[MAXJNT][3]; T gpos[MAXGEOM][3]; T gax[MAXGEOM][3]; };
-  // the fp64 Newton's L D L' factor between iterations (Stepper::factor_update): row i's unit-lower
-  // entries packed at [i (i - 1) / 2, i (i + 1) / 2), then d[FACNV], 1/d[FACNV].  It aliases the
-  // full-state arrays of `n` (written only after the solve) and the union's slack: no extra LDS.
-  struct Fac { T bvel[MAXBODY][6]; alignas(16) T cb[MAXDOF][2]; T fac[FACNV * (FACNV - 1) / 2 + 2 * FACNV]; };
   union {   // phase-local arrays (aliased)
     Kin k;                                                        // kinematics + collision
     struct { T crb[MAXBODY][10]; T buf[MAXDOF][6]; } c;          // composite rigid body
@@ -703,9 +565,7 @@ struct Scratch {
     struct { T bvel[MAXBODY][6];                                  // J x mapping (rows, Newton)
              alignas(16) T cb[MAXDOF][2];                         // Cholesky column pairs
              T cfrc[MAXBODY][6], linv[MAXBODY][3], mv[MAXBODY][3]; } n;   // full_state (after solve)
-    Fac nf;
   } u;
-  static_assert(sizeof(Fac) <= sizeof(Kin), "the Newton factor slot must fit the union without growing it");
 };
 
 // PGS solver scratch (the <option solver="PGS"> kernel instance only; the Newton instance never
@@ -964,7 +824,6 @@ __device__ __forceinline__ void contact_aggregates(MPtr<T> m, Scratch<T, C>& s, 
       int adr = s.con_adr[c];
       int nr = (s.con_bb[c] >> 16) == 1 ? 1 : 4;
       T U[6] = {0, 0, 0, 0, 0, 0}, F[3] = {0, 0, 0};
-#if HS_AGGR_STATIC
       // straight-line over the (at most 4) rows: every LDS operand is read up front (one round trip),
       // then the same sums in the same order as the row loop below
       const bool pyr = nr == 4;
@@ -995,20 +854,6 @@ __device__ __forceinline__ void contact_aggregates(MPtr<T> m, Scratch<T, C>& s, 
           for (int k = 0; k < 3; k++) F[k] += f * u[k];
         }
       }
-      if (false)
-#endif
-      for (int q = 0; q < nr; q++) {
-        int r = adr + q;
-        T f = s.row_f[r];
-        if (f != T(0)) {
-          T u[3];
-          row_u(m, s, rk_kind(s.row_kid[r]), c, u);
-          T D = s.row_D[r];
-          U[0] += D * u[0] * u[0]; U[1] += D * u[1] * u[1]; U[2] += D * u[2] * u[2];
-          U[3] += D * u[0] * u[1]; U[4] += D * u[0] * u[2]; U[5] += D * u[1] * u[2];
-          for (int k = 0; k < 3; k++) F[k] += f * u[k];
-        }
-      }
       for (int k = 0; k < 6; k++) s.con_U[c][k] = U[k];
       for (int k = 0; k < 3; k++) s.con_F[c][k] = F[k];
       act = F[0] != T(0) || F[1] != T(0) || F[2] != T(0) || U[0] != T(0) || U[1] != T(0) || U[2] != T(0);
@@ -1030,26 +875,19 @@ __device__ __forceinline__ void for_active_contacts(const uint32_t* act, F&& f) 
 // contact instead of a read, a branch on it and dependent reads; HS_CONTACT_FLAT) and the next
 // contact's reads issued before the current contact's arithmetic (HS_CONTACT_AHEAD): J'f and the
 // Hessian's contact terms.  A/B, fp64 ms per configs[1] launch: 0.635 -> flat 0.634 -> + ahead 0.632.
-#ifndef HS_CONTACT_AHEAD
-#define HS_CONTACT_AHEAD 1
-#endif
 template <typename T, typename C, typename LD, typename F>
 __device__ __forceinline__ void for_active_contacts_ld(const uint32_t* act, LD&& ld, F&& f) {
 #pragma unroll
   for (int w = 0; w < (C::CON + HL - 1) / HL; w++)
-    for_bits<T, HS_CONTACT_AHEAD != 0>(
+    for_bits<T, true>(
         act[w], [&](int j) { return ld(w * HL + j); }, [&](int j, const auto& v) { f(w * HL + j, v); });
 }
-#ifndef HS_CONTACT_FLAT
-#define HS_CONTACT_FLAT 1
-#endif
 
 // (J' f)_i for dof sub-lane i (contacts via point Jacobians, joint limits via the dof's
 // limit-row slots, tendon limits via rows [njl, nlim))
 template <typename T, typename C>
 __device__ __forceinline__ T jtf_lane(MPtr<T> m, const Scratch<T, C>& s, int sl, const T* cd) {
   T acc = 0;
-#if HS_CONTACT_FLAT
   struct CV { uint32_t m1, m2; T p[3], f[3]; };
   for_active_contacts_ld<T, C>(s.con_act, [&](int c) {
     CV v;
@@ -1065,19 +903,6 @@ __device__ __forceinline__ T jtf_lane(MPtr<T> m, const Scratch<T, C>& s, int sl,
       T jp[3] = {cd[3] + w[0], cd[4] + w[1], cd[5] + w[2]};
       T x = dot3(jp, v.f);
       acc += in2 ? x : -x;
-    }
-  });
-  if (false)
-#endif
-  for_active_contacts<C>(s.con_act, [&](int c) {
-    int in2 = bit(s.con_m2[c], sl), in1 = bit(s.con_m1[c], sl);
-    if (in1 != in2) {
-      T r[3] = {s.con_pos[c][0] - s.com[0], s.con_pos[c][1] - s.com[1], s.con_pos[c][2] - s.com[2]};
-      T w[3];
-      cross3(cd, r, w);
-      T jp[3] = {cd[3] + w[0], cd[4] + w[1], cd[5] + w[2]};
-      T v = dot3(jp, s.con_F[c]);
-      acc += in2 ? v : -v;
     }
   });
   if (sl < MAXDOF) {
@@ -1165,35 +990,15 @@ struct Stepper {
   __device__ Stepper(MPtr<T> mm, Scratch<T, C>& ss, int lane)
       : m(mm), s(ss), sl(lane & (HL - 1)), nb(mm->nbody), up(lane >= HL) {}
 
-  // Incremental factor (development build -DHS_NEWTON_INCR, fp64 only): Newton iterations after the
-  // first update the previous iteration's L D L' factor by rank-1 terms for the rows whose active
-  // state changed (at most NUPD per half; factor_update) instead of rebuilding H and factoring it,
-  // as MuJoCo's Newton does.  Measured slower on MI355X and left out of the product (DESIGN.md 3.2:
-  // the updates are serial 27-column chains, and the extra live state costs the queue kernel its
-  // last registers).
-#ifdef HS_NEWTON_INCR
-  static constexpr bool INCR = sizeof(T) == 8 && NV <= FACNV;
-#else
-  static constexpr bool INCR = false;
-#endif
-  // the Newton factor as L D L' (unit lower L): the same elimination, but the triangular solves lose
-  // one dependent multiply per column (fp64 0.740 -> 0.731 ms per configs[1] launch; the Euler
-  // factorization and the fp32 engine measured the same either way and stay L L').
-  // HS_NEWTON_LDL: bit 0 the fp32 engine, bit 1 the fp64 engine.
-#ifndef HS_NEWTON_LDL
-#define HS_NEWTON_LDL 2
-#endif
-  static constexpr bool LDLF = INCR || ((sizeof(T) == 8 ? 2 : 1) & HS_NEWTON_LDL) != 0;
-#ifdef HS_EULER_LDL
-  static constexpr bool LDLE = true;
-#else
+  // The Newton iterations rebuild H and factor it every time.  MuJoCo's rank-1 updates of the factor
+  // (mju_cholUpdate) were built and measured slower on MI355X (DESIGN.md 3.1 "Incremental factor"):
+  // each update is a serial 27-column chain, and the extra live state costs the queue kernel its last
+  // registers.
+  // the Newton factor as L D L' in the fp64 engine (unit lower L): the same elimination, but the
+  // triangular solves lose one dependent multiply per column (fp64 0.740 -> 0.731 ms per configs[1]
+  // launch; the Euler factorization and the fp32 engine measured the same either way and stay L L').
+  static constexpr bool LDLF = sizeof(T) == 8;
   static constexpr bool LDLE = false;
-#endif
-#ifndef HS_NUPD
-  static constexpr int NUPD = 4;
-#else
-  static constexpr int NUPD = HS_NUPD;
-#endif
   // the launch arguments (every step-kernel instance takes its KArgs at kernarg offset 0)
   __device__ __forceinline__ static KPtr<T> kargs() { return (KPtr<T>)__builtin_amdgcn_kernarg_segment_ptr(); }
 
@@ -1437,8 +1242,8 @@ struct Stepper {
       arm = m->dof_armature[sl];
     }
     WSYNC();
-    // CRB_G columns per scheduling group (one exposed LDS round trip per group, as in the Hessian)
-    if constexpr (HS_CRB_AHEAD) {
+    // one column per scheduling group (2 or 3 measured the same)
+    {
       // software-pipelined: column j+1's cdof / buf rows are read before column j's arithmetic
       T cb2[2][12];
       auto load = [&](auto jc, T (&dst)[12]) {
@@ -1456,36 +1261,7 @@ struct Stepper {
         const T v = (j <= sl) ? dot6(cj, bf) : dot6(cd, cj + 6);
         Mr[j] = rel ? v + ((j == sl) ? arm : T(0)) : T(0);
       });
-    } else if constexpr (CRB_G == 1) {
-#pragma unroll
-      for (int j = 0; j < NV; j++) {
-        uint32_t ancj = m->dof_ancmask[j];
-        bool rel = (sl < NV) && (bit(anci, j) || bit(ancj, sl));
-        T cj[6], bj[6];
-        for (int k = 0; k < 6; k++) { cj[k] = s.cdof[j][k]; bj[k] = s.u.c.buf[j][k]; }
-        T v = (j <= sl) ? dot6(cj, bf) : dot6(cd, bj);
-        Mr[j] = rel ? v + ((j == sl) ? arm : T(0)) : T(0);
-        if constexpr (HS_FENCE_CRB) SCHED_FENCE();
-      }
-    } else static_for<0, (NV + CRB_G - 1) / CRB_G>([&](auto gc) {
-      constexpr int j0 = decltype(gc)::value * CRB_G;
-      T cj[CRB_G][6], bj[CRB_G][6];
-      static_for<0, CRB_G>([&](auto tc) {
-        constexpr int t = decltype(tc)::value;
-        if constexpr (j0 + t < NV)
-          for (int k = 0; k < 6; k++) { cj[t][k] = s.cdof[j0 + t][k]; bj[t][k] = s.u.c.buf[j0 + t][k]; }
-      });
-      static_for<0, CRB_G>([&](auto tc) {
-        constexpr int t = decltype(tc)::value, j = j0 + t;
-        if constexpr (j < NV) {
-          const uint32_t ancj = m->dof_ancmask[j];
-          const bool rel = (sl < NV) && (bit(anci, j) || bit(ancj, sl));
-          const T v = (j <= sl) ? dot6(cj[t], bf) : dot6(cd, bj[t]);
-          Mr[j] = rel ? v + ((j == sl) ? arm : T(0)) : T(0);
-        }
-      });
-      if constexpr (HS_FENCE_CRB) SCHED_FENCE();
-    });
+    }
     WSYNC();
   }
 
@@ -1722,7 +1498,6 @@ struct Stepper {
     HS_STAMP(clk, 6);
     bool done = false;      // this half-wave's solver has converged
     int it = 0;
-    int fmask = 0;          // (INCR) rows q = 0..RPL-1 of this lane active in the saved factor
     if (sl == 0) s.niter = maxit;   // per env: the iteration at which this half converged
     for (; it < maxit; it++) {
       m = opaque(m);
@@ -1746,17 +1521,10 @@ struct Stepper {
       if (__ballot(!done) == 0) break;       // both envs of the wave converged
       T H[NV];
       T hdinv = 0, hdiag = 0;
-      bool full = true;     // this half builds H and factors it (else: its saved factor, updated)
-      if constexpr (INCR) {
-        if (it > 0 && opaque(kargs())->p.newton_incr) full = !factor_update(H, hdiag, hdinv, act, vr, fmask);
-        HS_STAMP(clk, 26);
-      }
-      if (full) {
       // Hessian lower rows: M + contact (tree form) + joint limits (diag) + dense rank-1 rows
       {
         T aug[6] = {0, 0, 0, 0, 0, 0};
         T dadd = 0;
-#if HS_CONTACT_FLAT
         struct CU { uint32_t m1, m2; T p[3], U[6]; };
         for_active_contacts_ld<T, C>(s.con_act, [&](int c) {
           CU v;
@@ -1777,22 +1545,6 @@ struct Stepper {
           cross3(r, z, rz);
           for (int k = 0; k < 3; k++) { aug[k] += rz[k]; aug[3 + k] += z[k]; }
         });
-        if (false)
-#endif
-        for_active_contacts<C>(s.con_act, [&](int c) {   // (contacts with U = 0 add exact zeros)
-          if (s.con_m1[c] != 0u) return;           // body-body: dense rank-1 rows below
-          if (!bit(s.con_m2[c], sl)) return;
-          T r[3] = {s.con_pos[c][0] - s.com[0], s.con_pos[c][1] - s.com[1], s.con_pos[c][2] - s.com[2]};
-          T w[3];
-          cross3(cd, r, w);
-          T jp[3] = {cd[3] + w[0], cd[4] + w[1], cd[5] + w[2]};
-          const T* U = s.con_U[c];
-          T z[3] = {U[0] * jp[0] + U[3] * jp[1] + U[4] * jp[2], U[3] * jp[0] + U[1] * jp[1] + U[5] * jp[2],
-                    U[4] * jp[0] + U[5] * jp[1] + U[2] * jp[2]};
-          T rz[3];
-          cross3(r, z, rz);
-          for (int k = 0; k < 3; k++) { aug[k] += rz[k]; aug[3 + k] += z[k]; }
-        });
         {   // active joint-limit rows of this dof (diagonal)
           int lr = s.lim_row[sl];
           int lo = (lr & 0xff) - 1, hi = (lr >> 8) - 1;
@@ -1802,20 +1554,16 @@ struct Stepper {
         HS_STAMP(clk, 27);
         // HESS_G columns per scheduling group: their cdof rows are read from LDS together, so one
         // LDS round trip is exposed per group instead of per column
-#ifdef HS_HESS_G
-        constexpr int HESS_G = HS_HESS_G;
-#else
         constexpr int HESS_G = sizeof(T) == 8 ? 2 : 1;
-#endif
         if constexpr (HESS_G == 1) {
 #pragma unroll
           for (int j = 0; j < NV; j++) {
             T cj[6];
             for (int k = 0; k < 6; k++) cj[k] = s.cdof[j][k];
             H[j] = Mr[j] + (bit(anci, j) ? dot6(cj, aug) : T(0)) + ((j == sl) ? dadd : T(0));
-            if constexpr (HS_FENCE_HESS) SCHED_FENCE();
+            SCHED_FENCE();
           }
-        } else if constexpr (HS_HESS_AHEAD) {
+        } else {
           // software-pipelined: group g+1's cdof rows are read before group g's arithmetic (fenced),
           // so each group's LDS round trip overlaps the previous group's FMAs
           constexpr int NG = (NV + HESS_G - 1) / HESS_G;
@@ -1839,20 +1587,7 @@ struct Stepper {
                 H[j] = Mr[j] + (bit(anci, j) ? dot6(cbuf[g & 1][t], aug) : T(0)) + ((j == sl) ? dadd : T(0));
             });
           });
-        } else static_for<0, (NV + HESS_G - 1) / HESS_G>([&](auto gc) {
-          constexpr int j0 = decltype(gc)::value * HESS_G;
-          T cj[HESS_G][6];
-          static_for<0, HESS_G>([&](auto tc) {
-            constexpr int t = decltype(tc)::value;
-            if constexpr (j0 + t < NV)
-              for (int k = 0; k < 6; k++) cj[t][k] = s.cdof[j0 + t][k];
-          });
-          static_for<0, HESS_G>([&](auto tc) {
-            constexpr int t = decltype(tc)::value, j = j0 + t;
-            if constexpr (j < NV) H[j] = Mr[j] + (bit(anci, j) ? dot6(cj[t], aug) : T(0)) + ((j == sl) ? dadd : T(0));
-          });
-          if constexpr (HS_FENCE_HESS) SCHED_FENCE();
-        });
+        }
         HS_STAMP(clk, 28);
         // dense rank-1 rows (tendon limits, body-body contacts): only the rows flagged in
         // dense_mask; the loop runs max(#rows of either half) times (wave-uniform control)
@@ -1900,14 +1635,7 @@ struct Stepper {
       HS_STAMP(clk, 9);
       chol_rows<NV, T, LDLF>(H, hdinv, sl, s.u.n.cb, &hdiag);   // (LDLF: as L D L')
       HS_STAMP(clk, 15);
-      }
       T sdir = -chol_solve<NV, T, LDLF>(H, hdinv, g, sl);
-      if constexpr (INCR) {   // the factor and its active set, for the next iteration's update
-        fmask = 0;
-#pragma unroll
-        for (int q = 0; q < C::RPL; q++) fmask |= act[q] ? (1 << q) : 0;
-        fac_store(H, hdiag, hdinv);
-      }
       if (sl >= NV) sdir = 0;
       HS_STAMP(clk, 10);
       // exact line search along sdir (piecewise-quadratic cost)
@@ -1992,76 +1720,6 @@ struct Stepper {
     HS_STAMP(clk, 12);
   }
 
-  // Incremental factor (fp64 Newton, iterations after the first; MuJoCo's Newton updates its
-  // Cholesky factor the same way, mju_cholUpdate): this half's L D L' factor of the previous
-  // iteration, saved in LDS (fac_store), updated by sqrt(D_r) J_r for every row r whose active state
-  // changed since it was factored -- rows that became active first (updates), then rows that left
-  // (downdates).  Returns false on a half with more than NUPD changed rows or a failed downdate:
-  // that half rebuilds H and factors it instead.
-  __device__ __forceinline__ bool factor_update(T (&H)[NV], T& hdiag, T& hdinv, const bool (&act)[C::RPL],
-                                                const bool (&vr)[C::RPL], int fmask) {
-    uint32_t ad[C::RPL], rm[C::RPL];
-    int cnt = 0;
-#pragma unroll
-    for (int q = 0; q < C::RPL; q++) {
-      const bool f = (fmask >> q) & 1;
-      ad[q] = hballot(act[q] && !f, up);
-      rm[q] = hballot(vr[q] && !act[q] && f, up);
-      cnt += __popc(ad[q]) + __popc(rm[q]);
-    }
-    const bool inc = cnt <= NUPD;
-    if (__ballot(inc) == 0) return false;
-    fac_load(H, hdiag, hdinv);
-    bool ok = true;
-    for (;;) {   // max(changed rows of either half) rounds, wave-uniform control
-      int r = -1;
-      bool add = false;
-#pragma unroll
-      for (int q = C::RPL - 1; q >= 0; q--)
-        if (rm[q]) r = HL * q + __builtin_ctz(rm[q]);
-#pragma unroll
-      for (int q = C::RPL - 1; q >= 0; q--)
-        if (ad[q]) { r = HL * q + __builtin_ctz(ad[q]); add = true; }
-      if (!inc) r = -1;
-      if (__ballot(r >= 0) == 0) break;
-      T v = 0;
-      if (r >= 0) {
-#pragma unroll
-        for (int q = 0; q < C::RPL; q++) {   // consume the row
-          if (q == r / HL) {
-            if (add) ad[q] &= ad[q] - 1u;
-            else rm[q] &= rm[q] - 1u;
-          }
-        }
-        v = sqrt(s.row_D[r]) * row_J_lane(r);
-      }
-      ok = ldl_rank1<NV>(H, hdiag, hdinv, v, add ? T(1) : T(-1), r >= 0, sl) && ok;
-    }
-    return inc && ok;
-  }
-  // the factor between Newton iterations: row sl's unit-lower entries packed in LDS (Scratch::Fac)
-  __device__ __forceinline__ void fac_store(const T (&H)[NV], T d, T dinv) {
-    T* f = s.u.nf.fac;
-    const int i = opaque_v(sl), base = i * (i - 1) / 2;
-    static_for<0, NV - 1>([&](auto jc) {
-      constexpr int j = decltype(jc)::value;
-      if (j < i && i < NV) f[base + j] = H[j];
-    });
-    if (i < NV) {
-      f[FACNV * (FACNV - 1) / 2 + i] = d;
-      f[FACNV * (FACNV - 1) / 2 + FACNV + i] = dinv;
-    }
-  }
-  __device__ __forceinline__ void fac_load(T (&H)[NV], T& d, T& dinv) {
-    const T* f = s.u.nf.fac;
-    const int i = opaque_v(sl), base = i * (i - 1) / 2;
-    static_for<0, NV>([&](auto jc) {
-      constexpr int j = decltype(jc)::value;
-      H[j] = (j < i && i < NV) ? f[base + j] : T(0);
-    });
-    d = i < NV ? f[FACNV * (FACNV - 1) / 2 + i] : T(1);
-    dinv = i < NV ? f[FACNV * (FACNV - 1) / 2 + FACNV + i] : T(1);
-  }
 
   // lane (dof) j's entry of constraint row r's Jacobian (the same per-row Jacobians row_Jx applies
   // through body velocities and the Newton Hessian's dense rank-1 terms use)
