@@ -508,15 +508,18 @@ def main():
                 tr = json.load(open(PROFILE_TRAFFIC)).get(args.precision, {})
                 if tr.get("n_envs") == n:
                     traffic = tr.get("hbm_bytes_per_launch")
-                    # VALU-issue view of the same kernel (what bounds it): VALU wave-instructions per
-                    # launch from the profile's PMC pass over the live launch time; a SIMD issues one
-                    # wave64 VALU op per 2 cycles at 2.4 GHz (MI355X_MICROARCH.md, wave scheduling)
-                    valu = tr.get("sq", {}).get("SQ_INSTS_VALU")
-                    if valu:
-                        peak = 256 * 4 * 2.4e9 / 2
-                        ach = valu / (kernel_ms * 1e-3)
-                        issue = {"valu_wave_instr_per_s": ach, "peak": peak, "frac": ach / peak,
-                                 "source": f"SQ_INSTS_VALU per launch from profiles ({tr.get('tag')})"}
+                    # what bounds it: the share of the waves' lifetime their SIMD's VALU spends on them
+                    # (SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES, same counter units) -- fp64 VALU ops issue at
+                    # half the fp32 rate, so an instruction count priced at a fixed cycles-per-op would
+                    # understate it; and the share parked on s_waitcnt (SQ_WAIT_ANY / SQ_WAVE_CYCLES)
+                    sq = tr.get("sq", {})
+                    if sq.get("SQ_ACTIVE_INST_VALU") and sq.get("SQ_WAVE_CYCLES"):
+                        wc = sq["SQ_WAVE_CYCLES"]
+                        issue = {"frac": sq["SQ_ACTIVE_INST_VALU"] / wc,
+                                 "wait_frac": sq.get("SQ_WAIT_ANY", 0.0) / wc,
+                                 "issue_any_frac": sq.get("SQ_ACTIVE_INST_ANY", 0.0) / wc,
+                                 "source": f"SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES of the committed profile "
+                                           f"({tr.get('tag')})"}
             except Exception:
                 traffic = None
         kname = ("step_kernel_queue" if queued else "step_kernel") + (
@@ -555,8 +558,8 @@ def main():
                          "kernel_ms_per_launch": kernel_ms, "envs_per_launch": n,
                          "schedule": ("chunk queue: persistent grid of resident waves, two items per env step "
                                       "(DESIGN.md 3.1)" if queued else "one wave per env pair"),
-                         "algo_bytes_per_env_step": abytes, "valu_issue": issue, "valu_flops": vflops,
-                         "note": "latency-bound kernel (see valu_issue and DESIGN.md 3.1); HBM fraction reported per "
+                         "algo_bytes_per_env_step": abytes, "valu_busy": issue, "valu_flops": vflops,
+                         "note": "latency-bound kernel (see valu_busy and DESIGN.md 3.1); HBM fraction reported per "
                                  "BASELINE.json; HIP events over the timed steps on the launch stream (the step "
                                  "kernel + the wide-tier launch, which exits at once when no env overflowed)"},
             "cpu_baseline": cpu_res,
