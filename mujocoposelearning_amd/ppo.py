@@ -580,6 +580,22 @@ class PPO:
             with torch.cuda.graph(g2, pool=pool, capture_error_mode="thread_local"):
                 g2_body()
             self._graphs = (g1, g2)
+            if not sync:
+                # world 1: the whole epoch -- every minibatch's gather, forward, loss, backward, clip and
+                # Adam, indices read from slices of one static permutation buffer -- as ONE graph, so
+                # small minibatches (README.md:23-53: batch 128, 128 steps per epoch) cost one replay
+                # per epoch instead of two per minibatch.  Each step starts from .grad = None, so its
+                # backward writes fresh gradients exactly as G1 does.
+                self._g_perm = torch.zeros(M, dtype=torch.long, device=dev)
+                ge = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(ge, pool=pool, capture_error_mode="thread_local"):
+                    for s0, e0 in zip(self._mb_bounds, self._mb_bounds[1:]):
+                        self.opt.zero_grad(set_to_none=True)
+                        loss, pg, vf = self._minibatch_loss(*src, self._g_perm[s0:e0])
+                        loss.backward()
+                        self._g_stats.add_(torch.stack([pg.detach(), vf.detach()]))
+                        self._clip_and_step()
+                self._epoch_graph = ge
         except RuntimeError as e:                  # capture refused: train eagerly from here on
             import warnings
             warnings.warn(f"PPO update graph capture failed ({e}); falling back to the eager update")
@@ -609,8 +625,14 @@ class PPO:
         self._g_ret.copy_(ret.reshape(-1))
         self._g_stats.zero_()
         n = 0
+        ge = getattr(self, "_epoch_graph", None)
         for epoch in range(self.n_epochs):
             perm = torch.randperm(M, device=self.device)
+            if ge is not None:                    # world 1: one replay per epoch
+                self._g_perm.copy_(perm)
+                ge.replay()
+                n += len(self._mb_bounds) - 1
+                continue
             for j, (s, e) in enumerate(zip(self._mb_bounds, self._mb_bounds[1:])):
                 self._g_idx.copy_(perm[s:e])
                 if self.sync_grads:

@@ -309,7 +309,7 @@ def test_fp64_1000_substeps_within_chaos_envelope(tape):
     """SURVEY 8d parity run: 1000 substeps.  The fp64 GPU engine may differ from the oracle only as
     much as the oracle differs from itself under a 1e-15 relative perturbation (the chaos
     envelope of this contact-rich system), with an absolute floor of 1e-9.  Full table:
-    profiles/parity_report.md (tests/parity_report.py)."""
+    profiles/parity_report.md (tools/probes/parity_report.py)."""
     import parity_report as pr
     from mujocoposelearning_amd.model import HsModel
     from oracle.oracle import Oracle

@@ -192,15 +192,18 @@ def test_gauss_logp_forward_backward_match_torch():
     assert torch.allclose(gls, gls_r, rtol=1e-4, atol=1e-3 * float(gls_r.abs().max())), float((gls - gls_r).abs().max())
 
 
-def test_graphed_update_matches_eager_update():
-    """PPO.train replayed as HIP graphs (G1 fwd+bwd, G2 clip+Adam) takes the same optimizer steps
-    as the eager loop: same rollout, same minibatch permutations -> same weights and losses."""
+@pytest.mark.parametrize("batch", [2048, 128])
+def test_graphed_update_matches_eager_update(batch):
+    """PPO.train replayed as HIP graphs takes the same optimizer steps as the eager loop: same
+    rollout, same minibatch permutations -> same weights and losses.  World 1 replays one graph per
+    epoch (every minibatch's fwd+bwd, clip and Adam); batch 128 is the reference's README config
+    (64 minibatches per epoch here)."""
     from mujocoposelearning_amd.model import HsModel
     from mujocoposelearning_amd.ppo import PPO
     from mujocoposelearning_amd.vec_env import HumanoidVecEnv
     env = HumanoidVecEnv({"model_path": XML, "duration": 10.0, "reward_config": {"type": "stand"}, "frame_skip": 3},
                          n_envs=512, model=HsModel(XML), seed=0)
-    kw = dict(n_steps=16, batch_size=2048, n_epochs=2, seed=0,
+    kw = dict(n_steps=16, batch_size=batch, n_epochs=2, seed=0,
               policy_kwargs={"activation_fn": "ReLU", "net_arch": {"pi": [256, 256], "vf": [256, 256]}})
     pa, pb = PPO(env, **kw), PPO(env, **kw)
     pb.graphs = False
@@ -212,7 +215,7 @@ def test_graphed_update_matches_eager_update():
         for it in range(2):                 # the second call replays the graphs captured by the first
             torch.manual_seed(100 + it)
             res.append(p.train(adv, ret))
-    assert pa._graphs is not None and pb._graphs is None
+    assert pa._graphs is not None and pb._graphs is None and pa._epoch_graph is not None
     for x, y in zip(pa.policy.parameters(), pb.policy.parameters()):
         assert torch.allclose(x, y, rtol=1e-4, atol=1e-6), float((x - y).abs().max())
     for ra, rb in zip(res[:2], res[2:]):

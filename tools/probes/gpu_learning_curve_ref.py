@@ -44,19 +44,27 @@ def main():
     ppo = PPO(env, n_steps=a.n_steps, seed=a.seed, **PPO_KWARGS)
     t0 = time.perf_counter()
     it = 0
+    t_roll = t_train = 0.0
     while ppo.num_timesteps < a.steps:
+        t1 = time.perf_counter()
         adv, ret = ppo.collect_rollouts()
         h = ppo.buf["obs"][..., 0]                     # obs[0] = qpos[2], the torso height
         upright = float((h > 1.0).float().mean())
         hmean = float(h.mean())
+        t2 = time.perf_counter()
         st = ppo.train(adv, ret)
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        t_roll += t2 - t1
+        t_train += t3 - t2
         it += 1
         if it % a.every == 0 or ppo.num_timesteps >= a.steps:
             ep = float(np.mean(ppo.ep_returns[-100:])) if ppo.ep_returns else float("nan")
             print(f"seed {a.seed} iter {it:5d} steps {ppo.num_timesteps / 1e6:7.3f}M ep_rew_mean {ep:8.2f} "
                   f"episodes {len(ppo.ep_returns):6d} upright {upright:.3f} height {hmean:.3f} "
                   f"vf_loss {st['value_loss']:.3f} log_std {float(ppo.policy.log_std.mean()):.3f} "
-                  f"{time.perf_counter() - t0:7.1f}s", flush=True)
+                  f"rollout {t_roll / it:.3f}s train {t_train / it:.3f}s per iter {time.perf_counter() - t0:7.1f}s",
+                  flush=True)
     env.close()
 
 
