@@ -8,4 +8,6 @@ echo "pytest rc=$rc" >> gpurun_out/r4c/gputest.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 300 python -u tools/probes/gpu_fp32_events.py > gpurun_out/r4c/fp32_events.md 2> gpurun_out/r4c/fp32_events.err || exit 5
 timeout -k 10 300 python -u tools/probes/gpu_learning_curve_ref.py --seed 0 --steps 0.5e6 --every 5 > gpurun_out/r4c/lc_timing.log 2>&1 || exit 6
+
+timeout -k 10 300 python -u tools/probes/gpu_timing.py fp64 staggered > gpurun_out/r4c/timing_fp64.txt 2>&1 || exit 7
 exit $rc
