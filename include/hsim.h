@@ -42,6 +42,10 @@
  * model is immutable and shareable; a batch owns (or is bound to) device buffers; every call
  * takes an optional HIP stream (NULL = default stream) and is asynchronous unless noted; a
  * batch is not re-entrant.  No torch types cross this boundary.
+ * Launches of ONE batch (hs_reset / hs_step / hs_physics_step) must be ordered: issue them on one
+ * stream, or order the streams (event wait).  Like one mjData, a batch is a single state: two
+ * unordered launches race on every buffer, and on the chunk-queue schedule they also share the
+ * batch's claim counters and cost-ordered claim lists, so pairs could be stepped twice or skipped.
  */
 #ifndef HSIM_H
 #define HSIM_H
