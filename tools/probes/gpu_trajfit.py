@@ -113,7 +113,7 @@ def cma_fit(shoot, q0, v0, s1, pop, gens, seed, sigma0=0.5, log=None):
             best = (float(F[idx[0]]), X[idx[0]].astype(np.float64))
         sel = (X[idx[:mu]].astype(np.float64) - m) / sigma
         yw = sel.T @ w
-        m = m + sigma * yw
+        m = np.clip(m + sigma * yw, -1, 1)    # keep the mean in the box (clipped samples otherwise let sigma run away)
         invsqrt = (B / D) @ B.T
         ps = (1 - cs) * ps + np.sqrt(cs * (2 - cs) * mueff) * invsqrt @ yw
         hs = np.linalg.norm(ps) / np.sqrt(1 - (1 - cs) ** (2 * (g + 1))) < (1.4 + 2 / (d + 1)) * chiN
