@@ -26,6 +26,9 @@ from mujocoposelearning_amd.vec_env import HumanoidVecEnv  # noqa: E402
 
 PPO_KWARGS = dict(learning_rate=5e-5, batch_size=128, n_epochs=10, gamma=0.99, gae_lambda=0.95, clip_range=0.2,
                   ent_coef=0.002, policy_kwargs={"activation_fn": "ReLU", "net_arch": {"pi": [256, 256], "vf": [256, 256]}})
+# the reference's config.py (README.md:154 points to it for "the hyperparams"): 5 M steps
+CONFIGPY_KWARGS = dict(learning_rate=3e-4, batch_size=256, n_epochs=20, gamma=0.99, gae_lambda=0.95, clip_range=0.2,
+                       ent_coef=0.0, policy_kwargs={"activation_fn": "ReLU", "net_arch": {"pi": [64, 64], "vf": [64, 64]}})
 
 
 def main():
@@ -37,11 +40,21 @@ def main():
     ap.add_argument("--precision", default="fp64")
     ap.add_argument("--reward", default="stand")
     ap.add_argument("--every", type=int, default=20)
+    ap.add_argument("--config", default="readme", choices=("readme", "configpy"))
+    ap.add_argument("--stagger", action="store_true",
+                    help="spread the envs' episode clocks over the episode (env i starts i/N into it, as bench.py's "
+                         "window): every rollout then holds every phase of an episode, as the reference's 8 envs x "
+                         "2048 steps (3 whole episodes per rollout) do; without it all envs reset together and a "
+                         "128-step rollout sees one fifth of the episode")
     a = ap.parse_args()
     cfg = env_config_from_kwargs({"reward_function": a.reward, "frame_skip": 3}, HUMANOID_XML)
     env = HumanoidVecEnv(cfg, n_envs=a.envs, model=HsModel(HUMANOID_XML), seed=a.seed, precision=a.precision)
     env.batch.configure(aux=False, ctrl=False)
-    ppo = PPO(env, n_steps=a.n_steps, seed=a.seed, **PPO_KWARGS)
+    ppo = PPO(env, n_steps=a.n_steps, seed=a.seed, **(PPO_KWARGS if a.config == "readme" else CONFIGPY_KWARGS))
+    if a.stagger:        # after PPO's reset: env i's episode clock at i/N of the 667-step episode
+        k = np.floor(np.arange(a.envs) * 667 / a.envs)
+        env.batch.t["time"].copy_(torch.as_tensor(k * 0.015 + 0.005, dtype=env.batch.dtype, device=env.device))
+        env.batch.t["step_count"].copy_(torch.as_tensor(k, dtype=torch.int32, device=env.device))
     t0 = time.perf_counter()
     it = 0
     t_roll = t_train = 0.0
