@@ -64,6 +64,34 @@ def make_model(xml_path, variant="truth"):
     return M
 
 
+def variant_xml(name, xml_path=None):
+    """A model file for the XML-edit variants (the GPU fit, tools/probes/gpu_trajfit.py, runs them
+    through both compilers): ``armature_zero`` sets every joint armature to 0, ``friction_07`` the
+    floor friction to 0.7 (what min-mixing the floor's 1 with the bodies' 0.7 would give)."""
+    import re
+    import tempfile
+    if xml_path is None:
+        from mujocoposelearning_amd.model import HUMANOID_XML as xml_path
+    src = open(xml_path).read()
+    if name == "truth":
+        return xml_path
+    if name == "armature_zero":
+        src, n = re.subn(r'armature="[^"]*"', 'armature="0"', src)
+        assert n > 0
+    elif name == "friction_07":
+        # the floor geom's friction 1 -> 0.7: max(0.7, body 0.7) = 0.7, as a min-mixing rule would give
+        src, n = re.subn(r'(<geom[^>]*name="floor"[^>]*?)friction="[^"]*"', r'\1friction="0.7 0.005 0.0001"', src)
+        if n == 0:
+            src, n = re.subn(r'(<geom[^>]*name="floor")', r'\1 friction="0.7 0.005 0.0001"', src)
+        assert n > 0
+    else:
+        raise ValueError(name)
+    d = tempfile.mkdtemp()
+    p = os.path.join(d, f"humanoid_{name}.xml")
+    open(p, "w").write(src)
+    return p
+
+
 class IntervalFit:
     """Controls of one key interval: u[k, :] for env step k = 0..4 of the interval."""
 

@@ -41,6 +41,8 @@ def main():
     ap.add_argument("--reward", default="stand")
     ap.add_argument("--every", type=int, default=20)
     ap.add_argument("--config", default="readme", choices=("readme", "configpy"))
+    ap.add_argument("--load", default=None, help="resume from a PPO.save zip (weights, Adam state, timesteps)")
+    ap.add_argument("--save", default=None, help="PPO.save zip written at the end (resume with --load)")
     ap.add_argument("--stagger", action="store_true",
                     help="spread the envs' episode clocks over the episode (env i starts i/N into it, as bench.py's "
                          "window): every rollout then holds every phase of an episode, as the reference's 8 envs x "
@@ -51,6 +53,8 @@ def main():
     env = HumanoidVecEnv(cfg, n_envs=a.envs, model=HsModel(HUMANOID_XML), seed=a.seed, precision=a.precision)
     env.batch.configure(aux=False, ctrl=False)
     ppo = PPO(env, n_steps=a.n_steps, seed=a.seed, **(PPO_KWARGS if a.config == "readme" else CONFIGPY_KWARGS))
+    if a.load:
+        ppo.load(a.load)
     if a.stagger:        # after PPO's reset: env i's episode clock at i/N of the 667-step episode
         k = np.floor(np.arange(a.envs) * 667 / a.envs)
         env.batch.t["time"].copy_(torch.as_tensor(k * 0.015 + 0.005, dtype=env.batch.dtype, device=env.device))
@@ -78,6 +82,8 @@ def main():
                   f"vf_loss {st['value_loss']:.3f} log_std {float(ppo.policy.log_std.mean()):.3f} "
                   f"rollout {t_roll / it:.3f}s train {t_train / it:.3f}s per iter {time.perf_counter() - t0:7.1f}s",
                   flush=True)
+    if a.save:
+        ppo.save(a.save)
     env.close()
 
 

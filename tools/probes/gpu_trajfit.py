@@ -18,9 +18,7 @@ Prints markdown; per-interval progress to stderr.
 """
 import argparse
 import os
-import re
 import sys
-import tempfile
 import time
 
 import numpy as np
@@ -35,27 +33,6 @@ from oracle import trajfit as T  # noqa: E402
 
 KEYS = os.path.join(ROOT, "tests", "golden", "humanoid_trajectory.xml")
 K, NU, FS = T.STEPS_PER_KEY, 21, T.FRAME_SKIP
-
-
-def variant_xml(name):
-    src = open(HUMANOID_XML).read()
-    if name == "truth":
-        return HUMANOID_XML
-    if name == "armature_zero":
-        src, n = re.subn(r'armature="[^"]*"', 'armature="0"', src)
-        assert n > 0
-    elif name == "friction_07":
-        # the floor geom's friction 1 -> 0.7: max(0.7, body 0.7) = 0.7, as a min-mixing rule would give
-        src, n = re.subn(r'(<geom[^>]*name="floor"[^>]*?)friction="[^"]*"', r'\1friction="0.7 0.005 0.0001"', src)
-        if n == 0:
-            src, n = re.subn(r'(<geom[^>]*name="floor")', r'\1 friction="0.7 0.005 0.0001"', src)
-        assert n > 0
-    else:
-        raise ValueError(name)
-    d = tempfile.mkdtemp()
-    p = os.path.join(d, f"humanoid_{name}.xml")
-    open(p, "w").write(src)
-    return p
 
 
 class GpuShooter:
@@ -186,7 +163,7 @@ def main():
     rows = []
     rng = np.random.default_rng(123)
     for var in a.variants.split(","):
-        xml = variant_xml(var)
+        xml = T.variant_xml(var)
         model = HsModel(xml)
         M = T.make_model(xml)
         shoot = GpuShooter(model, a.pop)
