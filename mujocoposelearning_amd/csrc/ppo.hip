@@ -550,6 +550,88 @@ __global__ __launch_bounds__(CS_COLS* CS_PHASES) void colsum_pair_kernel(const f
   }
 }
 
+
+// ------------------------------------------------------------------ fused 2-hidden-layer MLP forward
+// out = relu(relu(X W1 + b1) W2 + b2) W3 + b3 for one packed policy net (PPO rollout: the pi net's
+// mean per env step, the vf net's values once per rollout).  W1 [D][ld1], W2 [H][H], W3 [H][A] are
+// the packed ([in][out]) weights of ActorCritic.pack_heads, H = 256, A <= 32.  One workgroup (4 waves)
+// per 16 rows: the 16 x D input tile is staged in LDS, and each layer is v_mfma_f32_16x16x4_f32 tiles
+// (f32 in, f32 accumulate -- the fp32 GEMM's arithmetic in another summation order): wave w owns
+// output columns [64 w, 64 w + 64) of a hidden layer (4 accumulator tiles), B operands stream from
+// L2-resident weights, and the bias + ReLU epilogue writes the layer back to LDS for the next one.
+// Replaces three library GEMM launches and their two [N][256] HBM round trips.
+constexpr int MLP_H = 256, MLP_R = 16, MLP_TPB = 256, MLP_MAXD = 512;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(MLP_TPB) void mlp2_fwd_kernel(const float* __restrict__ X, int ldx, int D, int N,
+                                                           const float* __restrict__ W1, int ld1,
+                                                           const float* __restrict__ b1,
+                                                           const float* __restrict__ W2, const float* __restrict__ b2,
+                                                           const float* __restrict__ W3, int ld3,
+                                                           const float* __restrict__ b3, int A,
+                                                           float* __restrict__ out, int ldo) {
+  // row strides padded by one float: the 16 rows of an A operand fall in 16 different banks
+  __shared__ float xs[MLP_R * (MLP_MAXD + 1)];
+  __shared__ float hbuf[2][MLP_R * (MLP_H + 1)];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int row0 = blockIdx.x * MLP_R;
+  const int Dp = (D + 3) & ~3, sx = Dp + 1, sh = MLP_H + 1;
+  for (int e = threadIdx.x; e < MLP_R * Dp; e += MLP_TPB) {
+    const int r = e / Dp, c = e - r * Dp;
+    xs[r * sx + c] = (row0 + r < N && c < D) ? X[(size_t)(row0 + r) * ldx + c] : 0.f;
+  }
+  __syncthreads();
+  const int ar = lane & 15, ak = lane >> 4;        // A operand: row ar, k ak;  B: k ak, column ar
+  // hidden layer: dst = relu(src W + b), src in LDS (stride ss, K columns), W [K][ldw] global
+  auto hidden = [&](const float* src, int ss, int K, const float* __restrict__ W, int ldw,
+                    const float* __restrict__ bias, float* dst) {
+    const int c0 = wave * 64;
+    f32x4 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+    const float* wp = W + (size_t)ak * ldw + c0 + ar;
+#pragma unroll 4
+    for (int k = 0; k < K; k += 4) {
+      const float a = src[ar * ss + k + ak];
+      const bool kin = k + ak < K;
+#pragma unroll
+      for (int t = 0; t < 4; t++) {
+        const float b = kin ? wp[(size_t)k * ldw + 16 * t] : 0.f;
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      const int col = c0 + 16 * t + ar;
+      const float bb = bias[col];
+#pragma unroll
+      for (int r = 0; r < 4; r++) dst[(ak * 4 + r) * sh + col] = fmaxf(acc[t][r] + bb, 0.f);
+    }
+  };
+  hidden(xs, sx, D, W1, ld1, b1, hbuf[0]);
+  __syncthreads();
+  hidden(hbuf[0], sh, MLP_H, W2, MLP_H, b2, hbuf[1]);
+  __syncthreads();
+  // head: A <= 32 columns = 2 tiles, waves 0 and 1
+  if (wave < 2 && 16 * wave < A) {
+    const int col = 16 * wave + ar;
+    f32x4 acc = {0, 0, 0, 0};
+    const float* src = hbuf[1];
+#pragma unroll 4
+    for (int k = 0; k < MLP_H; k += 4) {
+      const float a = src[ar * sh + k + ak];
+      const float b = col < A ? W3[(size_t)(k + ak) * ld3 + col] : 0.f;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+    }
+    if (col < A) {
+      const float bb = b3[col];
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int row = row0 + ak * 4 + r;
+        if (row < N) out[(size_t)row * ldo + col] = acc[r] + bb;
+      }
+    }
+  }
+}
+
 }  // namespace
 
 // row chunks for colsum: enough workgroups to fill the chip (~1024) with >= 32 rows each;
@@ -730,6 +812,18 @@ hipError_t launch_colsum_pair(const float* x0, size_t rows0, size_t cols0, float
   if (t0 + t1 == 0) return hipSuccess;
   hipLaunchKernelGGL(colsum_pair_kernel, dim3(t0 + t1), dim3(CS_COLS, CS_PHASES), 0, stream, x0, rows0, cols0, out0, x1,
                      rows1, cols1, out1, t0);
+  return hipGetLastError();
+}
+
+
+hipError_t launch_mlp2_fwd(const float* X, int ldx, int D, int N, const float* W1, int ld1, const float* b1,
+                           const float* W2, const float* b2, const float* W3, int ld3, const float* b3, int A,
+                           float* out, int ldo, hipStream_t stream) {
+  if (D < 1 || D > MLP_MAXD || A < 1 || A > 32 || N < 0 || ld1 < MLP_H || ld3 < A || ldx < D || ldo < A)
+    return hipErrorInvalidValue;
+  if (N == 0) return hipSuccess;
+  mlp2_fwd_kernel<<<(N + MLP_R - 1) / MLP_R, MLP_TPB, 0, stream>>>(X, ldx, D, N, W1, ld1, b1, W2, b2, W3, ld3, b3, A,
+                                                                   out, ldo);
   return hipGetLastError();
 }
 

@@ -26,8 +26,10 @@ import torch.nn as nn
 
 
 from .ppo_ops import (Linear, _GaussLogpFn, _PPOLossFn, _SplitKLinearFn, _SplitKLinearReLUFn,  # noqa: F401
-                      _SPLITK_ROWS, adam_clip_step, colsum, gae_device, mlp_forward, ppo_act, ppo_loss,
-                      ppo_post)
+                      _SPLITK_ROWS, adam_clip_step, colsum, gae_device, mlp2_forward, mlp_forward, ppo_act,
+                      ppo_loss, ppo_post)
+
+FUSED_MLP = True      # rollout forward through the fused hs_mlp2_forward kernel where it applies
 
 
 def _flat_packed(pk):
@@ -161,6 +163,14 @@ class ActorCritic(nn.Module):
             return self(obs)[which]
         w1, b1, mid, w3, b3 = pk
         H = w1.shape[1] // 2
+        if (FUSED_MLP and obs.is_cuda and len(mid) == 1 and H == 256 and obs.shape[1] <= 512
+                and w3.shape[2] <= 32 and obs.dtype == torch.float32 and obs.stride(1) == 1):
+            # one fused MFMA launch (ppo.hip mlp2_fwd_kernel) instead of three GEMMs
+            A = w3.shape[2] if which == 0 else 1
+            out = mlp2_forward(obs, w1[:, which * H:(which + 1) * H], b1[which * H:(which + 1) * H].contiguous(),
+                               mid[0][0][which], mid[0][1][which, 0].contiguous(), w3[which], b3[which, 0].contiguous(),
+                               A)
+            return out if which == 0 else out[:, 0]
         act = (lambda b, x, w: torch._addmm_activation(b, x, w)) if obs.is_cuda else (  # noqa: E731
             lambda b, x, w: torch.addmm(b, x, w).relu_())
         h = act(b1[which * H:(which + 1) * H], obs, w1[:, which * H:(which + 1) * H])

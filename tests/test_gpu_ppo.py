@@ -503,3 +503,28 @@ def test_ppo_deep_net_arch_trains_on_gpu():
     assert all(not torch.equal(a, p.detach()) for a, p in zip(before, params))
     assert all(torch.isfinite(p).all() for p in params)
     env.close()
+
+
+@pytest.mark.parametrize("N,D", [(4096, 352), (1000, 350), (33, 7)])
+def test_fused_mlp_forward_matches_gemm_chain(N, D):
+    """hs_mlp2_forward (ppo.hip mlp2_fwd_kernel: MFMA f32 tiles, one launch) == the packed GEMM chain
+    of ActorCritic.net_forward for the pi mean and the vf value; odd row counts and input widths
+    (the 16-row tile and the K padding)."""
+    from mujocoposelearning_amd import ppo as P
+    torch.manual_seed(0)
+    pol = P.ActorCritic(D, 21, [256, 256], [256, 256], torch.nn.ReLU).cuda()
+    with torch.no_grad():
+        for p in pol.parameters():
+            p.add_(0.05 * torch.randn_like(p))
+    pol.pack_heads()
+    obs = torch.randn(N, D, device="cuda") * 2
+    outs = {}
+    for fused in (True, False):
+        P.FUSED_MLP = fused
+        try:
+            outs[fused] = [pol.net_forward(obs, 0).clone(), pol.net_forward(obs, 1).clone()]
+        finally:
+            P.FUSED_MLP = True
+    for a, b in zip(outs[True], outs[False]):
+        assert a.shape == b.shape
+        assert torch.allclose(a, b, rtol=1e-4, atol=1e-4 * (1 + float(b.abs().max()))), float((a - b).abs().max())
