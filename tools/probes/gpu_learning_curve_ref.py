@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--reward", default="stand")
     ap.add_argument("--every", type=int, default=20)
     ap.add_argument("--config", default="readme", choices=("readme", "configpy"))
+    ap.add_argument("--ent-coef", type=float, default=None, help="override the config's ent_coef (diagnosis runs)")
     ap.add_argument("--load", default=None, help="resume from a PPO.save zip (weights, Adam state, timesteps)")
     ap.add_argument("--save", default=None, help="PPO.save zip written at the end (resume with --load)")
     ap.add_argument("--stagger", action="store_true",
@@ -52,7 +53,10 @@ def main():
     cfg = env_config_from_kwargs({"reward_function": a.reward, "frame_skip": 3}, HUMANOID_XML)
     env = HumanoidVecEnv(cfg, n_envs=a.envs, model=HsModel(HUMANOID_XML), seed=a.seed, precision=a.precision)
     env.batch.configure(aux=False, ctrl=False)
-    ppo = PPO(env, n_steps=a.n_steps, seed=a.seed, **(PPO_KWARGS if a.config == "readme" else CONFIGPY_KWARGS))
+    kw = dict(PPO_KWARGS if a.config == "readme" else CONFIGPY_KWARGS)
+    if a.ent_coef is not None:
+        kw["ent_coef"] = a.ent_coef
+    ppo = PPO(env, n_steps=a.n_steps, seed=a.seed, **kw)
     if a.load:
         ppo.load(a.load)
     if a.stagger:        # after PPO's reset: env i's episode clock at i/N of the 667-step episode
