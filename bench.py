@@ -182,6 +182,7 @@ def main():
     ap.add_argument("--train-iters", type=int, default=2, help="PPO iterations of the train mode (0: skip)")
     ap.add_argument("--no-configs", action="store_true", help="skip the configs[3]/[4] legs")
     ap.add_argument("--no-fp32", action="store_true", help="skip the fp32 sim-only leg")
+    ap.add_argument("--no-tape", action="store_true", help="skip the open-loop tape leg (hs_step_tape)")
     ap.add_argument("--no-episodes", action="store_true", help="skip the full-episode T0/T1/T2 legs")
     ap.add_argument("--no-precondition", action="store_true",
                     help="time from a synchronized reset (standing humanoids only) instead of the staggered mix")
@@ -291,6 +292,23 @@ def main():
         barrier()
         return max_over_ranks(time.perf_counter() - t0), ev0.elapsed_time(ev1) / steps
 
+    def timed_tape(e, tape, steps, warmup, offset=0):
+        """The same window as ``timed`` as ONE tape launch (HsBatch.step_tape: K env steps, each env
+        pair's step t + 1 starting once its own step t is committed); open loop, bitwise the step
+        loop's results (tests/test_gpu_tape.py).  Returns (wall seconds max over ranks, ms per env step)."""
+        for k in range(warmup):
+            e.step_tensors(tape[(offset + k) % tape.shape[0]])
+        idx = torch.arange(offset + warmup, offset + warmup + steps, device=dev) % tape.shape[0]
+        tp = tape.index_select(0, idx).contiguous()
+        barrier()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        e.batch.step_tape(tp, outputs=False)
+        ev1.record(stream)
+        barrier()
+        return max_over_ranks(time.perf_counter() - t0), ev0.elapsed_time(ev1) / steps
+
     def ints_over_ranks(vals, op):
         """elementwise MAX / SUM of a list of per-rank integer counters over all ranks"""
         t = torch.tensor(vals, dtype=torch.int64, device=red_dev)
@@ -343,6 +361,20 @@ def main():
                         kernel_ms_per_launch=ms, stats=stats_of(e, tape, EPISODE + args.warmup + args.steps),
                         note="same workload and staggered episode mix, fp32 engine (parity within fp32 tolerances, "
                              "not the reference's fp64: see DESIGN.md 4)")
+        e.close()
+
+    # ---- open-loop tape leg: the same fp64 window as one tape launch (not the headline: a policy in
+    # the loop steps one env step per launch)
+    tape_leg = None
+    if not args.no_tape:
+        e = make_env(args.precision, 1000)
+        precondition(e, tape)
+        el, ms = timed_tape(e, tape, args.steps, args.warmup, offset=EPISODE)
+        tape_leg = dict(value=n * args.steps * ranks / el, unit="env_steps/s", dtype="f64" if args.precision == "fp64"
+                        else "f32", steps=args.steps, ms_per_env_step=ms, tape_aborts=e.batch.tape_aborts(),
+                        note="same workload, window and action tape as the headline, all timed env steps in ONE "
+                             "hs_step_tape launch (open loop: each env pair's step t+1 starts when its own step t "
+                             "is committed, so steps do not end on their slowest pair); bitwise the per-step results")
         e.close()
 
     # ---- full episodes from a synchronized reset on tapes T0 / T1 / T2, per phase
@@ -441,6 +473,12 @@ def main():
             r = dict(value=n_x * ks * ranks / el, unit="env_steps/s", n_envs_per_gpu=n_x, obs_dim=e.obs_dim,
                      workload=label)
             e.close()
+            if not args.no_tape:   # the same window as one open-loop tape launch
+                e = make_env(args.precision, 4000, cfg_x=cfg_x, n_x=n_x)
+                precondition(e, tp)
+                elt, _ = timed_tape(e, tp, ks, args.warmup, offset=EPISODE)
+                r["tape"] = dict(value=n_x * ks * ranks / elt, unit="env_steps/s", tape_aborts=e.batch.tape_aborts())
+                e.close()
             return r
         config_legs = {
             "configs[3]": leg({**cfg, "reward_config": {"type": "kneeling"}}, n,
@@ -570,6 +608,7 @@ def main():
             "train": train_res,
             "gae": gae_res,
             "sim_only_stream_groups": grouped,
+            "sim_only_tape": tape_leg,
             "other_configs": config_legs,
         }
         print(json.dumps(out))

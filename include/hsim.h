@@ -15,6 +15,7 @@
  *   hs_reset             <- HumanoidEnv.reset: mj_resetData + noise + one mj_step  custom_env.py:97-150
  *   hs_step              <- HumanoidEnv.step: frame_skip x mj_step, _get_state, reward, done
  *                           custom_env.py:152-230 (+ SB3 auto-reset on done)
+ *   hs_step_tape         <- K x HumanoidEnv.step over a given action tape (open loop), one launch
  *   hs_physics_step      <- raw `data.ctrl[:] = a; mujoco.mj_step(model, data)` custom_env.py:159-160
  *   hs_debug_lose_handoff   (test hook: mj_step's warning + mj_resetData path, custom_env.py:160)
  *   hs_state_io          <- reads/writes of data.qpos/qvel/qacc_warmstart/time/ctrl (custom_env.py:105-117)
@@ -165,6 +166,28 @@ int hs_get_config(const hs_batch* b, hs_env_config* cfg);
 int hs_reset(hs_batch* b, const uint8_t* mask, const void* qpos_noise, const void* qvel_noise, void* stream);
 /* actions: [N][nu] float32 device. Runs frame_skip substeps, writes obs/reward/terminated/truncated. */
 int hs_step(hs_batch* b, const float* actions, void* stream);
+/* Per-step outputs of hs_step_tape, device arrays (batch precision for obs / reward):
+ * obs [K][N][obs_dim], reward [K][N], terminated / truncated [K][N] uint8. */
+typedef struct hs_tape_out {
+  void* obs;
+  void* reward;
+  uint8_t* terminated;
+  uint8_t* truncated;
+} hs_tape_out;
+/* K = n_steps consecutive hs_step calls over an action tape: actions [K][N][nu] float32 device.
+ * Same results, bitwise, as K hs_step calls (states, per-step obs / reward / done flags, auto-resets
+ * and their final-step info; the terminal obs / info rows hold each env's last finished episode).
+ * One launch on the chunk-queue schedule with whole env steps as items: an env pair's step t + 1
+ * starts as soon as its own step t is committed, so steps of different pairs overlap and the launch
+ * does not end every step on its slowest pair.  out = NULL: only the batch's buffers (last step);
+ * otherwise every step's outputs, and the batch buffers as after the last step.  If an env overflows
+ * the resident contact tier the launch stops and the tape is replayed step by step (counted by
+ * hs_tape_aborts).  Synchronizes the stream.  1 <= K <= 511.  With HS_SCHED_DIRECT / SINGLE, or
+ * K = 1, it runs the K hs_step calls.  Open-loop stepping (a given action tape: benchmarks,
+ * trajectory evaluation); a policy in the loop steps with hs_step. */
+int hs_step_tape(hs_batch* b, const float* actions, int n_steps, const hs_tape_out* out, void* stream);
+/* tape launches of this batch that were replayed step by step (resident-tier overflow) */
+int hs_tape_aborts(const hs_batch* b, uint64_t* n);
 /* Auto-reset noise source of hs_step: [N][nq] / [N][nv] device arrays of the batch precision with
  * the raw U(-noise_scale, noise_scale) draws of the NEXT reset of each env (the kernel applies the
  * x0.1 height factor and zeroes the quaternion part, custom_env.py:109-114); NULL, NULL = the

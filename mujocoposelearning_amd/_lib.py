@@ -36,6 +36,10 @@ class hs_buffers(C.Structure):
                                           "terminal_total_reward")]
 
 
+class hs_tape_out(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("obs", "reward", "terminated", "truncated")]
+
+
 class hs_batch_info(C.Structure):
     _fields_ = [(n, C.c_int) for n in ("n_envs", "precision", "nq", "nv", "nu", "nbody", "obs_dim", "elem_size",
                                        "resident_con", "resident_efc", "wide_con", "wide_efc", "resident_waves",
@@ -74,6 +78,8 @@ def lib():
         "hs_set_seed": (i, [vp, u64]),
         "hs_reset": (i, [vp, vp, vp, vp, vp]),
         "hs_step": (i, [vp, vp, vp]),
+        "hs_step_tape": (i, [vp, vp, i, vp, vp]),
+        "hs_tape_aborts": (i, [vp, vp]),
         "hs_set_autoreset_noise": (i, [vp, vp, vp]),
         "hs_physics_step": (i, [vp, vp, i, vp]),
         "hs_state_io": (i, [vp, i, vp, vp, vp, vp, vp]),
@@ -112,7 +118,7 @@ def lib():
 
 
 EXPORTED = ("hs_model_load", "hs_model_free", "hs_model_field", "hs_batch_create", "hs_batch_destroy",
-            "hs_batch_get_info", "hs_get_buffers", "hs_set_config", "hs_set_seed", "hs_get_config", "hs_reset", "hs_step", "hs_set_autoreset_noise",
+            "hs_batch_get_info", "hs_get_buffers", "hs_set_config", "hs_set_seed", "hs_get_config", "hs_reset", "hs_step", "hs_step_tape", "hs_tape_aborts", "hs_set_autoreset_noise",
             "hs_physics_step", "hs_state_io", "hs_kinematics", "hs_set_debug", "hs_debug_lose_handoff", "hs_get_debug", "hs_synchronize", "hs_batch_counters", "hs_gae",
             "hs_ppo_act", "hs_ppo_post", "hs_gauss_logp", "hs_gauss_logp_grad",
             "hs_ppo_loss_workspace", "hs_ppo_loss", "hs_ppo_loss_grad", "hs_adam_workspace", "hs_adam_clip",

@@ -245,6 +245,40 @@ class HsBatch:
         self._launch(lambda h, lo, hi, st: check(lib().hs_step(h, a.data_ptr() + lo * row, st)), a, join=join)
         return self.t["obs"], self.t["reward"], self.t["terminated"], self.t["truncated"]
 
+    def step_tape(self, actions, outputs=True):
+        """K consecutive ``step`` calls over an action tape [K, N, nu] (float32, on device) in one
+        launch (hs_step_tape: a pair's step t + 1 starts once its own step t is committed, so the
+        launch does not end every step on its slowest pair).  Bitwise the results of K ``step``
+        calls.  outputs=True returns the per-step (obs [K, N, obs_dim], reward [K, N], terminated,
+        truncated [K, N] uint8); the batch's own buffers hold the last step either way.  Open loop:
+        benchmarks, trajectory evaluation -- a policy in the loop steps with ``step``.  Synchronous;
+        one stream group only."""
+        torch = _torch()
+        if len(self._groups) != 1:
+            raise NotImplementedError("step_tape: one stream group only")
+        a = torch.as_tensor(actions, device=self.device).to(torch.float32).contiguous()
+        if a.dim() != 3 or a.shape[1:] != (self.n, self.model.nu):
+            raise ValueError(f"step_tape: actions must be [K, {self.n}, {self.model.nu}], got {tuple(a.shape)}")
+        K = a.shape[0]
+        res, out = None, None
+        if outputs:
+            res = (torch.empty(K, self.n, self.obs_dim, dtype=self.dtype, device=self.device),
+                   torch.empty(K, self.n, dtype=self.dtype, device=self.device),
+                   torch.empty(K, self.n, dtype=torch.uint8, device=self.device),
+                   torch.empty(K, self.n, dtype=torch.uint8, device=self.device))
+            out = _lib.hs_tape_out(*[x.data_ptr() for x in res])
+        h = self._groups[0][0]
+        check(lib().hs_step_tape(h, a.data_ptr(), K, C.byref(out) if out is not None else None, self.stream))
+        if outputs:
+            return res
+        return self.t["obs"], self.t["reward"], self.t["terminated"], self.t["truncated"]
+
+    def tape_aborts(self):
+        """Tape launches replayed step by step because an env overflowed the resident tier."""
+        v = C.c_uint64(0)
+        check(lib().hs_tape_aborts(self._groups[0][0], C.byref(v)))
+        return int(v.value)
+
     def physics_step(self, ctrl=None, nsub=1):
         """nsub raw mj_step's with the given ctrl [N, nu] (None keeps the current ctrl)."""
         torch = _torch()

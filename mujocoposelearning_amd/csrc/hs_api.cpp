@@ -1,6 +1,8 @@
 // hsim C ABI implementation (product).  See include/hsim.h for the reference interfaces replaced.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -34,6 +36,8 @@ struct hs_batch {
   hs_env_config cfg{};
   bool ctrl_stale = false;                   // env steps ran with HS_OUT_CTRL off: buf.ctrl is not data.ctrl
   int lose_pair1 = 0;                        // hs_debug_lose_handoff test hook (pair + 1; 0 = off)
+  void* tape_backup = nullptr;               // hs_step_tape: the state before a tape launch (replay on abort)
+  unsigned long long tape_aborts = 0;        // tape launches replayed step by step (resident-tier overflow)
 };
 
 namespace {
@@ -155,18 +159,24 @@ hs::StepParams params_of(const hs_batch* b, int mode, int nsub) {
 }
 
 int launch(hs_batch* b, int mode, const float* act, const uint8_t* mask, const void* nq, const void* nvz, int nsub,
-           void* stream) {
+           void* stream, int nsteps = 1, const hs_tape_out* tape = nullptr) {
   if (!b) return fail("null batch");
   DeviceGuard g(b->device);
   hipError_t e;
   auto p = params_of(b, mode, nsub);
+  p.nsteps = nsteps;
   int nv = b->model->host.nv;
-  if (b->precision == HS_FP64)
+  if (b->precision == HS_FP64) {
+    hs::TapeOut<double> to{tape ? (double*)tape->obs : nullptr, tape ? (double*)tape->reward : nullptr,
+                           tape ? tape->terminated : nullptr, tape ? tape->truncated : nullptr};
     e = hs::launch_step<double>((const hs::DevModel<double>*)b->dmodel, nv, env_buffers<double>(b), act, mask,
-                                (const double*)nq, (const double*)nvz, p, b->n, (hipStream_t)stream);
-  else
+                                (const double*)nq, (const double*)nvz, p, b->n, (hipStream_t)stream, &to);
+  } else {
+    hs::TapeOut<float> to{tape ? (float*)tape->obs : nullptr, tape ? (float*)tape->reward : nullptr,
+                          tape ? tape->terminated : nullptr, tape ? tape->truncated : nullptr};
     e = hs::launch_step<float>((const hs::DevModel<float>*)b->dmodel, nv, env_buffers<float>(b), act, mask,
-                               (const float*)nq, (const float*)nvz, p, b->n, (hipStream_t)stream);
+                               (const float*)nq, (const float*)nvz, p, b->n, (hipStream_t)stream, &to);
+  }
   if (e == hipErrorInvalidValue) return fail("no kernel instance for this model's nv (compiled: nv = 27)");
   return hip_ok(e, "step kernel launch") ? 0 : -1;
 }
@@ -398,6 +408,7 @@ void hs_batch_destroy(hs_batch* b) {
   if (b->redo_total) (void)hipFree(b->redo_total);
   if (b->mid) uc_release(b->device, (size_t)b->n * hs::MIDDIM * (b->precision == HS_FP64 ? 8 : 4), b->mid);
   if (b->qsync) uc_release(b->device, hs::qsync_words(b->n) * sizeof(int), b->qsync);
+  if (b->tape_backup) (void)hipFree(b->tape_backup);
   delete b;
 }
 
@@ -470,6 +481,118 @@ int hs_step(hs_batch* b, const float* actions, void* stream) {
   // a step with the ctrl copy on rewrites every env's data.ctrl (commit), one with it off leaves it stale
   if (rc == 0) b->ctrl_stale = !(b->cfg.outputs & HS_OUT_CTRL);
   return rc;
+}
+
+int hs_step_tape(hs_batch* b, const float* actions, int n_steps, const hs_tape_out* out, void* stream) {
+  if (!b) return fail("null batch");
+  if (!actions) return fail("hs_step_tape: actions must not be NULL");
+  if (n_steps < 1 || n_steps > hs::QTAG_STEPS)
+    return fail("hs_step_tape: n_steps must be in [1, " + std::to_string(hs::QTAG_STEPS) + "]");
+  if (out && (!out->obs || !out->reward || !out->terminated || !out->truncated))
+    return fail("hs_step_tape: pass all four per-step output arrays, or out = NULL");
+  DeviceGuard g(b->device);
+  const auto& h = b->model->host;
+  const size_t N = (size_t)b->n, es = b->precision == HS_FP64 ? 8 : 4, nu = (size_t)h.nu;
+  hipStream_t st = (hipStream_t)stream;
+  // n_steps hs_step calls, each step's outputs copied into its slice (the reference path, and the
+  // replay of an aborted tape launch)
+  auto per_step = [&]() -> int {
+    for (int t = 0; t < n_steps; t++) {
+      int rc = hs_step(b, actions + (size_t)t * N * nu, stream);
+      if (rc) return rc;
+      if (out) {
+        const size_t d = (size_t)b->obs_dim;
+        if (!hip_ok(hipMemcpyAsync((char*)out->obs + t * N * d * es, b->buf.obs, N * d * es, hipMemcpyDeviceToDevice, st),
+                    "tape obs") ||
+            !hip_ok(hipMemcpyAsync((char*)out->reward + t * N * es, b->buf.reward, N * es, hipMemcpyDeviceToDevice, st),
+                    "tape reward") ||
+            !hip_ok(hipMemcpyAsync(out->terminated + t * N, b->buf.terminated, N, hipMemcpyDeviceToDevice, st),
+                    "tape terminated") ||
+            !hip_ok(hipMemcpyAsync(out->truncated + t * N, b->buf.truncated, N, hipMemcpyDeviceToDevice, st),
+                    "tape truncated"))
+          return -1;
+      }
+    }
+    return 0;
+  };
+  const int resident = b->precision == HS_FP64 ? hs::resident_waves<double>(h.solver == 1)
+                                               : hs::resident_waves<float>(h.solver == 1);
+  const bool tape_sched = b->cfg.schedule == HS_SCHED_AUTO || b->cfg.schedule == HS_SCHED_FIXED_ORDER;
+  // without auto-reset a finished env keeps rewriting its terminal info every step (one launch
+  // must write each batch address once, see hs_kernels.hip step_pair): step by step
+  if (n_steps == 1 || !tape_sched || !b->cfg.autoreset || resident <= 0 || !b->mid || !b->qsync) return per_step();
+  // each env finishes at most one episode per launch (its terminal obs / info rows are then written
+  // once): launches of at most the shortest episode's length -- an episode starts at time = one
+  // timestep (the reset's mj_step) and ends at time >= duration (custom_env.py:213) or at max_steps
+  const double dt = h.timestep * b->cfg.frame_skip;
+  const double spans = std::floor((b->cfg.duration - h.timestep) / dt - 1e-9);
+  const int min_len = (int)std::max(1.0, std::min((double)b->cfg.max_steps, spans));
+  if (n_steps > min_len) {
+    for (int t0 = 0; t0 < n_steps; t0 += min_len) {
+      const int k = std::min(min_len, n_steps - t0);
+      hs_tape_out sub{};
+      if (out) {
+        sub.obs = (char*)out->obs + (size_t)t0 * N * b->obs_dim * es;
+        sub.reward = (char*)out->reward + (size_t)t0 * N * es;
+        sub.terminated = out->terminated + (size_t)t0 * N;
+        sub.truncated = out->truncated + (size_t)t0 * N;
+      }
+      int rc = hs_step_tape(b, actions + (size_t)t0 * N * nu, k, out ? &sub : nullptr, stream);
+      if (rc) return rc;
+    }
+    return 0;
+  }
+  // state before the launch: an env that overflows the resident tier stops the tape launch
+  // (QS_ABORT), and the tape is then replayed step by step from here (the wide tier re-runs the
+  // overflowing steps) -- the same results, bitwise, as n_steps hs_step calls either way
+  struct Region { void* p; size_t bytes; } regs[] = {
+      {b->buf.qpos, N * h.nq * es}, {b->buf.qvel, N * h.nv * es}, {b->buf.qacc_warmstart, N * h.nv * es},
+      {b->buf.ctrl, N * nu * es}, {b->buf.time, N * es}, {b->buf.total_reward, N * es},
+      {b->buf.step_count, N * 4}, {b->buf.episode, N * 4}, {b->buf.warning, N * HS_NWARN * 4},
+      {b->redo_total, sizeof(unsigned long long)}};
+  size_t total = 0;
+  for (auto& r : regs) total += (r.bytes + 255) & ~(size_t)255;
+  if (!b->tape_backup && !hip_ok(hipMalloc(&b->tape_backup, total), "hipMalloc(tape backup)")) return -1;
+  size_t off = 0;
+  for (auto& r : regs) {
+    if (!hip_ok(hipMemcpyAsync((char*)b->tape_backup + off, r.p, r.bytes, hipMemcpyDeviceToDevice, st), "tape backup"))
+      return -1;
+    off += (r.bytes + 255) & ~(size_t)255;
+  }
+  if (!hip_ok(hipMemsetAsync(b->qsync + hs::QS_ABORT, 0, sizeof(int), st), "tape abort word")) return -1;
+  int rc = launch(b, hs::MODE_ENV_STEP, actions, nullptr, b->ar_qpos_noise, b->ar_qvel_noise, b->cfg.frame_skip,
+                  stream, n_steps, out);
+  if (rc) return rc;
+  int aborted = 0;
+  if (!hip_ok(hipMemcpyAsync(&aborted, b->qsync + hs::QS_ABORT, sizeof(int), hipMemcpyDeviceToHost, st),
+              "tape abort word") ||
+      !hip_ok(hipStreamSynchronize(st), "tape launch"))
+    return -1;
+  if (aborted) {
+    off = 0;
+    for (auto& r : regs) {
+      if (!hip_ok(hipMemcpyAsync(r.p, (char*)b->tape_backup + off, r.bytes, hipMemcpyDeviceToDevice, st), "tape restore"))
+        return -1;
+      off += (r.bytes + 255) & ~(size_t)255;
+    }
+    if (!hip_ok(hipMemsetAsync(b->redo, 0, 2 * sizeof(int), st), "tape redo list")) return -1;
+    b->tape_aborts++;
+    return per_step();
+  }
+  b->ctrl_stale = !(b->cfg.outputs & HS_OUT_CTRL);
+  if (out) {   // the batch's own output buffers hold the last step, as after n_steps hs_step calls
+    const size_t d = (size_t)b->obs_dim, t = (size_t)n_steps - 1;
+    if (!hip_ok(hipMemcpyAsync(b->buf.obs, (char*)out->obs + t * N * d * es, N * d * es, hipMemcpyDeviceToDevice, st),
+                "tape obs") ||
+        !hip_ok(hipMemcpyAsync(b->buf.reward, (char*)out->reward + t * N * es, N * es, hipMemcpyDeviceToDevice, st),
+                "tape reward") ||
+        !hip_ok(hipMemcpyAsync(b->buf.terminated, out->terminated + t * N, N, hipMemcpyDeviceToDevice, st),
+                "tape terminated") ||
+        !hip_ok(hipMemcpyAsync(b->buf.truncated, out->truncated + t * N, N, hipMemcpyDeviceToDevice, st),
+                "tape truncated"))
+      return -1;
+  }
+  return 0;
 }
 
 int hs_debug_lose_handoff(hs_batch* b, int env) {
@@ -719,6 +842,12 @@ int hs_batch_counters(const hs_batch* b, uint64_t* wide_reruns) {
       !hip_ok(hipMemcpy(&v, b->redo_total, sizeof v, hipMemcpyDeviceToHost), "counters"))
     return -1;
   *wide_reruns = v;
+  return 0;
+}
+
+int hs_tape_aborts(const hs_batch* b, uint64_t* n) {
+  if (!b || !n) return fail("null argument");
+  *n = b->tape_aborts;
   return 0;
 }
 

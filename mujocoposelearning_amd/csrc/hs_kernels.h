@@ -10,15 +10,25 @@ namespace hs {
 
 constexpr int AUXDIM = MAXDOF + 8;   // per env: qacc[nv], com[3], ncon, nefc, newton iters, solver flag
 constexpr int DBGDIM = 32768;        // stage dump (env 0 only) for parity debugging
-// hand-off row of a queued env step (qpos, qvel, qacc_warmstart, time, warning counters)
+// hand-off row of a queued env step (qpos, qvel, qacc_warmstart, time, warning counters, and the
+// env bookkeeping a tape launch carries from one env step to the next: step count, episode, return)
 constexpr int MID_Q = 0, MID_V = MAXQ, MID_WS = MAXQ + MAXDOF, MID_TIME = MAXQ + 2 * MAXDOF, MID_W = MID_TIME + 1;
+constexpr int MID_SC = MID_W + 4, MID_EP = MID_W + 5, MID_TOT = MID_W + 6;
 constexpr int MIDDIM = MID_W + 7;
 // chunk-queue sync words (uncached device memory): claim counter, exit counter, launch epoch,
 // per-pair flags.  A pair's flag holds the tag of the launch whose first chunk last handed its state
 // over (tag = epoch + 1, the epoch advanced by the last wave out of every queued launch), so a flag
 // left over from an earlier launch -- e.g. by a producer that arrived after its consumer timed out
-// -- never matches: no reset store, no returning atomic.
-constexpr int QS_HEAD = 0, QS_EXIT = 1, QS_EPOCH = 2, QS_FLAG = 3;
+// -- never matches: no reset store, no returning atomic.  QS_ABORT: a tape launch (p.nsteps > 1)
+// stops when an env overflows the resident tier (the host replays the tape step by step).
+constexpr int QS_HEAD = 0, QS_EXIT = 1, QS_EPOCH = 2, QS_ABORT = 3, QS_FLAG = 4;
+// flag value of a queued hand-off: the launch tag (epoch + 1, 20 bits) and the hand-off's position
+// in the launch (the env step of a tape launch and its stage), so a consumer waits for exactly its
+// predecessor: stage 0 = first chunk of step t handed over, 1 = step t committed
+constexpr int QTAG_STEPS = 511;   // most env steps per tape launch
+__host__ __device__ constexpr int qtag(uint32_t epoch, int t, int stage) {
+  return (int)((((epoch & 0xFFFFFu) + 1u) << 10) | (uint32_t)(2 * t + stage + 1));
+}
 // Cost-ordered claims: every queued launch measures each pair's duration (first chunk + last
 // substep, 100 MHz realtime clock) and counts the pair into one of QNB buckets of QBIN ticks,
 // heaviest first; the next queued launch claims the pairs bucket by bucket (a counting sort done
@@ -90,6 +100,15 @@ struct StepParams {
   int qorder;            // chunk queue: 1 = cost-ordered claims (QNB buckets), 0 = the qmul permutation only
   int dbg_lose_pair1;    // test hook (hs_debug_lose_handoff): pair + 1 whose hand-off is treated as lost; 0 = off
   int single;            // set by launch_step: 1 = one env per wave (upper half-wave a ghost), 0 = env pairs
+  int nsteps;            // env steps per launch: 1, or a tape launch of nsteps (MODE_ENV_STEP, chunk queue)
+};
+// per-step outputs of a tape launch ([nsteps][N][...] each; null: the batch's own buffers, last step wins)
+template <typename T>
+struct TapeOut {
+  T* obs;
+  T* reward;
+  uint8_t* terminated;
+  uint8_t* truncated;
 };
 // hs_env_config.schedule (SCHED_FIXED_ORDER: AUTO with the chunk queue's claims in the fixed
 // permutation instead of cost order -- A/B runs and tests)
@@ -101,10 +120,13 @@ enum Solver { SOLVER_NEWTON = 0, SOLVER_PGS = 1 };
 
 // actions: [N][nu] float32 (may be null in MODE_RESET); reset_mask: [N] (null = all);
 // noise_qpos/noise_qvel: [N][nq]/[N][nv] host-supplied reset noise (null = device RNG).
+// p.nsteps > 1: a tape launch -- actions [nsteps][N][nu], outputs per step in `tape` (may be null), env
+// steps of one env pair run back to back on the chunk queue with the state handed over through
+// b.mid; no wide-tier launch follows (an overflow sets qsync[QS_ABORT], the host replays the tape).
 template <typename T>
 hipError_t launch_step(const DevModel<T>* dmodel, int nv, const EnvBuffers<T>& b, const float* actions,
                        const uint8_t* reset_mask, const T* noise_qpos, const T* noise_qvel,
-                       const StepParams& p, int nenv, hipStream_t stream);
+                       const StepParams& p, int nenv, hipStream_t stream, const TapeOut<T>* tape = nullptr);
 
 // waves of the resident step-kernel instance the current device holds at once (0 if unknown)
 template <typename T>

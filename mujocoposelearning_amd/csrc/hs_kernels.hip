@@ -223,6 +223,7 @@ struct KArgs {
   const T* nz_v;              // [N][nv] or null
   StepParams p;
   int nenv;
+  TapeOut<T> tape;            // per-step outputs of a tape launch (p.nsteps > 1), or all null
 };
 template <typename T>
 using KPtr = const __attribute__((address_space(4))) KArgs<T>*;
@@ -237,6 +238,19 @@ __device__ __forceinline__ bool bit(uint32_t mask, int i) { return i < 32 && ((m
 template <typename T>
 __device__ __forceinline__ bool isbad(T x) {
   return !(x <= T(1e10) && x >= T(-1e10));   // NaN or |x| > mjMAXVAL
+}
+
+// Chunk-queue hand-off rows (b.mid, uncached) are written and read at agent scope.  A row is rewritten
+// by one CU and read by another, and a tape launch reads env e's row once per env step, often on a CU
+// whose vector L1 still holds the line from an earlier step: plain loads could return that stale line
+// (measured: tape launches were nondeterministic with plain loads, tests/test_gpu_tape.py).
+template <typename T>
+__device__ __forceinline__ T row_ld(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ void row_st(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------------------------ small algebra
@@ -2268,7 +2282,7 @@ __device__ __forceinline__ void commit(MPtr<T> m, KPtr<T> k, const Stepper<T, NV
 template <typename T, int NV, bool PGS, typename C>
 __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCache<T, C>* pcache, int idx,
                                           int nidx, const int* list, int s0, int s1, int pair, bool ghost = false,
-                                          int tag = 0) {
+                                          int wait_tag = 0, int set_tag = 0, int tstep = 0) {
   constexpr bool WIDE = C::WIDE;
   const int lane = opaque_v(threadIdx.x);   // (no lane-derived value hoisted out of the chunk-queue loop)
   const bool up = lane >= HL;
@@ -2290,25 +2304,35 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
   uint32_t episode;
   T total, act;
   {
-    if (s0 > 0) {   // queued last substep: wait for the pair's first chunk to hand the state over
+    if (wait_tag != 0) {   // queued: wait for the pair's previous chunk (or tape step) to hand the state over
       int* flag = ka->b.qsync + QS_FLAG + pair;
-      int seen = 0;
+      int seen = 0, abort = 0;
       if (lane == 0) {   // bounded (~0.5 s): a broken hand-off must not hang the GPU
         int w = 0;
         if (pair + 1 != ka->p.dbg_lose_pair1)   // test hook: treat this pair's hand-off as lost
-          while ((seen = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != tag && ++w < (1 << 22))
+          while ((seen = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != wait_tag &&
+                 ++w < (1 << 22)) {
+            // a tape launch that aborted (overflow) never hands this pair over: leave at once
+            if (tstep > 0 && (abort = __hip_atomic_load(ka->b.qsync + QS_ABORT, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT)) != 0)
+              break;
             __builtin_amdgcn_s_sleep(2);
+          }
       }
-      const bool lost = __builtin_amdgcn_readfirstlane(seen) != tag;
+      if (__builtin_amdgcn_readfirstlane(abort) != 0) return;   // results discarded: the host replays
+      const bool lost = __builtin_amdgcn_readfirstlane(seen) != wait_tag;
       WSYNC();   // (compiler order: the row loads stay behind the poll)
       const T* r = ka->b.mid + (size_t)env_id * MIDDIM;
-      time = r[MID_TIME];
-      xws = (sl < nv) ? r[MID_WS + sl] : T(0);
-      if (sl < nq) s.qpos[sl] = r[MID_Q + sl];
-      if (sl + HL < nq) s.qpos[sl + HL] = r[MID_Q + sl + HL];
-      if (sl < nv) s.qvel[sl] = r[MID_V + sl];
+      time = row_ld(r + MID_TIME);
+      xws = (sl < nv) ? row_ld(r + MID_WS + sl) : T(0);
+      if (sl < nq) s.qpos[sl] = row_ld(r + MID_Q + sl);
+      if (sl + HL < nq) s.qpos[sl + HL] = row_ld(r + MID_Q + sl + HL);
+      if (sl < nv) s.qvel[sl] = row_ld(r + MID_V + sl);
 #pragma unroll
-      for (int w = 0; w < NWARN; w++) warn[w] = (int)r[MID_W + w];
+      for (int w = 0; w < NWARN; w++) warn[w] = (int)row_ld(r + MID_W + w);
+      step_count = (int)row_ld(r + MID_SC);
+      episode = (uint32_t)row_ld(r + MID_EP);
+      total = row_ld(r + MID_TOT);
       // never seen in practice; if it were, the state is poisoned so that mj_checkPos resets the
       // env and counts HS_WARN_BADQPOS -- loud, like MuJoCo's warning path, never silent
       if (lost && sl == 2) s.qpos[2] = T(NAN);
@@ -2318,16 +2342,17 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
       if (sl < nq) s.qpos[sl] = ka->b.qpos[(size_t)env_id * nq + sl];
       if (sl + HL < nq) s.qpos[sl + HL] = ka->b.qpos[(size_t)env_id * nq + sl + HL];
       if (sl < nv) s.qvel[sl] = ka->b.qvel[(size_t)env_id * nv + sl];
+      step_count = ka->b.step_count[env_id];
+      episode = ka->b.episode[env_id];
+      total = ka->b.total_reward[env_id];
     }
     // data.ctrl is an input only to a raw physics call that keeps the current ctrl; env steps set
     // it from the action, resets zero it
     const float* actions = ka->actions;
     if (sl < nu) s.ctrl[sl] = (mode == MODE_PHYSICS && !actions) ? ka->b.ctrl[(size_t)env_id * nu + sl] : T(0);
-    step_count = ka->b.step_count[env_id];
-    episode = ka->b.episode[env_id];
-    total = ka->b.total_reward[env_id];
-    // the action is the same for all substeps: one load, issued with the state loads
-    act = (actions && sl < nu) ? (T)actions[(size_t)env_id * nu + sl] : T(0);
+    // the action is the same for all substeps: one load, issued with the state loads (a tape
+    // launch's step tstep reads its own [N][nu] slice)
+    act = (actions && sl < nu) ? (T)actions[((size_t)tstep * ka->nenv + env_id) * nu + sl] : T(0);
   }
   WSYNC();
   st.clk.start();
@@ -2347,6 +2372,37 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
       }
       return true;
     }
+  };
+  // Tape launch (set_tag on a whole-step item): the state goes on to the pair's next env step only
+  // through its hand-off row (uncached), together with the warning counters accumulated so far.
+  // Only the tape's LAST step commits to the batch buffers: consecutive steps of one env may run on
+  // different XCDs, whose L2s are not coherent with each other, so two steps writing the same
+  // batch address would leave whichever dirty line is written back last.  For the same reason the
+  // batch's obs / reward / done rows are written by the last step only when the tape has no
+  // per-step outputs, and the host keeps each env to at most one finished episode per tape launch
+  // (hs_step_tape), so its terminal obs / info rows are written once.
+  const bool tape_handoff = set_tag != 0 && s1 == ka->p.nsub;
+  const bool tape_final = !(ka->p.nsteps > 1 && tstep < ka->p.nsteps - 1);
+  bool deferred = false;
+  auto handoff = [&](KPtr<T> k, int env, T time_, T xws_, int sc, uint32_t ep, T tot) {
+    T* r = k->b.mid + (size_t)env * MIDDIM;
+    if (sl < nq) row_st(r + MID_Q + sl, s.qpos[sl]);
+    if (sl + HL < nq) row_st(r + MID_Q + sl + HL, s.qpos[sl + HL]);
+    if (sl < nv) { row_st(r + MID_V + sl, s.qvel[sl]); row_st(r + MID_WS + sl, xws_); }
+    if (sl == 0) {
+      row_st(r + MID_TIME, time_);
+#pragma unroll
+      for (int w = 0; w < NWARN; w++) row_st(r + MID_W + w, (T)warn[w]);
+      row_st(r + MID_SC, (T)sc);
+      row_st(r + MID_EP, (T)ep);
+      row_st(r + MID_TOT, tot);
+    }
+  };
+  // this env step's output rows: the tape's slice tstep, or the batch's own buffers (null: an
+  // intermediate step of a tape launch without per-step outputs writes none)
+  auto obs_row = [&](KPtr<T> k, int env, int obs_dim) -> T* {
+    if (k->tape.obs) return k->tape.obs + ((size_t)tstep * k->nenv + env) * obs_dim;
+    return tape_final ? k->b.obs + (size_t)env * obs_dim : nullptr;
   };
 
   // Both halves always run the same instruction stream; a half that is inactive (ghost env,
@@ -2371,17 +2427,20 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
       KPtr<T> k = opaque(ka);
       if (active) {
         T* r = k->b.mid + (size_t)env * MIDDIM;
-        if (sl < nq) r[MID_Q + sl] = s.qpos[sl];
-        if (sl + HL < nq) r[MID_Q + sl + HL] = s.qpos[sl + HL];
-        if (sl < nv) { r[MID_V + sl] = s.qvel[sl]; r[MID_WS + sl] = xws; }
+        if (sl < nq) row_st(r + MID_Q + sl, s.qpos[sl]);
+        if (sl + HL < nq) row_st(r + MID_Q + sl + HL, s.qpos[sl + HL]);
+        if (sl < nv) { row_st(r + MID_V + sl, s.qvel[sl]); row_st(r + MID_WS + sl, xws); }
         if (sl == 0) {
-          r[MID_TIME] = time;
+          row_st(r + MID_TIME, time);
 #pragma unroll
-          for (int w = 0; w < NWARN; w++) r[MID_W + w] = (T)warn[w];
+          for (int w = 0; w < NWARN; w++) row_st(r + MID_W + w, (T)warn[w]);
+          row_st(r + MID_SC, (T)step_count);
+          row_st(r + MID_EP, (T)episode);
+          row_st(r + MID_TOT, total);
         }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the row is in memory before the flag is
-      if (lane == 0) __hip_atomic_store(k->b.qsync + QS_FLAG + pair, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) __hip_atomic_store(k->b.qsync + QS_FLAG + pair, set_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       HS_FLUSH();
       break;
     }
@@ -2390,7 +2449,8 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
         KPtr<T> k = opaque(ka);
         const int obs_dim = k->p.obs_dim;
         HS_STAMP(st.clk, 22);
-        if (active) write_obs(st.m, s, sl, st.qfa, k->b.obs + (size_t)env * obs_dim, obs_dim);
+        T* orow = obs_row(k, env, obs_dim);
+        if (active && orow) write_obs(st.m, s, sl, st.qfa, orow, obs_dim);
         HS_STAMP(st.clk, 23);
         if (k->p.mode == MODE_ENV_STEP) {
           step_count += 1;
@@ -2404,10 +2464,11 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
           HS_STAMP(st.clk, 25);
           total += r;
           bool term = (double)time >= k->p.duration;
-          if (sl == 0 && active) {
-            k->b.reward[env] = r;
-            k->b.terminated[env] = term;
-            k->b.truncated[env] = trunc;
+          if (sl == 0 && active && (k->tape.reward || tape_final)) {
+            const size_t o = k->tape.reward ? (size_t)tstep * k->nenv : 0;
+            (k->tape.reward ? k->tape.reward : k->b.reward)[o + env] = r;
+            (k->tape.terminated ? k->tape.terminated : k->b.terminated)[o + env] = term;
+            (k->tape.truncated ? k->tape.truncated : k->b.truncated)[o + env] = trunc;
           }
           // the final step's info of a finished episode (SubprocVecEnv returns its step_count /
           // total_reward before resetting, custom_env.py:216-224), with or without auto-reset
@@ -2421,7 +2482,12 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
           }
         }
         if (active && !do_reset) {
-          if (!defer(k)) commit(st.m, k, st, env, time, xws, step_count, episode, total, warn, k->p.full_state != 0);
+          if (!defer(k)) {
+            if (tape_final) commit(st.m, k, st, env, time, xws, step_count, episode, total, warn, k->p.full_state != 0);
+            if (tape_handoff) handoff(k, env, time, xws, step_count, episode, total);
+          } else {
+            deferred = true;
+          }
           active = false;   // committed (or deferred); a reset pass below is scratch work for this half
         }
       }
@@ -2456,8 +2522,14 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
         KPtr<T> k = opaque(ka);
         if (k->b.dbg && env == 0) dump_debug(st, k->b.dbg);
         const int obs_dim = k->p.obs_dim;
-        write_obs(st.m, s, sl, st.qfa, k->b.obs + (size_t)env * obs_dim, obs_dim);
-        if (!defer(k)) commit(st.m, k, st, env, time, xws, 0, episode, T(0), warn, k->p.full_state != 0);
+        T* orow = obs_row(k, env, obs_dim);
+        if (orow) write_obs(st.m, s, sl, st.qfa, orow, obs_dim);
+        if (!defer(k)) {
+          if (tape_final) commit(st.m, k, st, env, time, xws, 0, episode, T(0), warn, k->p.full_state != 0);
+          if (tape_handoff) handoff(k, env, time, xws, 0, episode, T(0));
+        } else {
+          deferred = true;
+        }
       }
       HS_FLUSH();
       break;
@@ -2471,6 +2543,17 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
     tot_iter += st.niter;
 #endif
     if (st.dbg && active && !in_reset) dump_debug(st, st.dbg);
+  }
+  if (tape_handoff) {   // the pair's next env step may start: rows in memory, then the flag
+    KPtr<T> k = opaque(ka);
+    const bool any_deferred = __ballot(deferred) != 0;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) {
+      if (any_deferred)   // an env overflowed the resident tier: stop the whole tape launch
+        __hip_atomic_store(k->b.qsync + QS_ABORT, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        __hip_atomic_store(k->b.qsync + QS_FLAG + pair, set_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -2508,11 +2591,10 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !PGS) ? 2 : 1) void step_ker
 template <typename T, int NV, bool PGS>
 __global__ __launch_bounds__(64, 1) void step_kernel_queue(KArgs<T> /* read via kernarg ptr */) {
   const KPtr<T> ka = (KPtr<T>)__builtin_amdgcn_kernarg_segment_ptr();
-  // this launch's hand-off tag: the epoch only changes after every wave of the launch has left the
-  // claim loop (last wave out, below)
+  // this launch's epoch (its hand-off tags are qtag(epoch, ...)): the epoch only changes after every
+  // wave of the launch has left the claim loop (last wave out, below)
   const uint32_t epoch = __builtin_amdgcn_readfirstlane(
       __hip_atomic_load(ka->b.qsync + QS_EPOCH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  const int tag = (int)(epoch & 0x3fffffff) + 1;
   __shared__ Scratch<T, Resident<T>> smem[2];
   PgsCache<T, Resident<T>>* pcache = nullptr;
   if constexpr (PGS) {
@@ -2535,14 +2617,23 @@ __global__ __launch_bounds__(64, 1) void step_kernel_queue(KArgs<T> /* read via 
   }
   for (;;) {
     const KPtr<T> k = opaque(ka);       // nothing uniform kept live across items
-    const int nsub = k->p.nsub, npairs = (k->nenv + 1) / 2;
+    const int nsub = k->p.nsub, npairs = (k->nenv + 1) / 2, K = k->p.nsteps;
     int* qs = k->b.qsync;
     int i = 0;
     if (threadIdx.x == 0) i = atomicAdd(&qs[QS_HEAD], 1);
     i = __builtin_amdgcn_readfirstlane(i);
-    if (i >= 2 * npairs) break;
-    const bool last = i >= npairs;
-    const int ii = last ? i - npairs : i;
+    // tape launch: K whole env steps per pair, step-major (step t of every pair, then step t + 1);
+    // one env step: every pair's first chunk, then every pair's last substep
+    const bool tape = K > 1;
+    if (i >= (tape ? K * npairs : 2 * npairs)) break;
+    if (tape) {   // an aborted tape launch only drains its claims
+      int ab = 0;
+      if (threadIdx.x == 0) ab = __hip_atomic_load(qs + QS_ABORT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__builtin_amdgcn_readfirstlane(ab) != 0) continue;
+    }
+    const int t = tape ? i / npairs : 0;
+    const bool last = !tape && i >= npairs;
+    const int ii = tape ? i - t * npairs : (last ? i - npairs : i);
     int pair;
     if (qpre[QNB] == npairs) {   // bucket b holds claims [qpre[b], qpre[b + 1])
       const int lane = opaque_v(threadIdx.x);
@@ -2555,18 +2646,26 @@ __global__ __launch_bounds__(64, 1) void step_kernel_queue(KArgs<T> /* read via 
       pair = (int)((uint64_t)ii * (uint32_t)k->p.qmul % (uint32_t)npairs);
     }
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    step_pair<T, NV, PGS, Resident<T>>(k, smem, pcache, 2 * pair + (opaque_v(threadIdx.x) >= HL ? 1 : 0), k->nenv,
-                                       nullptr, last ? nsub - 1 : 0, last ? nsub : nsub - 1, pair, false, tag);
+    const int env = 2 * pair + (opaque_v(threadIdx.x) >= HL ? 1 : 0);
+    // ONE step_pair call site (the whole pipeline is inlined): a tape item is env step t, waiting for
+    // the pair's step t - 1 and handing over to its step t + 1; otherwise the first chunk hands over
+    // to the last substep
+    const int s0 = last ? nsub - 1 : 0, s1 = (tape || last) ? nsub : nsub - 1;
+    const int wait_tag = tape ? (t > 0 ? qtag(epoch, t - 1, 1) : 0) : (last ? qtag(epoch, 0, 0) : 0);
+    const int set_tag = tape ? (t < K - 1 ? qtag(epoch, t, 1) : 0) : (last ? 0 : qtag(epoch, 0, 0));
+    step_pair<T, NV, PGS, Resident<T>>(k, smem, pcache, env, k->nenv, nullptr, s0, s1, pair, false, wait_tag, set_tag,
+                                       t);
     // the pair's duration for the next launch's order: the first chunk's is kept in qcost (its
     // store trails the hand-off, but the last substep reads it ~100 us later; a stale value only
-    // makes the order less exact, never the results different)
+    // makes the order less exact, never the results different); a tape launch times the pair's
+    // last env step
     const uint32_t d = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t0);
     if (threadIdx.x == 0) {
       qs = opaque(ka)->b.qsync;
-      if (!last) {
+      if (!last && !tape) {
         qs[qs_cost(npairs) + pair] = (int)d;
-      } else {
-        const uint32_t tot = d + (uint32_t)qs[qs_cost(npairs) + pair];
+      } else if (!tape || t == K - 1) {
+        const uint32_t tot = tape ? d : d + (uint32_t)qs[qs_cost(npairs) + pair];
         const int b = QNB - 1 - (int)min(tot / (uint32_t)QBIN, (uint32_t)(QNB - 1));
         const int slot = atomicAdd(&qs[qs_cnt(npairs, (epoch + 1) & 1) + b], 1);
         qs[qs_ord(npairs, (epoch + 1) & 1) + (size_t)b * npairs + slot] = pair;
@@ -2666,10 +2765,12 @@ int resident_waves(bool pgs) {
 template <typename T>
 hipError_t launch_step(const DevModel<T>* dmodel, int nv, const EnvBuffers<T>& b, const float* actions,
                        const uint8_t* reset_mask, const T* noise_qpos, const T* noise_qvel,
-                       const StepParams& p, int nenv, hipStream_t stream) {
+                       const StepParams& p, int nenv, hipStream_t stream, const TapeOut<T>* tape) {
   if (nenv <= 0) return hipSuccess;
   if (nv != 27) return hipErrorInvalidValue;
-  KArgs<T> args{(MPtr<T>)dmodel, b, actions, reset_mask, noise_qpos, noise_qvel, p, nenv};
+  KArgs<T> args{(MPtr<T>)dmodel, b, actions, reset_mask, noise_qpos, noise_qvel, p, nenv,
+                tape ? *tape : TapeOut<T>{nullptr, nullptr, nullptr, nullptr}};
+  if (args.p.nsteps < 1) args.p.nsteps = 1;
   // chunk-queue schedule when the env pairs outnumber the waves the GPU holds at once (the fp64
   // engine: 1 wave per SIMD), for multi-substep calls (HS_SCHED_DIRECT: never)
   const int npairs = (nenv + 1) / 2;
@@ -2677,6 +2778,16 @@ hipError_t launch_step(const DevModel<T>* dmodel, int nv, const EnvBuffers<T>& b
   const bool may_queue = p.schedule == SCHED_AUTO || p.schedule == SCHED_FIXED_ORDER;
   args.p.queue = (may_queue && b.mid && b.qsync && p.mode != MODE_RESET && p.nsub >= 2 && resident > 0 &&
                   npairs > resident) ? 1 : 0;
+  // tape launch (several env steps of an action tape): always the chunk queue, with whole env steps
+  // as items, whatever the batch size -- a pair's next env step starts as soon as its own previous
+  // one is committed, so the steps of different pairs overlap instead of each step ending on its
+  // slowest pair
+  const bool tape_launch = args.p.nsteps > 1;
+  if (tape_launch) {
+    if (p.mode != MODE_ENV_STEP || !b.mid || !b.qsync || resident <= 0 || args.p.nsteps > QTAG_STEPS)
+      return hipErrorInvalidValue;
+    args.p.queue = 1;
+  }
   args.p.qorder = p.schedule == SCHED_AUTO ? 1 : 0;
   // fallback claim order (first queued launch, SCHED_FIXED_ORDER): a fixed multiplicative
   // permutation of the pairs (the same for both chunk kinds, so a pair's last substep is still
@@ -2695,7 +2806,8 @@ hipError_t launch_step(const DevModel<T>* dmodel, int nv, const EnvBuffers<T>& b
   // otherwise leave SIMDs idle with one wave per env pair
   args.p.single = (!args.p.queue && (p.schedule == SCHED_SINGLE ||
                                      (p.schedule == 0 && resident > 0 && nenv <= resident))) ? 1 : 0;
-  const dim3 grid(args.p.queue ? resident : (args.p.single ? nenv : npairs)), block(WAVE);
+  const dim3 grid(args.p.queue ? (tape_launch ? std::min(resident, npairs) : resident) : (args.p.single ? nenv : npairs)),
+      block(WAVE);
   // the wide tier's grid: enough waves for a few deferred envs at once, few enough that the
   // common no-overflow launch (every wave reads the count and exits) costs a few microseconds
   const dim3 wgrid(std::min((nenv + 1) / 2, 32));
@@ -2703,13 +2815,13 @@ hipError_t launch_step(const DevModel<T>* dmodel, int nv, const EnvBuffers<T>& b
   if (p.solver == SOLVER_PGS) {
     if (args.p.queue) hipLaunchKernelGGL((step_kernel_queue<T, 27, true>), grid, block, 0, stream, args);
     else hipLaunchKernelGGL((step_kernel<T, 27, true>), grid, block, 0, stream, args);
-    if (b.redo) hipLaunchKernelGGL((step_kernel_wide<T, 27, true>), wgrid, block, 0, stream, args);
+    if (b.redo && !tape_launch) hipLaunchKernelGGL((step_kernel_wide<T, 27, true>), wgrid, block, 0, stream, args);
     return hipGetLastError();
   }
 #endif
   if (args.p.queue) hipLaunchKernelGGL((step_kernel_queue<T, 27, false>), grid, block, 0, stream, args);
   else hipLaunchKernelGGL((step_kernel<T, 27, false>), grid, block, 0, stream, args);
-  if (b.redo) hipLaunchKernelGGL((step_kernel_wide<T, 27, false>), wgrid, block, 0, stream, args);
+  if (b.redo && !tape_launch) hipLaunchKernelGGL((step_kernel_wide<T, 27, false>), wgrid, block, 0, stream, args);
   return hipGetLastError();
 }
 
@@ -2724,14 +2836,14 @@ hipError_t launch_kinematics(const DevModel<T>* dmodel, int nv, const T* qpos, T
 #ifndef HS_ONLY_F64
 template hipError_t launch_step<float>(const DevModel<float>*, int, const EnvBuffers<float>&, const float*,
                                        const uint8_t*, const float*, const float*, const StepParams&, int,
-                                       hipStream_t);
+                                       hipStream_t, const TapeOut<float>*);
 template int resident_waves<float>(bool);
 template hipError_t launch_kinematics<float>(const DevModel<float>*, int, const float*, float*, hipStream_t);
 #endif
 #if !defined(HS_DEV_F32_ONLY) && !defined(HS_ONLY_F32)
 template hipError_t launch_step<double>(const DevModel<double>*, int, const EnvBuffers<double>&, const float*,
                                         const uint8_t*, const double*, const double*, const StepParams&, int,
-                                        hipStream_t);
+                                        hipStream_t, const TapeOut<double>*);
 #endif
 
 #if !defined(HS_DEV_F32_ONLY) && !defined(HS_ONLY_F32)

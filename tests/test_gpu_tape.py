@@ -1,0 +1,130 @@
+"""Tape launches (hs_step_tape / HsBatch.step_tape): K consecutive env steps over a given action
+tape in ONE launch of the chunk-queue kernel, whole env steps as items, each env pair's step t + 1
+waiting only for its own step t (hs_kernels.hip step_kernel_queue).
+
+The contract is bitwise equality with K ``step`` calls (custom_env.py:152-230 per step): states,
+every step's obs / reward / terminated / truncated, auto-resets inside the tape with their
+terminal obs and final-step info, warnings -- on the fp64 engine at configs[1] size (4096 envs,
+more pairs than resident waves) and at a small odd count, on the fp32 engine, with full-state obs,
+and through the overflow path (an env over the resident contact tier stops the launch and the tape
+is replayed step by step, where the wide tier re-runs it).
+"""
+import numpy as np
+import pytest
+
+from conftest import XML
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def model():
+    from mujocoposelearning_amd.model import HsModel
+    return HsModel(XML)
+
+
+def _run(model, n, prec, acts, t0, tape, full_state=False, reward_id=0, lying=None, outputs=True, pre_step=True):
+    import torch
+    from mujocoposelearning_amd.batch import HsBatch
+    b = HsBatch(model, n, precision=prec, seed=3, full_state=full_state)
+    b.configure(frame_skip=3, duration=10.0, reward_id=reward_id, autoreset=1, max_steps=750)
+    b.reset()
+    b.set_state(time=t0)
+    if lying is not None:
+        idx, q = lying
+        st = b.get_state()
+        st["qpos"][idx] = q
+        st["qvel"][idx] = 0.0
+        st["qacc_warmstart"][idx] = 0.0
+        b.set_state(**st)
+    if pre_step:
+        b.step(acts[0])                 # one ordinary step first (the queue's cost order is then set)
+    K = acts.shape[0] - 2
+    if tape:
+        res = b.step_tape(acts[1:1 + K], outputs=outputs)
+        if outputs:
+            per = [x.clone() for x in res]
+        else:
+            per = None
+    else:
+        o, r, te, tr = [], [], [], []
+        for k in range(K):
+            b.step(acts[1 + k])
+            o.append(b.obs.clone()); r.append(b.reward.clone()); te.append(b.terminated.clone())
+            tr.append(b.truncated.clone())
+        per = [torch.stack(o), torch.stack(r), torch.stack(te), torch.stack(tr)]
+    fin = [b.qpos.clone(), b.qvel.clone(), b.qacc_warmstart.clone(), b.time.clone(), b.warning.clone(),
+           b.step_count.clone(), b.episode.clone(), b.total_reward.clone(), b.obs.clone(), b.reward.clone(),
+           b.terminated.clone(), b.truncated.clone(), b.terminal_obs.clone(), b.terminal_step_count.clone(),
+           b.terminal_total_reward.clone()]
+    if full_state:
+        fin += [b.cfrc_ext.clone(), b.subtree_linvel.clone()]
+    b.step(acts[-1])                    # an ordinary step after the tape: flags / epoch / order stay sound
+    after = [b.qpos.clone(), b.obs.clone(), b.reward.clone()]
+    info = dict(aborts=b.tape_aborts(), reruns=b.wide_reruns(), queued=b.queued())
+    b.close()
+    return per, fin, after, info
+
+
+def _same(name, xs, ys):
+    import torch
+    for k, (x, y) in enumerate(zip(xs, ys)):
+        if not torch.equal(x, y):
+            d = (x.double() - y.double()).abs()
+            raise AssertionError(f"{name}[{k}]: max |diff| {float(d.max()):.3e}, "
+                                 f"{int((d.reshape(d.shape[0], -1).amax(1) > 0).sum())} rows differ")
+
+
+CASES = [("fp64", 4096, False, 0), ("fp64", 777, False, 0), ("fp32", 4096, False, 0), ("fp64", 1024, True, 1)]
+
+
+@pytest.mark.parametrize("prec,n,full,reward", CASES, ids=[f"{p}-{n}{'-full' if f else ''}" for p, n, f, _ in CASES])
+def test_step_tape_bitwise_equals_step_loop(model, prec, n, full, reward):
+    import torch
+    K = 40
+    g = torch.Generator(device="cuda").manual_seed(21)
+    acts = torch.rand(K + 2, n, 21, device="cuda", generator=g) * 2 - 1
+    t0 = np.floor(np.arange(n) * 667 / n) * 0.015 + 0.005      # staggered clocks: resets inside the tape
+    per_a, fin_a, aft_a, info_a = _run(model, n, prec, acts, t0, True, full, reward)
+    per_b, fin_b, aft_b, info_b = _run(model, n, prec, acts, t0, False, full, reward)
+    assert info_a["aborts"] == 0 and info_a["reruns"] == info_b["reruns"]
+    assert int(torch.stack([x for x in per_b[2]]).sum()) > 0     # episodes ended inside the tape
+    _same("per-step", per_a, per_b)
+    _same("final", fin_a, fin_b)
+    _same("after", aft_a, aft_b)
+
+
+def test_step_tape_without_outputs_matches(model):
+    import torch
+    n, K = 4096, 12
+    g = torch.Generator(device="cuda").manual_seed(4)
+    acts = torch.rand(K + 2, n, 21, device="cuda", generator=g) * 2 - 1
+    t0 = np.floor(np.arange(n) * 667 / n) * 0.015 + 0.005
+    _, fin_a, aft_a, _ = _run(model, n, "fp64", acts, t0, True, outputs=False)
+    _, fin_b, aft_b, _ = _run(model, n, "fp64", acts, t0, False)
+    _same("final", fin_a, fin_b)
+    _same("after", aft_a, aft_b)
+
+
+def test_step_tape_overflow_replays_step_by_step(model):
+    """16 envs lying pressed into the floor (over the resident tier's contacts / rows): the tape
+    launch stops at the first overflow, the tape is replayed step by step from the saved state (the
+    wide tier re-runs the overflowing steps), and the results are bitwise the step loop's."""
+    import torch
+    from oracle.oracle import Oracle
+    from test_gpu_contacts import lying_states
+    n, K = 4096, 6
+    o = Oracle(XML)
+    q = np.stack(lying_states(o, 16, seed=11))
+    idx = np.arange(16) * 255 + 7
+    g = torch.Generator(device="cuda").manual_seed(9)
+    acts = torch.rand(K + 2, n, 21, device="cuda", generator=g) * 2 - 1
+    t0 = np.zeros(n) + 0.005
+    # lying when the tape starts: its first step overflows
+    per_a, fin_a, aft_a, info_a = _run(model, n, "fp64", acts, t0, True, lying=(idx, q), pre_step=False)
+    per_b, fin_b, aft_b, info_b = _run(model, n, "fp64", acts, t0, False, lying=(idx, q), pre_step=False)
+    assert info_a["aborts"] == 1, info_a
+    assert info_a["reruns"] == info_b["reruns"] >= len(idx), (info_a, info_b)
+    _same("per-step", per_a, per_b)
+    _same("final", fin_a, fin_b)
+    _same("after", aft_a, aft_b)
