@@ -438,6 +438,38 @@ def main():
                        note="policy MLP[256,256] (pi+vf, packed GEMM chain, fp32) forward + hs_ppo_act "
                             "(diag-Gaussian sample, log-prob, clip) + env step")
         e.close()
+        # PPO.collect_rollouts end to end (32 steps: sample, env step, buffers, values, GAE), the fused
+        # rollout (hs_rollout: the pi net inside the env kernel, one launch per rollout) against the
+        # per-step path (policy GEMMs + hs_ppo_act + env launch + hs_ppo_post per step, one HIP graph)
+        from mujocoposelearning_amd import ppo as ppo_mod
+        collect = {}
+        for fused in (True, False):
+            ppo_mod.FUSED_ROLLOUT = fused
+            e = make_env(args.precision, 6000)
+            p = ppo_mod.PPO(e, n_steps=32, batch_size=32768, n_epochs=1, seed=0,
+                            policy_kwargs={"net_arch": {"pi": [256, 256], "vf": [256, 256]}, "activation_fn": "ReLU"})
+            kk = np.floor(np.arange(n) * EPISODE / n)              # staggered episode clocks (the window's mix)
+            e.batch.t["time"].copy_(torch.as_tensor(kk * FRAME_SKIP * TIMESTEP + TIMESTEP, dtype=e.batch.dtype,
+                                                    device=dev))
+            e.batch.t["step_count"].copy_(torch.as_tensor(kk, dtype=torch.int32, device=dev))
+            for _ in range(2):
+                p.collect_rollouts()
+            barrier()
+            tc0 = time.perf_counter()
+            R = 4
+            for _ in range(R):
+                p.collect_rollouts()
+            barrier()
+            collect["fused" if fused else "per_step"] = dict(
+                value=n * 32 * R * ranks / max_over_ranks(time.perf_counter() - tc0), unit="env_steps/s",
+                used_fused=p._fused_rollout_args() is not None, fallbacks=getattr(p, "fused_fallbacks", 0))
+            e.close()
+        ppo_mod.FUSED_ROLLOUT = True
+        rollout["collect_rollouts"] = dict(
+            **collect, n_steps=32, note="PPO.collect_rollouts (sampling, env steps, rollout buffers, values, GAE) "
+                                        "from staggered episode clocks; fused = hs_rollout (policy forward in the "
+                                        "env kernel, one launch per rollout), per_step = one HIP graph of per-step "
+                                        "launches")
 
     # ---- extra sim-only leg: free-running stream groups (opt-in)
     grouped = None

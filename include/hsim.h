@@ -16,6 +16,7 @@
  *   hs_step              <- HumanoidEnv.step: frame_skip x mj_step, _get_state, reward, done
  *                           custom_env.py:152-230 (+ SB3 auto-reset on done)
  *   hs_step_tape         <- K x HumanoidEnv.step over a given action tape (open loop), one launch
+ *   hs_rollout           <- SB3 PPO.collect_rollouts' per-step loop (policy + env step + buffers), one launch
  *   hs_physics_step      <- raw `data.ctrl[:] = a; mujoco.mj_step(model, data)` custom_env.py:159-160
  *   hs_debug_lose_handoff   (test hook: mj_step's warning + mj_resetData path, custom_env.py:160)
  *   hs_state_io          <- reads/writes of data.qpos/qvel/qacc_warmstart/time/ctrl (custom_env.py:105-117)
@@ -188,6 +189,53 @@ typedef struct hs_tape_out {
 int hs_step_tape(hs_batch* b, const float* actions, int n_steps, const hs_tape_out* out, void* stream);
 /* tape launches of this batch that were replayed step by step (resident-tier overflow) */
 int hs_tape_aborts(const hs_batch* b, uint64_t* n);
+
+/* Fused PPO rollout (the fp64 Newton engine).  The SB3 MlpPolicy's pi net -- two hidden layers of
+ * 256, ReLU, then the action head, fp32 -- with [in][out] row-major weights (w1 [obs_dim][ld1],
+ * columns 0..255 the pi net's, w2 [256][256], w3 [256][act_dim]) and the DiagGaussian log_std. */
+typedef struct hs_policy {
+  const float *w1, *b1, *w2, *b2, *w3, *b3, *log_std;
+  int ld1, obs_dim, act_dim;
+} hs_policy;
+/* The RolloutBuffer of SB3 PPO.collect_rollouts (on_policy_algorithm.py, 2.3.2) for t_total steps of
+ * N envs, device arrays: obs [t_total][N][obs_dim] (row 0 = the rollout's first obs), obs_last
+ * [N][obs_dim] (the obs after the last step), actions [t_total][N][act_dim] (unclipped samples),
+ * log_probs / episode_starts / rewards [t_total][N] f32, dones / boot [t_total][N] u8 (boot:
+ * TimeLimit.truncated and not terminated), episode_returns [t_total][N] f64, terminal_obs
+ * [t_total][N][obs_dim] (rows of the boot envs), ep_acc [N] f64 (running return, in / out),
+ * episode_start [N] f32 (out), actions_clipped [N][act_dim] (in: step t_begin's clipped action;
+ * out: step t_begin + n_steps'), counter_base (device u64) and seed: the noise of hs_ppo_act. */
+typedef struct hs_rollout_bufs {
+  float* obs;
+  float* obs_last;
+  float* actions;
+  float* log_probs;
+  float* episode_starts;
+  float* rewards;
+  uint8_t* dones;
+  double* episode_returns;
+  uint8_t* boot;
+  float* terminal_obs;
+  double* ep_acc;
+  float* episode_start;
+  float* actions_clipped;
+  const uint64_t* counter_base;
+  uint64_t seed;
+  int deterministic;
+} hs_rollout_bufs;
+/* Steps [t_begin, t_begin + n_steps) of a PPO rollout in ONE launch: hs_step with the given clipped
+ * action for step t_begin, then for every later step the policy forward on the returned obs, the
+ * Gaussian sample (hs_ppo_act's Philox stream, counter step + *counter_base), the clip, and
+ * hs_ppo_post's bookkeeping (rewards, dones, episode returns, bootstrap flags / terminal obs, the
+ * next obs row, episode_start) -- on each env's wave, each env pair's step t + 1 starting when its
+ * own step t is done.  Replaces the per-step loop of SB3 collect_rollouts (train_sb3.py:229 ->
+ * on_policy_algorithm.py) for envs stepped by this engine; values are evaluated after the rollout.
+ * n_steps <= hs_rollout_max_steps(b) (the shortest episode).  Returns 0, or 1 when an env overflowed
+ * the resident contact tier: the env state, ep_acc, episode_start and actions_clipped are restored
+ * to the call's start, and the caller collects these steps step by step (hs_step).  Synchronizes. */
+int hs_rollout(hs_batch* b, const hs_policy* pol, const hs_rollout_bufs* rb, int t_begin, int n_steps, int t_total,
+               void* stream);
+int hs_rollout_max_steps(const hs_batch* b);
 /* Auto-reset noise source of hs_step: [N][nq] / [N][nv] device arrays of the batch precision with
  * the raw U(-noise_scale, noise_scale) draws of the NEXT reset of each env (the kernel applies the
  * x0.1 height factor and zeroes the quaternion part, custom_env.py:109-114); NULL, NULL = the

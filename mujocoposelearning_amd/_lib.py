@@ -40,6 +40,18 @@ class hs_tape_out(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ("obs", "reward", "terminated", "truncated")]
 
 
+class hs_policy(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("w1", "b1", "w2", "b2", "w3", "b3", "log_std")] + \
+               [("ld1", C.c_int), ("obs_dim", C.c_int), ("act_dim", C.c_int)]
+
+
+class hs_rollout_bufs(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("obs", "obs_last", "actions", "log_probs", "episode_starts", "rewards",
+                                          "dones", "episode_returns", "boot", "terminal_obs", "ep_acc",
+                                          "episode_start", "actions_clipped", "counter_base")] + \
+               [("seed", C.c_uint64), ("deterministic", C.c_int)]
+
+
 class hs_batch_info(C.Structure):
     _fields_ = [(n, C.c_int) for n in ("n_envs", "precision", "nq", "nv", "nu", "nbody", "obs_dim", "elem_size",
                                        "resident_con", "resident_efc", "wide_con", "wide_efc", "resident_waves",
@@ -80,6 +92,8 @@ def lib():
         "hs_step": (i, [vp, vp, vp]),
         "hs_step_tape": (i, [vp, vp, i, vp, vp]),
         "hs_tape_aborts": (i, [vp, vp]),
+        "hs_rollout": (i, [vp, vp, vp, i, i, i, vp]),
+        "hs_rollout_max_steps": (i, [vp]),
         "hs_set_autoreset_noise": (i, [vp, vp, vp]),
         "hs_physics_step": (i, [vp, vp, i, vp]),
         "hs_state_io": (i, [vp, i, vp, vp, vp, vp, vp]),
@@ -118,7 +132,7 @@ def lib():
 
 
 EXPORTED = ("hs_model_load", "hs_model_free", "hs_model_field", "hs_batch_create", "hs_batch_destroy",
-            "hs_batch_get_info", "hs_get_buffers", "hs_set_config", "hs_set_seed", "hs_get_config", "hs_reset", "hs_step", "hs_step_tape", "hs_tape_aborts", "hs_set_autoreset_noise",
+            "hs_batch_get_info", "hs_get_buffers", "hs_set_config", "hs_set_seed", "hs_get_config", "hs_reset", "hs_step", "hs_step_tape", "hs_tape_aborts", "hs_rollout", "hs_rollout_max_steps", "hs_set_autoreset_noise",
             "hs_physics_step", "hs_state_io", "hs_kinematics", "hs_set_debug", "hs_debug_lose_handoff", "hs_get_debug", "hs_synchronize", "hs_batch_counters", "hs_gae",
             "hs_ppo_act", "hs_ppo_post", "hs_gauss_logp", "hs_gauss_logp_grad",
             "hs_ppo_loss_workspace", "hs_ppo_loss", "hs_ppo_loss_grad", "hs_adam_workspace", "hs_adam_clip",

@@ -36,7 +36,8 @@ struct hs_batch {
   hs_env_config cfg{};
   bool ctrl_stale = false;                   // env steps ran with HS_OUT_CTRL off: buf.ctrl is not data.ctrl
   int lose_pair1 = 0;                        // hs_debug_lose_handoff test hook (pair + 1; 0 = off)
-  void* tape_backup = nullptr;               // hs_step_tape: the state before a tape launch (replay on abort)
+  void* tape_backup = nullptr;               // hs_step_tape / hs_rollout: the state before a tape launch (replay on abort)
+  size_t tape_backup_bytes = 0;
   unsigned long long tape_aborts = 0;        // tape launches replayed step by step (resident-tier overflow)
 };
 
@@ -159,7 +160,7 @@ hs::StepParams params_of(const hs_batch* b, int mode, int nsub) {
 }
 
 int launch(hs_batch* b, int mode, const float* act, const uint8_t* mask, const void* nq, const void* nvz, int nsub,
-           void* stream, int nsteps = 1, const hs_tape_out* tape = nullptr) {
+           void* stream, int nsteps = 1, const hs_tape_out* tape = nullptr, const hs::RolloutArgs* ro = nullptr) {
   if (!b) return fail("null batch");
   DeviceGuard g(b->device);
   hipError_t e;
@@ -170,7 +171,7 @@ int launch(hs_batch* b, int mode, const float* act, const uint8_t* mask, const v
     hs::TapeOut<double> to{tape ? (double*)tape->obs : nullptr, tape ? (double*)tape->reward : nullptr,
                            tape ? tape->terminated : nullptr, tape ? tape->truncated : nullptr};
     e = hs::launch_step<double>((const hs::DevModel<double>*)b->dmodel, nv, env_buffers<double>(b), act, mask,
-                                (const double*)nq, (const double*)nvz, p, b->n, (hipStream_t)stream, &to);
+                                (const double*)nq, (const double*)nvz, p, b->n, (hipStream_t)stream, &to, ro);
   } else {
     hs::TapeOut<float> to{tape ? (float*)tape->obs : nullptr, tape ? (float*)tape->reward : nullptr,
                           tape ? tape->terminated : nullptr, tape ? tape->truncated : nullptr};
@@ -179,6 +180,69 @@ int launch(hs_batch* b, int mode, const float* act, const uint8_t* mask, const v
   }
   if (e == hipErrorInvalidValue) return fail("no kernel instance for this model's nv (compiled: nv = 27)");
   return hip_ok(e, "step kernel launch") ? 0 : -1;
+}
+
+// -- tape launches (hs_step_tape, hs_rollout) --------------------------------------------------
+// Each env finishes at most one episode per tape launch (its terminal obs / info rows are then written
+// once, see hs_kernels.hip step_pair): launches of at most the shortest episode's length.  An episode
+// starts at time = one timestep (the reset's mj_step) and ends at time >= duration (custom_env.py:213)
+// or at max_steps.
+int min_episode_len(const hs_batch* b) {
+  const auto& h = b->model->host;
+  const double dt = h.timestep * b->cfg.frame_skip;
+  const double spans = std::floor((b->cfg.duration - h.timestep) / dt - 1e-9);
+  return (int)std::max(1.0, std::min((double)b->cfg.max_steps, spans));
+}
+
+struct Region { void* p; size_t bytes; };
+
+// the env state a tape launch changes (restored when it aborts on a resident-tier overflow)
+std::vector<Region> state_regions(const hs_batch* b) {
+  const auto& h = b->model->host;
+  const size_t N = (size_t)b->n, es = b->precision == HS_FP64 ? 8 : 4;
+  return {{b->buf.qpos, N * h.nq * es}, {b->buf.qvel, N * h.nv * es}, {b->buf.qacc_warmstart, N * h.nv * es},
+          {b->buf.ctrl, N * h.nu * es}, {b->buf.time, N * es}, {b->buf.total_reward, N * es},
+          {b->buf.step_count, N * 4}, {b->buf.episode, N * 4}, {b->buf.warning, N * HS_NWARN * 4},
+          {b->redo_total, sizeof(unsigned long long)}};
+}
+
+// Back up `regs`, run `go` (the tape launch), and read the abort word: 0 = done, 1 = aborted (the
+// regions are restored and the redo list cleared), -1 = error.  Synchronizes the stream.
+template <typename F>
+int guarded_tape(hs_batch* b, const std::vector<Region>& regs, hipStream_t st, F&& go) {
+  size_t total = 0;
+  for (auto& r : regs) total += (r.bytes + 255) & ~(size_t)255;
+  if (total > b->tape_backup_bytes) {
+    if (b->tape_backup) (void)hipFree(b->tape_backup);
+    b->tape_backup = nullptr;
+    b->tape_backup_bytes = 0;
+    if (!hip_ok(hipMalloc(&b->tape_backup, total), "hipMalloc(tape backup)")) return -1;
+    b->tape_backup_bytes = total;
+  }
+  size_t off = 0;
+  for (auto& r : regs) {
+    if (!hip_ok(hipMemcpyAsync((char*)b->tape_backup + off, r.p, r.bytes, hipMemcpyDeviceToDevice, st), "tape backup"))
+      return -1;
+    off += (r.bytes + 255) & ~(size_t)255;
+  }
+  if (!hip_ok(hipMemsetAsync(b->qsync + hs::QS_ABORT, 0, sizeof(int), st), "tape abort word")) return -1;
+  int rc = go();
+  if (rc) return rc < 0 ? rc : -1;
+  int aborted = 0;
+  if (!hip_ok(hipMemcpyAsync(&aborted, b->qsync + hs::QS_ABORT, sizeof(int), hipMemcpyDeviceToHost, st),
+              "tape abort word") ||
+      !hip_ok(hipStreamSynchronize(st), "tape launch"))
+    return -1;
+  if (!aborted) return 0;
+  off = 0;
+  for (auto& r : regs) {
+    if (!hip_ok(hipMemcpyAsync(r.p, (char*)b->tape_backup + off, r.bytes, hipMemcpyDeviceToDevice, st), "tape restore"))
+      return -1;
+    off += (r.bytes + 255) & ~(size_t)255;
+  }
+  if (!hip_ok(hipMemsetAsync(b->redo, 0, 2 * sizeof(int), st), "tape redo list")) return -1;
+  b->tape_aborts++;
+  return 1;
 }
 
 template <typename T>
@@ -521,12 +585,7 @@ int hs_step_tape(hs_batch* b, const float* actions, int n_steps, const hs_tape_o
   // without auto-reset a finished env keeps rewriting its terminal info every step (one launch
   // must write each batch address once, see hs_kernels.hip step_pair): step by step
   if (n_steps == 1 || !tape_sched || !b->cfg.autoreset || resident <= 0 || !b->mid || !b->qsync) return per_step();
-  // each env finishes at most one episode per launch (its terminal obs / info rows are then written
-  // once): launches of at most the shortest episode's length -- an episode starts at time = one
-  // timestep (the reset's mj_step) and ends at time >= duration (custom_env.py:213) or at max_steps
-  const double dt = h.timestep * b->cfg.frame_skip;
-  const double spans = std::floor((b->cfg.duration - h.timestep) / dt - 1e-9);
-  const int min_len = (int)std::max(1.0, std::min((double)b->cfg.max_steps, spans));
+  const int min_len = min_episode_len(b);
   if (n_steps > min_len) {
     for (int t0 = 0; t0 < n_steps; t0 += min_len) {
       const int k = std::min(min_len, n_steps - t0);
@@ -542,43 +601,15 @@ int hs_step_tape(hs_batch* b, const float* actions, int n_steps, const hs_tape_o
     }
     return 0;
   }
-  // state before the launch: an env that overflows the resident tier stops the tape launch
-  // (QS_ABORT), and the tape is then replayed step by step from here (the wide tier re-runs the
-  // overflowing steps) -- the same results, bitwise, as n_steps hs_step calls either way
-  struct Region { void* p; size_t bytes; } regs[] = {
-      {b->buf.qpos, N * h.nq * es}, {b->buf.qvel, N * h.nv * es}, {b->buf.qacc_warmstart, N * h.nv * es},
-      {b->buf.ctrl, N * nu * es}, {b->buf.time, N * es}, {b->buf.total_reward, N * es},
-      {b->buf.step_count, N * 4}, {b->buf.episode, N * 4}, {b->buf.warning, N * HS_NWARN * 4},
-      {b->redo_total, sizeof(unsigned long long)}};
-  size_t total = 0;
-  for (auto& r : regs) total += (r.bytes + 255) & ~(size_t)255;
-  if (!b->tape_backup && !hip_ok(hipMalloc(&b->tape_backup, total), "hipMalloc(tape backup)")) return -1;
-  size_t off = 0;
-  for (auto& r : regs) {
-    if (!hip_ok(hipMemcpyAsync((char*)b->tape_backup + off, r.p, r.bytes, hipMemcpyDeviceToDevice, st), "tape backup"))
-      return -1;
-    off += (r.bytes + 255) & ~(size_t)255;
-  }
-  if (!hip_ok(hipMemsetAsync(b->qsync + hs::QS_ABORT, 0, sizeof(int), st), "tape abort word")) return -1;
-  int rc = launch(b, hs::MODE_ENV_STEP, actions, nullptr, b->ar_qpos_noise, b->ar_qvel_noise, b->cfg.frame_skip,
+  // an env that overflows the resident tier stops the tape launch (QS_ABORT), and the tape is then
+  // replayed step by step from the saved state (the wide tier re-runs the overflowing steps) -- the
+  // same results, bitwise, as n_steps hs_step calls either way
+  int rc = guarded_tape(b, state_regions(b), st, [&] {
+    return launch(b, hs::MODE_ENV_STEP, actions, nullptr, b->ar_qpos_noise, b->ar_qvel_noise, b->cfg.frame_skip,
                   stream, n_steps, out);
-  if (rc) return rc;
-  int aborted = 0;
-  if (!hip_ok(hipMemcpyAsync(&aborted, b->qsync + hs::QS_ABORT, sizeof(int), hipMemcpyDeviceToHost, st),
-              "tape abort word") ||
-      !hip_ok(hipStreamSynchronize(st), "tape launch"))
-    return -1;
-  if (aborted) {
-    off = 0;
-    for (auto& r : regs) {
-      if (!hip_ok(hipMemcpyAsync(r.p, (char*)b->tape_backup + off, r.bytes, hipMemcpyDeviceToDevice, st), "tape restore"))
-        return -1;
-      off += (r.bytes + 255) & ~(size_t)255;
-    }
-    if (!hip_ok(hipMemsetAsync(b->redo, 0, 2 * sizeof(int), st), "tape redo list")) return -1;
-    b->tape_aborts++;
-    return per_step();
-  }
+  });
+  if (rc < 0) return rc;
+  if (rc == 1) return per_step();
   b->ctrl_stale = !(b->cfg.outputs & HS_OUT_CTRL);
   if (out) {   // the batch's own output buffers hold the last step, as after n_steps hs_step calls
     const size_t d = (size_t)b->obs_dim, t = (size_t)n_steps - 1;
@@ -593,6 +624,66 @@ int hs_step_tape(hs_batch* b, const float* actions, int n_steps, const hs_tape_o
       return -1;
   }
   return 0;
+}
+
+int hs_rollout_max_steps(const hs_batch* b) {
+  if (!b) return fail("null batch");
+  return min_episode_len(b);
+}
+
+int hs_rollout(hs_batch* b, const hs_policy* pol, const hs_rollout_bufs* rb, int t_begin, int n_steps, int t_total,
+               void* stream) {
+  if (!b || !pol || !rb) return fail("null argument");
+  const auto& h = b->model->host;
+  if (b->precision != HS_FP64 || h.solver == 1)
+    return fail("hs_rollout: the fused rollout runs on the fp64 Newton engine");
+  if (!b->cfg.autoreset || b->ar_qpos_noise || b->cfg.reward_id == HS_REWARD_NONE)
+    return fail("hs_rollout: needs auto-reset with the on-device reset noise and a device reward");
+  if (b->cfg.schedule != HS_SCHED_AUTO && b->cfg.schedule != HS_SCHED_FIXED_ORDER)
+    return fail("hs_rollout: needs the chunk-queue schedule (HS_SCHED_AUTO or HS_SCHED_FIXED_ORDER)");
+  if (pol->obs_dim != b->obs_dim || pol->act_dim != h.nu || pol->act_dim > 32 || pol->obs_dim % 4 ||
+      pol->obs_dim > 512 || pol->ld1 < 256 || pol->ld1 % 4)
+    return fail("hs_rollout: policy shape (obs_dim " + std::to_string(pol->obs_dim) + ", act_dim " +
+                std::to_string(pol->act_dim) + ", ld1 " + std::to_string(pol->ld1) +
+                ") does not fit the fused forward (obs_dim = the batch's, a multiple of 4 and <= 512; act_dim = nu "
+                "<= 32; hidden layers of 256)");
+  if (n_steps < 1 || t_begin < 0 || t_begin + n_steps > t_total || n_steps > min_episode_len(b) ||
+      n_steps > hs::QTAG_STEPS)
+    return fail("hs_rollout: steps [t_begin, t_begin + n_steps) must lie in [0, t_total) and n_steps in [1, " +
+                std::to_string(std::min(min_episode_len(b), hs::QTAG_STEPS)) + "] (hs_rollout_max_steps)");
+  for (const void* q : {(const void*)pol->w1, (const void*)pol->b1, (const void*)pol->w2, (const void*)pol->b2,
+                        (const void*)pol->w3, (const void*)pol->b3, (const void*)pol->log_std, (const void*)rb->obs,
+                        (const void*)rb->obs_last, (const void*)rb->actions, (const void*)rb->log_probs,
+                        (const void*)rb->episode_starts, (const void*)rb->rewards, (const void*)rb->dones,
+                        (const void*)rb->episode_returns, (const void*)rb->boot, (const void*)rb->terminal_obs,
+                        (const void*)rb->ep_acc, (const void*)rb->episode_start, (const void*)rb->actions_clipped,
+                        (const void*)rb->counter_base})
+    if (!q) return fail("hs_rollout: every policy weight and rollout buffer must be given");
+  DeviceGuard g(b->device);
+  const int resident = hs::resident_waves<double>(false);
+  if (resident <= 0 || !b->mid || !b->qsync) return fail("hs_rollout: no resident-wave count / queue buffers");
+  hs::RolloutArgs ro{};
+  ro.w1 = pol->w1; ro.b1 = pol->b1; ro.w2 = pol->w2; ro.b2 = pol->b2; ro.w3 = pol->w3; ro.b3 = pol->b3;
+  ro.log_std = pol->log_std;
+  ro.ld1 = pol->ld1; ro.D = pol->obs_dim; ro.A = pol->act_dim;
+  ro.t_begin = t_begin; ro.t_total = t_total;
+  ro.obs = rb->obs; ro.obs_last = rb->obs_last; ro.act = rb->actions; ro.logp = rb->log_probs;
+  ro.start = rb->episode_starts; ro.rew = rb->rewards; ro.done = rb->dones; ro.epret = rb->episode_returns;
+  ro.boot = rb->boot; ro.tobs = rb->terminal_obs; ro.ep_acc = rb->ep_acc; ro.episode_start = rb->episode_start;
+  ro.act_clip = rb->actions_clipped; ro.ctr_base = rb->counter_base;
+  ro.k0 = (uint32_t)rb->seed; ro.k1 = (uint32_t)(rb->seed >> 32); ro.deterministic = rb->deterministic;
+  const size_t N = (size_t)b->n;
+  std::vector<Region> regs = state_regions(b);
+  regs.push_back({rb->ep_acc, N * sizeof(double)});
+  regs.push_back({rb->episode_start, N * sizeof(float)});
+  regs.push_back({rb->actions_clipped, N * (size_t)pol->act_dim * sizeof(float)});
+  hipStream_t st = (hipStream_t)stream;
+  int rc = guarded_tape(b, regs, st, [&] {
+    return launch(b, hs::MODE_ENV_STEP, rb->actions_clipped, nullptr, nullptr, nullptr, b->cfg.frame_skip, stream,
+                  n_steps, nullptr, &ro);
+  });
+  if (rc == 0) b->ctrl_stale = !(b->cfg.outputs & HS_OUT_CTRL);
+  return rc;
 }
 
 int hs_debug_lose_handoff(hs_batch* b, int env) {

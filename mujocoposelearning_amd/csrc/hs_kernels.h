@@ -14,7 +14,9 @@ constexpr int DBGDIM = 32768;        // stage dump (env 0 only) for parity debug
 // env bookkeeping a tape launch carries from one env step to the next: step count, episode, return)
 constexpr int MID_Q = 0, MID_V = MAXQ, MID_WS = MAXQ + MAXDOF, MID_TIME = MAXQ + 2 * MAXDOF, MID_W = MID_TIME + 1;
 constexpr int MID_SC = MID_W + 4, MID_EP = MID_W + 5, MID_TOT = MID_W + 6;
-constexpr int MIDDIM = MID_W + 7;
+// a fused rollout (hs_rollout) also hands over the next step's clipped action and the episode return
+constexpr int MID_ACT = MID_W + 7, MID_EPACC = MID_ACT + 32;
+constexpr int MIDDIM = MID_EPACC + 1;
 // chunk-queue sync words (uncached device memory): claim counter, exit counter, launch epoch,
 // per-pair flags.  A pair's flag holds the tag of the launch whose first chunk last handed its state
 // over (tag = epoch + 1, the epoch advanced by the last wave out of every queued launch), so a flag
@@ -120,13 +122,47 @@ enum Solver { SOLVER_NEWTON = 0, SOLVER_PGS = 1 };
 
 // actions: [N][nu] float32 (may be null in MODE_RESET); reset_mask: [N] (null = all);
 // noise_qpos/noise_qvel: [N][nq]/[N][nv] host-supplied reset noise (null = device RNG).
+// Fused PPO rollout (hs_rollout, fp64 engine): a tape launch whose actions come from the policy.
+// After each env step the env's wave runs the SB3 MlpPolicy's pi net (2 hidden layers of 256, ReLU)
+// on the new obs, draws the action (the Philox stream of ppo_act_kernel) and does the rollout
+// buffer bookkeeping of ppo_post_kernel, so a K-step rollout is one launch.  Rollout buffers are
+// indexed by the global step g = t_begin + t.
+struct RolloutArgs {
+  const float* w1;      // [D][ld1] pi layer 1 ([in][out], columns 0..255), ld1 >= 256
+  const float* b1;      // [256]
+  const float* w2;      // [256][256]
+  const float* b2;      // [256]
+  const float* w3;      // [256][A]
+  const float* b3;      // [A]
+  const float* log_std; // [A]
+  int ld1, D, A;
+  int t_begin, t_total; // global step of this launch's first step; rollout length (n_steps)
+  float* obs;           // [t_total][N][D]: rows g + 1 written (row 0 is the caller's)
+  float* obs_last;      // [N][D]: the obs after step t_total - 1 (the next rollout's first obs)
+  float* act;           // [t_total][N][A] unclipped samples (row t_begin is the caller's)
+  float* logp;          // [t_total][N]
+  float* start;         // [t_total][N] episode_start before step g
+  float* rew;           // [t_total][N]
+  uint8_t* done;        // [t_total][N]
+  double* epret;        // [t_total][N] episode return so far (ppo_post's ep_return_out)
+  uint8_t* boot;        // [t_total][N] TimeLimit.truncated and not terminated
+  float* tobs;          // [t_total][N][D] terminal obs of the boot envs
+  double* ep_acc;       // [N] running episode return, in / out
+  float* episode_start; // [N] out: done of the launch's last step
+  float* act_clip;      // [N][A] in: step t_begin's clipped action; out: the next launch's
+  const uint64_t* ctr_base;   // noise counter base (device); step g draws counter g + *ctr_base
+  uint32_t k0, k1;            // Philox key (the 64-bit seed)
+  int deterministic;
+};
+
 // p.nsteps > 1: a tape launch -- actions [nsteps][N][nu], outputs per step in `tape` (may be null), env
 // steps of one env pair run back to back on the chunk queue with the state handed over through
 // b.mid; no wide-tier launch follows (an overflow sets qsync[QS_ABORT], the host replays the tape).
 template <typename T>
 hipError_t launch_step(const DevModel<T>* dmodel, int nv, const EnvBuffers<T>& b, const float* actions,
                        const uint8_t* reset_mask, const T* noise_qpos, const T* noise_qvel,
-                       const StepParams& p, int nenv, hipStream_t stream, const TapeOut<T>* tape = nullptr);
+                       const StepParams& p, int nenv, hipStream_t stream, const TapeOut<T>* tape = nullptr,
+                       const RolloutArgs* ro = nullptr);
 
 // waves of the resident step-kernel instance the current device holds at once (0 if unknown)
 template <typename T>

@@ -28,6 +28,7 @@
 #include <type_traits>
 
 #include "hs_kernels.h"
+#include "hs_philox.h"
 #include "hs_model.h"
 
 namespace hs {
@@ -224,6 +225,7 @@ struct KArgs {
   StepParams p;
   int nenv;
   TapeOut<T> tape;            // per-step outputs of a tape launch (p.nsteps > 1), or all null
+  RolloutArgs ro;             // fused rollout (ro.obs != null): actions from the policy, see hs_kernels.h
 };
 template <typename T>
 using KPtr = const __attribute__((address_space(4))) KArgs<T>*;
@@ -579,6 +581,9 @@ struct Scratch {
     struct { T bvel[MAXBODY][6];                                  // J x mapping (rows, Newton)
              alignas(16) T cb[MAXDOF][2];                         // Cholesky column pairs
              T cfrc[MAXBODY][6], linv[MAXBODY][3], mv[MAXBODY][3]; } n;   // full_state (after solve)
+    // fused rollout's policy forward (fp64 engine only: inside the union's 4 KB there; the fp32
+    // engine's union is smaller and must not grow, so its member is a stub)
+    struct { alignas(16) float x[sizeof(T) == 8 ? 512 : 4]; alignas(16) float h[sizeof(T) == 8 ? 256 : 4]; } pol;
   } u;
 };
 
@@ -2175,8 +2180,8 @@ __device__ __forceinline__ T compute_reward(MPtr<T> m, const Scratch<T, C>& s, K
 }
 
 // custom_env.py:232-261 layout; qfrc_actuator comes from registers (sub-lane i holds dof i)
-template <typename T, typename C>
-__device__ __forceinline__ void write_obs(MPtr<T> m, const Scratch<T, C>& s, int sl, T qfa, T* out,
+template <typename T, typename C, typename O>
+__device__ __forceinline__ void write_obs(MPtr<T> m, const Scratch<T, C>& s, int sl, T qfa, O* out,
                           int obs_dim) {
   int nq = m->nq, nv = m->nv;
   int o1 = nq - 2, o2 = o1 + nv, o3 = o2 + 10 * m->nbody, o4 = o3 + 6 * m->nbody;
@@ -2186,12 +2191,59 @@ __device__ __forceinline__ void write_obs(MPtr<T> m, const Scratch<T, C>& s, int
     else if (k < o2) v = s.qvel[k - o1];
     else if (k < o3) { int q = k - o2; v = s.cinert[q / 10][q % 10]; }
     else { int q = k - o3; v = s.cvel[q / 6][q % 6]; }
-    out[k] = v;
+    out[k] = (O)v;
   }
-  if (sl < nv && o4 + sl < obs_dim) out[o4 + sl] = qfa;
+  if (sl < nv && o4 + sl < obs_dim) out[o4 + sl] = (O)qfa;
   const int o5 = o4 + nv, nf = 6 * (m->nbody - 1);
   if (obs_dim >= o5 + nf)    // full_state: + cfrc_ext[1:] (custom_env.py:247,255, commented out there)
-    for (int k = sl; k < nf; k += HL) out[o5 + k] = s.u.n.cfrc[1 + k / 6][k % 6];
+    for (int k = sl; k < nf; k += HL) out[o5 + k] = (O)s.u.n.cfrc[1 + k / 6][k % 6];
+}
+
+// Fused rollout: the SB3 MlpPolicy's pi net (mlp_extractor.policy_net + action_net, fp32 as SB3's
+// policy) on one env's obs, both half-waves at once, each on its own env.  Hidden layers of 256:
+// sub-lane sl owns outputs 8 sl .. 8 sl + 7, two 16-B weight loads per input (coalesced over the
+// half-wave, the same addresses for both halves); the head: sub-lane sl < A owns action sl.  The obs
+// row and the hidden activations are staged in the scratch union (free after the env step).
+// Returns the action mean of sub-lane sl (0 for sl >= A).
+template <typename T, typename C>
+__device__ __forceinline__ float policy_mean(KPtr<T> k, const float* obs, Scratch<T, C>& s, int sl) {
+  float* x = s.u.pol.x;
+  float* h = s.u.pol.h;
+  const int D = k->ro.D, A = k->ro.A, ld1 = k->ro.ld1;
+  for (int i = sl; i < D; i += HL) x[i] = obs[i];
+  WSYNC();
+  auto layer = [&](const float* w, int ld, const float* b, const float* in, int n, float* out) {
+    float acc[8];
+    const float4 b0 = reinterpret_cast<const float4*>(b + 8 * sl)[0], b1 = reinterpret_cast<const float4*>(b + 8 * sl)[1];
+    acc[0] = b0.x; acc[1] = b0.y; acc[2] = b0.z; acc[3] = b0.w;
+    acc[4] = b1.x; acc[5] = b1.y; acc[6] = b1.z; acc[7] = b1.w;
+    const float* wl = w + 8 * sl;
+#pragma unroll 2
+    for (int i = 0; i < n; i += 4) {
+      const float4 xv = *reinterpret_cast<const float4*>(in + i);
+      const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+      for (int ii = 0; ii < 4; ii++) {
+        const float4* wr = reinterpret_cast<const float4*>(wl + (size_t)(i + ii) * ld);
+        const float4 u0 = wr[0], u1 = wr[1];
+        acc[0] += xs[ii] * u0.x; acc[1] += xs[ii] * u0.y; acc[2] += xs[ii] * u0.z; acc[3] += xs[ii] * u0.w;
+        acc[4] += xs[ii] * u1.x; acc[5] += xs[ii] * u1.y; acc[6] += xs[ii] * u1.z; acc[7] += xs[ii] * u1.w;
+      }
+    }
+    WSYNC();   // every sub-lane has read `in` (out may alias it)
+#pragma unroll
+    for (int j = 0; j < 8; j++) out[8 * sl + j] = fmaxf(acc[j], 0.f);
+    WSYNC();
+  };
+  layer(k->ro.w1, ld1, k->ro.b1, x, D, h);       // obs -> h1
+  layer(k->ro.w2, 256, k->ro.b2, h, 256, x);     // h1 -> h2 (into the obs slot)
+  float mean = 0.f;
+  if (sl < A) {
+    mean = k->ro.b3[sl];
+    const float* w3 = k->ro.w3 + sl;
+    for (int i = 0; i < 256; i++) mean += x[i] * w3[(size_t)i * A];
+  }
+  return mean;
 }
 
 template <typename T, int NV, typename C>
@@ -2279,7 +2331,7 @@ __device__ __forceinline__ void commit(MPtr<T> m, KPtr<T> k, const Stepper<T, NV
 // qacc_warmstart, time), so the hand-off is exact: results are bitwise those of one wave running all
 // substeps.
 // ghost: this half-wave mirrors env idx (the single-env schedule's upper half) and commits nothing.
-template <typename T, int NV, bool PGS, typename C>
+template <typename T, int NV, bool PGS, typename C, bool ROLL = false>
 __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCache<T, C>* pcache, int idx,
                                           int nidx, const int* list, int s0, int s1, int pair, bool ghost = false,
                                           int wait_tag = 0, int set_tag = 0, int tstep = 0) {
@@ -2293,6 +2345,13 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
   const int mode = ka->p.mode;
   if (mode == MODE_RESET && ka->reset_mask && !ka->reset_mask[env_id]) active = false;
   if (__ballot(active) == 0) return;                  // wave-uniform exit
+  const bool real = active;                           // this half steps (and commits) a real env
+  // fused rollout (fp64 engine): the episode return so far and the step's done flag, carried to the
+  // policy forward after the step; the action of steps after the launch's first comes in the row
+  const bool rollout = ROLL && ka->ro.obs != nullptr;
+  double epacc = 0.0;
+  bool rdone = false;
+  T act_row = T(0);
   Scratch<T, C>& s = smem[up ? 1 : 0];
   MPtr<T> m = ka->m;
   const int nq = m->nq, nv = m->nv, nu = m->nu;
@@ -2333,6 +2392,10 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
       step_count = (int)row_ld(r + MID_SC);
       episode = (uint32_t)row_ld(r + MID_EP);
       total = row_ld(r + MID_TOT);
+      if (rollout) {
+        if (sl < nu) act_row = row_ld(r + MID_ACT + sl);
+        epacc = (double)row_ld(r + MID_EPACC);
+      }
       // never seen in practice; if it were, the state is poisoned so that mj_checkPos resets the
       // env and counts HS_WARN_BADQPOS -- loud, like MuJoCo's warning path, never silent
       if (lost && sl == 2) s.qpos[2] = T(NAN);
@@ -2345,6 +2408,7 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
       step_count = ka->b.step_count[env_id];
       episode = ka->b.episode[env_id];
       total = ka->b.total_reward[env_id];
+      if (rollout) epacc = ka->ro.ep_acc[env_id];
     }
     // data.ctrl is an input only to a raw physics call that keeps the current ctrl; env steps set
     // it from the action, resets zero it
@@ -2352,7 +2416,9 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
     if (sl < nu) s.ctrl[sl] = (mode == MODE_PHYSICS && !actions) ? ka->b.ctrl[(size_t)env_id * nu + sl] : T(0);
     // the action is the same for all substeps: one load, issued with the state loads (a tape
     // launch's step tstep reads its own [N][nu] slice)
-    act = (actions && sl < nu) ? (T)actions[((size_t)tstep * ka->nenv + env_id) * nu + sl] : T(0);
+    // (a rollout's `actions` is its first step's, ro.act_clip; later steps' come in the row)
+    act = (rollout && tstep > 0) ? act_row
+        : (actions && sl < nu) ? (T)actions[((size_t)tstep * ka->nenv + env_id) * nu + sl] : T(0);
   }
   WSYNC();
   st.clk.start();
@@ -2403,6 +2469,12 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
   auto obs_row = [&](KPtr<T> k, int env, int obs_dim) -> T* {
     if (k->tape.obs) return k->tape.obs + ((size_t)tstep * k->nenv + env) * obs_dim;
     return tape_final ? k->b.obs + (size_t)env * obs_dim : nullptr;
+  };
+  // fused rollout: the rollout buffer's obs row of step g + 1 (the obs this step returns)
+  auto ro_next_obs = [&](KPtr<T> k, int env) -> float* {
+    const int g = k->ro.t_begin + tstep;
+    return g + 1 < k->ro.t_total ? k->ro.obs + ((size_t)(g + 1) * k->nenv + env) * k->ro.D
+                                 : k->ro.obs_last + (size_t)env * k->ro.D;
   };
 
   // Both halves always run the same instruction stream; a half that is inactive (ghost env,
@@ -2476,6 +2548,24 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
             if (k->b.term_step_count) k->b.term_step_count[env] = step_count;
             if (k->b.term_total_reward) k->b.term_total_reward[env] = total;
           }
+          // fused rollout: SB3 collect_rollouts' bookkeeping of this step (ppo_post_kernel): reward and
+          // done rows, the episode return, TimeLimit.truncated envs' terminal obs for the bootstrap,
+          // and the returned obs (an env that auto-resets returns its reset obs, written below)
+          if (rollout && active) {
+            const float rf = (float)r;
+            const double acc = epacc + (double)rf;
+            rdone = term || trunc;
+            const size_t gi = (size_t)(k->ro.t_begin + tstep) * k->nenv + env;
+            if (sl == 0) {
+              k->ro.rew[gi] = rf;
+              k->ro.done[gi] = rdone;
+              k->ro.epret[gi] = acc;
+              k->ro.boot[gi] = trunc && !term;
+            }
+            epacc = rdone ? 0.0 : acc;
+            if (trunc && !term) write_obs(st.m, s, sl, st.qfa, k->ro.tobs + gi * obs_dim, obs_dim);
+            if (!rdone) write_obs(st.m, s, sl, st.qfa, ro_next_obs(k, env), obs_dim);
+          }
           if ((term || trunc) && k->p.autoreset && active) {
             write_obs(st.m, s, sl, st.qfa, k->b.terminal_obs + (size_t)env * obs_dim, obs_dim);
             do_reset = true;
@@ -2524,6 +2614,7 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
         const int obs_dim = k->p.obs_dim;
         T* orow = obs_row(k, env, obs_dim);
         if (orow) write_obs(st.m, s, sl, st.qfa, orow, obs_dim);
+        if (rollout) write_obs(st.m, s, sl, st.qfa, ro_next_obs(k, env), obs_dim);   // the reset obs
         if (!defer(k)) {
           if (tape_final) commit(st.m, k, st, env, time, xws, 0, episode, T(0), warn, k->p.full_state != 0);
           if (tape_handoff) handoff(k, env, time, xws, 0, episode, T(0));
@@ -2543,6 +2634,47 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
     tot_iter += st.niter;
 #endif
     if (st.dbg && active && !in_reset) dump_debug(st, st.dbg);
+  }
+  if constexpr (ROLL) {
+    if (rollout) {   // the policy acts on the step's obs: step g + 1's action, drawn as ppo_act_kernel does
+      KPtr<T> k = opaque(ka);
+      const int g = k->ro.t_begin + tstep, N = k->nenv, A = k->ro.A;
+      const bool last_of_launch = tstep == k->p.nsteps - 1;
+      T* r = k->b.mid + (size_t)env_id * MIDDIM;
+      if (g + 1 < k->ro.t_total) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's obs row is written before it is read
+        const float mean = policy_mean(k, k->ro.obs + ((size_t)(g + 1) * N + env_id) * k->ro.D, s, sl);
+        const float ls = sl < A ? k->ro.log_std[sl] : 0.f;
+        float z = 0.f;
+        if (!k->ro.deterministic && sl < A)
+          z = policy_noise((uint32_t)env_id, (uint32_t)sl, (uint64_t)(g + 1) + *k->ro.ctr_base, k->ro.k0, k->ro.k1);
+        const float a = mean + __expf(ls) * z;
+        const float lp = half_sum(sl < A ? -0.5f * z * z - ls - 0.91893853320467274f : 0.f);
+        if (real) {
+          const size_t gi = (size_t)(g + 1) * N + env_id;
+          if (sl < A) {
+            const float ac = fminf(fmaxf(a, -1.f), 1.f);
+            k->ro.act[gi * A + sl] = a;
+            if (last_of_launch) k->ro.act_clip[(size_t)env_id * A + sl] = ac;
+            else row_st(r + MID_ACT + sl, (T)ac);
+          }
+          if (sl == 0) {
+            k->ro.logp[gi] = lp;
+            k->ro.start[gi] = rdone ? 1.f : 0.f;
+          }
+        }
+      }
+      // the rollout's last step: act_clip ends as the action that step ran with (as the per-step path)
+      if (real && last_of_launch && g + 1 >= k->ro.t_total && sl < A) k->ro.act_clip[(size_t)env_id * A + sl] = (float)act;
+      if (real && sl == 0) {
+        if (last_of_launch) {
+          k->ro.ep_acc[env_id] = epacc;
+          k->ro.episode_start[env_id] = rdone ? 1.f : 0.f;
+        } else {
+          row_st(r + MID_EPACC, (T)epacc);
+        }
+      }
+    }
   }
   if (tape_handoff) {   // the pair's next env step may start: rows in memory, then the flag
     KPtr<T> k = opaque(ka);
@@ -2588,7 +2720,9 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !PGS) ? 2 : 1) void step_ker
 // results are bitwise the same in any order.  Items are claimed only by running waves and a
 // last-substep item waits only on its own pair's first chunk, claimed npairs items earlier by a
 // running wave: no residency can deadlock it.
-template <typename T, int NV, bool PGS>
+// ROLL: the fused-rollout instance (fp64 Newton engine; launch_step picks it for hs_rollout), so the
+// policy forward's code and registers stay out of the per-step kernel
+template <typename T, int NV, bool PGS, bool ROLL = false>
 __global__ __launch_bounds__(64, 1) void step_kernel_queue(KArgs<T> /* read via kernarg ptr */) {
   const KPtr<T> ka = (KPtr<T>)__builtin_amdgcn_kernarg_segment_ptr();
   // this launch's epoch (its hand-off tags are qtag(epoch, ...)): the epoch only changes after every
@@ -2624,7 +2758,7 @@ __global__ __launch_bounds__(64, 1) void step_kernel_queue(KArgs<T> /* read via 
     i = __builtin_amdgcn_readfirstlane(i);
     // tape launch: K whole env steps per pair, step-major (step t of every pair, then step t + 1);
     // one env step: every pair's first chunk, then every pair's last substep
-    const bool tape = K > 1;
+    const bool tape = K > 1 || k->ro.obs != nullptr;   // (a fused rollout is a tape launch even for K = 1)
     if (i >= (tape ? K * npairs : 2 * npairs)) break;
     if (tape) {   // an aborted tape launch only drains its claims
       int ab = 0;
@@ -2653,8 +2787,8 @@ __global__ __launch_bounds__(64, 1) void step_kernel_queue(KArgs<T> /* read via 
     const int s0 = last ? nsub - 1 : 0, s1 = (tape || last) ? nsub : nsub - 1;
     const int wait_tag = tape ? (t > 0 ? qtag(epoch, t - 1, 1) : 0) : (last ? qtag(epoch, 0, 0) : 0);
     const int set_tag = tape ? (t < K - 1 ? qtag(epoch, t, 1) : 0) : (last ? 0 : qtag(epoch, 0, 0));
-    step_pair<T, NV, PGS, Resident<T>>(k, smem, pcache, env, k->nenv, nullptr, s0, s1, pair, false, wait_tag, set_tag,
-                                       t);
+    step_pair<T, NV, PGS, Resident<T>, ROLL>(k, smem, pcache, env, k->nenv, nullptr, s0, s1, pair, false, wait_tag,
+                                             set_tag, t);
     // the pair's duration for the next launch's order: the first chunk's is kept in qcost (its
     // store trails the hand-off, but the last substep reads it ~100 us later; a stale value only
     // makes the order less exact, never the results different); a tape launch times the pair's
@@ -2765,11 +2899,14 @@ int resident_waves(bool pgs) {
 template <typename T>
 hipError_t launch_step(const DevModel<T>* dmodel, int nv, const EnvBuffers<T>& b, const float* actions,
                        const uint8_t* reset_mask, const T* noise_qpos, const T* noise_qvel,
-                       const StepParams& p, int nenv, hipStream_t stream, const TapeOut<T>* tape) {
+                       const StepParams& p, int nenv, hipStream_t stream, const TapeOut<T>* tape,
+                       const RolloutArgs* ro) {
   if (nenv <= 0) return hipSuccess;
   if (nv != 27) return hipErrorInvalidValue;
   KArgs<T> args{(MPtr<T>)dmodel, b, actions, reset_mask, noise_qpos, noise_qvel, p, nenv,
-                tape ? *tape : TapeOut<T>{nullptr, nullptr, nullptr, nullptr}};
+                tape ? *tape : TapeOut<T>{nullptr, nullptr, nullptr, nullptr}, ro ? *ro : RolloutArgs{}};
+  // fused rollouts: the fp64 Newton engine
+  if (ro && (sizeof(T) != 8 || !ro->obs || p.solver == SOLVER_PGS)) return hipErrorInvalidValue;
   if (args.p.nsteps < 1) args.p.nsteps = 1;
   // chunk-queue schedule when the env pairs outnumber the waves the GPU holds at once (the fp64
   // engine: 1 wave per SIMD), for multi-substep calls (HS_SCHED_DIRECT: never)
@@ -2782,7 +2919,7 @@ hipError_t launch_step(const DevModel<T>* dmodel, int nv, const EnvBuffers<T>& b
   // as items, whatever the batch size -- a pair's next env step starts as soon as its own previous
   // one is committed, so the steps of different pairs overlap instead of each step ending on its
   // slowest pair
-  const bool tape_launch = args.p.nsteps > 1;
+  const bool tape_launch = args.p.nsteps > 1 || ro != nullptr;
   if (tape_launch) {
     if (p.mode != MODE_ENV_STEP || !b.mid || !b.qsync || resident <= 0 || args.p.nsteps > QTAG_STEPS)
       return hipErrorInvalidValue;
@@ -2819,6 +2956,10 @@ hipError_t launch_step(const DevModel<T>* dmodel, int nv, const EnvBuffers<T>& b
     return hipGetLastError();
   }
 #endif
+  if (ro) {
+    if constexpr (sizeof(T) == 8) hipLaunchKernelGGL((step_kernel_queue<T, 27, false, true>), grid, block, 0, stream, args);
+    return hipGetLastError();
+  }
   if (args.p.queue) hipLaunchKernelGGL((step_kernel_queue<T, 27, false>), grid, block, 0, stream, args);
   else hipLaunchKernelGGL((step_kernel<T, 27, false>), grid, block, 0, stream, args);
   if (b.redo && !tape_launch) hipLaunchKernelGGL((step_kernel_wide<T, 27, false>), wgrid, block, 0, stream, args);
@@ -2836,14 +2977,14 @@ hipError_t launch_kinematics(const DevModel<T>* dmodel, int nv, const T* qpos, T
 #ifndef HS_ONLY_F64
 template hipError_t launch_step<float>(const DevModel<float>*, int, const EnvBuffers<float>&, const float*,
                                        const uint8_t*, const float*, const float*, const StepParams&, int,
-                                       hipStream_t, const TapeOut<float>*);
+                                       hipStream_t, const TapeOut<float>*, const RolloutArgs*);
 template int resident_waves<float>(bool);
 template hipError_t launch_kinematics<float>(const DevModel<float>*, int, const float*, float*, hipStream_t);
 #endif
 #if !defined(HS_DEV_F32_ONLY) && !defined(HS_ONLY_F32)
 template hipError_t launch_step<double>(const DevModel<double>*, int, const EnvBuffers<double>&, const float*,
                                         const uint8_t*, const double*, const double*, const StepParams&, int,
-                                        hipStream_t, const TapeOut<double>*);
+                                        hipStream_t, const TapeOut<double>*, const RolloutArgs*);
 #endif
 
 #if !defined(HS_DEV_F32_ONLY) && !defined(HS_ONLY_F32)

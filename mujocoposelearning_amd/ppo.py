@@ -30,6 +30,7 @@ from .ppo_ops import (Linear, _GaussLogpFn, _PPOLossFn, _SplitKLinearFn, _SplitK
                       ppo_loss, ppo_post)
 
 FUSED_MLP = True      # rollout forward through the fused hs_mlp2_forward kernel where it applies
+FUSED_ROLLOUT = True  # whole rollouts as hs_rollout launches (policy inside the env kernel) where they apply
 
 
 def _flat_packed(pk):
@@ -307,12 +308,15 @@ class PPO:
         b, env, pol = self.buf, self.env, self.policy
         T, N = self.n_steps, env.num_envs
         pol.pack_heads()
-        if self.graphs and self._rollout_graph is None and getattr(env, "graph_safe", False):
-            self._capture_rollout()                   # on failure: graphs off, eager body below
-        if self._rollout_graph is not None:
-            self._rollout_graph.replay()
+        if self._fused_rollout_args() is not None:
+            self._rollout_fused()
         else:
-            self._rollout_body()
+            if self.graphs and self._rollout_graph is None and getattr(env, "graph_safe", False):
+                self._capture_rollout()                   # on failure: graphs off, eager body below
+            if self._rollout_graph is not None:
+                self._rollout_graph.replay()
+            else:
+                self._rollout_body()
         self.ep_returns += b["epret"][b["done"]].tolist()      # one device -> host transfer per rollout
         boot = b["boot"].view(-1).nonzero().squeeze(1)
         if boot.numel():                                        # deferred TimeLimit bootstrap
@@ -321,13 +325,77 @@ class PPO:
         last_v = pol.value(self.obs)
         return gae(b["rew"], b["val"], b["start"], last_v, self.episode_start, self.gamma, self.gae_lambda)
 
-    def _rollout_body(self):
-        """The T env steps of a device rollout (what the rollout graph captures)."""
+    def _fused_rollout_args(self):
+        """(batch handle, hs_policy) when the whole rollout can run as hs_rollout launches -- the env's
+        fp64 engine with the device reward (HumanoidVecEnv.rollout_handle) and a pi net of two ReLU
+        layers of 256 (the reference's net_arch, README.md:44-50) -- else None."""
+        if not FUSED_ROLLOUT or self.device.type != "cuda":
+            return None
+        handle = self.env.rollout_handle() if hasattr(self.env, "rollout_handle") else None
+        pk = self.policy._packed
+        if handle is None or pk is None:
+            return None
+        w1, b1, mid, w3, b3 = pk
+        D, A = w1.shape[0], w3.shape[2]
+        if (len(mid) != 1 or w1.shape[1] != 512 or D != self.env.obs_dim or D % 4 or D > 512 or A > 32
+                or A != self.env.act_dim):
+            return None
+        from . import _lib
+        ls = self.policy.log_std.detach()
+        keep = (w1, b1, mid[0][0][0], mid[0][1][0, 0], w3[0], b3[0, 0], ls)
+        if not all(t.is_contiguous() for t in keep):
+            return None
+        pol = _lib.hs_policy(*[t.data_ptr() for t in keep], w1.shape[1], D, A)
+        return handle, pol, keep
+
+    def _rollout_fused(self):
+        """collect_rollouts as hs_rollout launches: this method samples step 0's action on the first obs
+        (the per-step sampler, as _rollout_body), then each launch runs up to hs_rollout_max_steps env
+        steps with the policy forward, sampling and buffer bookkeeping inside the env kernel
+        (hs_kernels.hip step_pair), each env pair's step t + 1 starting when its own step t is done.
+        The noise is hs_ppo_act's Philox stream, so the draws are those of the per-step path; the
+        policy means agree with the GEMM chain to fp32 rounding (tests/test_gpu_ppo.py).  A launch
+        that hits a resident-tier contact overflow is undone by the library, and the rest of the
+        rollout runs step by step."""
+        import ctypes as C
+
+        from . import _lib
+        b, env, pol = self.buf, self.env, self.policy
+        T = self.n_steps
+        handle, cpol, keep = self._fused_rollout_args()
+        b["obs"][0].copy_(self.obs)
+        mean = pol.net_forward(b["obs"][0], 0)
+        ppo_act(mean, self._zero_n, pol.log_std.detach(), self.episode_start, self._noise_seed, 0, False,
+                b["act"][0], self._act_clip, b["logp"][0], self._val_scratch, b["start"][0],
+                counter_base=self._noise_ctr)
+        rb = _lib.hs_rollout_bufs(b["obs"].data_ptr(), self.obs.data_ptr(), b["act"].data_ptr(), b["logp"].data_ptr(),
+                                  b["start"].data_ptr(), b["rew"].data_ptr(), b["done"].data_ptr(),
+                                  b["epret"].data_ptr(), b["boot"].data_ptr(), b["tobs"].data_ptr(),
+                                  self.ep_acc.data_ptr(), self.episode_start.data_ptr(), self._act_clip.data_ptr(),
+                                  self._noise_ctr.data_ptr(), self._noise_seed, 0)
+        L = _lib.check(_lib.lib().hs_rollout_max_steps(handle))
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        t0 = 0
+        while t0 < T:
+            k = min(L, T - t0)
+            rc = _lib.check(_lib.lib().hs_rollout(handle, C.byref(cpol), C.byref(rb), t0, k, T, stream))
+            if rc == 1:                       # resident-tier overflow: state restored, step by step from t0
+                self.fused_fallbacks = getattr(self, "fused_fallbacks", 0) + 1
+                self._rollout_body(t_from=t0)
+                return
+            t0 += k
+        del keep
+        self._rollout_tail()
+
+    def _rollout_body(self, t_from=0):
+        """The T env steps of a device rollout (what the rollout graph captures); t_from > 0: the
+        rest of a rollout whose steps [0, t_from) are in the buffers (the fused path's fallback)."""
         b, env, pol = self.buf, self.env, self.policy
         T, N = self.n_steps, env.num_envs
         gamma = float(self.gamma)
-        b["obs"][0].copy_(self.obs)
-        for t in range(T):
+        if t_from == 0:
+            b["obs"][0].copy_(self.obs)
+        for t in range(t_from, T):
             mean = pol.net_forward(b["obs"][t], 0) if pol._packed is not None else pol.heads(b["obs"][t])[0]
             ppo_act(mean, self._zero_n, pol.log_std.detach(), self.episode_start, self._noise_seed, t, False,
                     b["act"][t], self._act_clip, b["logp"][t], self._val_scratch, b["start"][t],
@@ -337,6 +405,11 @@ class PPO:
             ppo_post(rew.float(), term.to(torch.uint8), trunc.to(torch.uint8), None, gamma, obs.float(), nxt,
                      b["rew"][t], b["done"][t], self.ep_acc, b["epret"][t], self.episode_start,
                      terminal_obs=env.terminal_obs.float(), boot_obs_out=b["tobs"][t], boot_out=b["boot"][t])
+        self._rollout_tail()
+
+    def _rollout_tail(self):
+        b, pol = self.buf, self.policy
+        T, N = self.n_steps, self.env.num_envs
         self._noise_ctr.add_(T)
         # values of every buffered obs in one batched vf forward (SB3 stores V(obs_t) per step;
         # the policy does not change inside a rollout, so this is the same quantity)

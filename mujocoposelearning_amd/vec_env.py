@@ -122,6 +122,16 @@ class HumanoidVecEnv(_Base):
         return (self._host_reward is None and getattr(self.batch, "_streams", None) is None
                 and self._streams is None and self._seeds is None)
 
+    def rollout_handle(self):
+        """The hs_batch handle a fused PPO rollout (hs_rollout) may step, or None: the fp64 Newton
+        engine with the device reward and on-device reset noise (graph_safe), one stream group and
+        auto-reset on."""
+        b = self.batch
+        if (not self.graph_safe or b.precision != "fp64" or not b.cfg.autoreset or len(b._groups) != 1
+                or int(self.model.field("opt_solver")[0]) != 0):
+            return None
+        return b._groups[0][0]
+
     @property
     def terminal_obs(self):
         """[N, obs_dim] device tensor: pre-reset obs of envs whose episode ended in the last step."""

@@ -364,15 +364,17 @@ def test_device_rollout_deferred_timelimit_bootstrap():
 
 
 @pytest.mark.parametrize("prec,n,steps", [("fp32", 256, 12), ("fp64", 4096, 6)])
-def test_graphed_rollout_matches_eager_rollout(prec, n, steps):
+def test_graphed_rollout_matches_eager_rollout(prec, n, steps, monkeypatch):
     """The device rollout captured as one HIP graph (PPO._capture_rollout) writes exactly what the
     eager loop writes: two identical envs + policies, one graphed and one eager, two rollouts
     each (the second replays the graph with fresh noise and a reset inside).  The fp64 case at
     configs[1] size runs the env steps on the chunk-queue schedule (persistent grid, self-resetting
     claim counter and pair flags) inside the replayed graph."""
+    from mujocoposelearning_amd import ppo as ppo_mod
     from mujocoposelearning_amd.model import HsModel
     from mujocoposelearning_amd.ppo import PPO
     from mujocoposelearning_amd.vec_env import HumanoidVecEnv
+    monkeypatch.setattr(ppo_mod, "FUSED_ROLLOUT", False)     # this test is about the per-step graph path
     model = HsModel(XML)
     cfg = {"model_path": XML, "duration": 0.2 if prec == "fp32" else 0.1, "reward_config": {"type": "stand"},
            "frame_skip": 3}
