@@ -505,6 +505,27 @@ def main():
             r = dict(value=n_x * ks * ranks / el, unit="env_steps/s", n_envs_per_gpu=n_x, obs_dim=e.obs_dim,
                      workload=label)
             e.close()
+            if not args.no_rollout and cfg_x.get("full_state_obs"):
+                # configs[4] in the trainer: PPO.collect_rollouts with the fused rollout (hs_rollout)
+                from mujocoposelearning_amd import ppo as ppo_mod
+                e = make_env(args.precision, 4100, cfg_x=cfg_x, n_x=n_x)
+                p = ppo_mod.PPO(e, n_steps=32, batch_size=8192, n_epochs=1, seed=0,
+                                policy_kwargs={"net_arch": {"pi": [256, 256], "vf": [256, 256]},
+                                               "activation_fn": "ReLU"})
+                kk = np.floor(np.arange(n_x) * EPISODE / n_x)
+                e.batch.t["time"].copy_(torch.as_tensor(kk * FRAME_SKIP * TIMESTEP + TIMESTEP, dtype=e.batch.dtype,
+                                                        device=dev))
+                e.batch.t["step_count"].copy_(torch.as_tensor(kk, dtype=torch.int32, device=dev))
+                for _ in range(2):
+                    p.collect_rollouts()
+                barrier()
+                tc0 = time.perf_counter()
+                for _ in range(4):
+                    p.collect_rollouts()
+                barrier()
+                r["collect_rollouts_fused"] = dict(value=n_x * 32 * 4 * ranks / max_over_ranks(time.perf_counter() - tc0),
+                                                   unit="env_steps/s", used_fused=p._fused_rollout_args() is not None)
+                e.close()
             if not args.no_tape:   # the same window as one open-loop tape launch
                 e = make_env(args.precision, 4000, cfg_x=cfg_x, n_x=n_x)
                 precondition(e, tp)
