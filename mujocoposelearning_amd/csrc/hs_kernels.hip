@@ -2200,48 +2200,64 @@ __device__ __forceinline__ void write_obs(MPtr<T> m, const Scratch<T, C>& s, int
 }
 
 // Fused rollout: the SB3 MlpPolicy's pi net (mlp_extractor.policy_net + action_net, fp32 as SB3's
-// policy) on one env's obs, both half-waves at once, each on its own env.  Hidden layers of 256:
-// sub-lane sl owns outputs 8 sl .. 8 sl + 7, two 16-B weight loads per input (coalesced over the
-// half-wave, the same addresses for both halves); the head: sub-lane sl < A owns action sl.  The obs
-// row and the hidden activations are staged in the scratch union (free after the env step).
-// Returns the action mean of sub-lane sl (0 for sl >= A).
+// policy) on the wave's two envs at once (the lower half-wave's env and the upper's; a ghost half
+// mirrors its partner).  Hidden layers of 256: lane L (of 64) owns outputs 4L .. 4L + 3 for BOTH envs,
+// so each input costs one 16-B weight load per lane (coalesced: the wave reads each weight row once)
+// and two LDS broadcasts (the two envs' inputs).  The head: sub-lane sl < A of each half owns action
+// sl of its half's env.  The obs rows and hidden activations are staged in each half's scratch union
+// (free after the env step).  Returns the action mean of (this half's env, sub-lane sl), 0 for sl >= A.
+#ifndef HS_POL_UNROLL
+#define HS_POL_UNROLL 4
+#endif
+#ifndef HS_POL_HEAD_UNROLL
+#define HS_POL_HEAD_UNROLL 16
+#endif
+constexpr int kPolUnroll = HS_POL_UNROLL, kPolHeadUnroll = HS_POL_HEAD_UNROLL;
 template <typename T, typename C>
-__device__ __forceinline__ float policy_mean(KPtr<T> k, const float* obs, Scratch<T, C>& s, int sl) {
-  float* x = s.u.pol.x;
-  float* h = s.u.pol.h;
+__device__ __forceinline__ float policy_mean(KPtr<T> k, const float* obs, Scratch<T, C>* smem, int lane) {
+  const bool up = lane >= HL;
+  const int sl = lane & (HL - 1);
+  float* xa = smem[0].u.pol.x;   // lower half's env
+  float* xb = smem[1].u.pol.x;   // upper half's env
+  float* ha = smem[0].u.pol.h;
+  float* hb = smem[1].u.pol.h;
   const int D = k->ro.D, A = k->ro.A, ld1 = k->ro.ld1;
-  for (int i = sl; i < D; i += HL) x[i] = obs[i];
+  float* xo = up ? xb : xa;
+  for (int i = sl; i < D; i += HL) xo[i] = obs[i];
   WSYNC();
-  auto layer = [&](const float* w, int ld, const float* b, const float* in, int n, float* out) {
-    float acc[8];
-    const float4 b0 = reinterpret_cast<const float4*>(b + 8 * sl)[0], b1 = reinterpret_cast<const float4*>(b + 8 * sl)[1];
-    acc[0] = b0.x; acc[1] = b0.y; acc[2] = b0.z; acc[3] = b0.w;
-    acc[4] = b1.x; acc[5] = b1.y; acc[6] = b1.z; acc[7] = b1.w;
-    const float* wl = w + 8 * sl;
-#pragma unroll 2
+  auto layer = [&](const float* w, int ld, const float* b, const float* ina, const float* inb, int n, float* outa,
+                   float* outb) {
+    const float4 bb = reinterpret_cast<const float4*>(b + 4 * lane)[0];
+    float a[4] = {bb.x, bb.y, bb.z, bb.w}, c[4] = {bb.x, bb.y, bb.z, bb.w};
+    const float* wl = w + 4 * lane;
+#pragma unroll kPolUnroll
     for (int i = 0; i < n; i += 4) {
-      const float4 xv = *reinterpret_cast<const float4*>(in + i);
-      const float xs[4] = {xv.x, xv.y, xv.z, xv.w};
+      const float4 va = *reinterpret_cast<const float4*>(ina + i);
+      const float4 vb = *reinterpret_cast<const float4*>(inb + i);
+      const float xs[4] = {va.x, va.y, va.z, va.w}, ys[4] = {vb.x, vb.y, vb.z, vb.w};
 #pragma unroll
       for (int ii = 0; ii < 4; ii++) {
-        const float4* wr = reinterpret_cast<const float4*>(wl + (size_t)(i + ii) * ld);
-        const float4 u0 = wr[0], u1 = wr[1];
-        acc[0] += xs[ii] * u0.x; acc[1] += xs[ii] * u0.y; acc[2] += xs[ii] * u0.z; acc[3] += xs[ii] * u0.w;
-        acc[4] += xs[ii] * u1.x; acc[5] += xs[ii] * u1.y; acc[6] += xs[ii] * u1.z; acc[7] += xs[ii] * u1.w;
+        const float4 u = *reinterpret_cast<const float4*>(wl + (size_t)(i + ii) * ld);
+        a[0] += xs[ii] * u.x; a[1] += xs[ii] * u.y; a[2] += xs[ii] * u.z; a[3] += xs[ii] * u.w;
+        c[0] += ys[ii] * u.x; c[1] += ys[ii] * u.y; c[2] += ys[ii] * u.z; c[3] += ys[ii] * u.w;
       }
     }
-    WSYNC();   // every sub-lane has read `in` (out may alias it)
+    WSYNC();   // every lane has read the inputs (the outputs may alias them)
 #pragma unroll
-    for (int j = 0; j < 8; j++) out[8 * sl + j] = fmaxf(acc[j], 0.f);
+    for (int j = 0; j < 4; j++) {
+      outa[4 * lane + j] = fmaxf(a[j], 0.f);
+      outb[4 * lane + j] = fmaxf(c[j], 0.f);
+    }
     WSYNC();
   };
-  layer(k->ro.w1, ld1, k->ro.b1, x, D, h);       // obs -> h1
-  layer(k->ro.w2, 256, k->ro.b2, h, 256, x);     // h1 -> h2 (into the obs slot)
+  layer(k->ro.w1, ld1, k->ro.b1, xa, xb, D, ha, hb);        // obs -> h1
+  layer(k->ro.w2, 256, k->ro.b2, ha, hb, 256, xa, xb);      // h1 -> h2 (into the obs slots)
   float mean = 0.f;
   if (sl < A) {
     mean = k->ro.b3[sl];
     const float* w3 = k->ro.w3 + sl;
-    for (int i = 0; i < 256; i++) mean += x[i] * w3[(size_t)i * A];
+#pragma unroll kPolHeadUnroll
+    for (int i = 0; i < 256; i++) mean += xo[i] * w3[(size_t)i * A];
   }
   return mean;
 }
@@ -2643,7 +2659,7 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
       T* r = k->b.mid + (size_t)env_id * MIDDIM;
       if (g + 1 < k->ro.t_total) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's obs row is written before it is read
-        const float mean = policy_mean(k, k->ro.obs + ((size_t)(g + 1) * N + env_id) * k->ro.D, s, sl);
+        const float mean = policy_mean(k, k->ro.obs + ((size_t)(g + 1) * N + env_id) * k->ro.D, smem, lane);
         const float ls = sl < A ? k->ro.log_std[sl] : 0.f;
         float z = 0.f;
         if (!k->ro.deterministic && sl < A)
