@@ -123,3 +123,40 @@ def test_fused_rollout_overflow_falls_back_step_by_step():
     _check_rollout(ppo, replay, ep_acc0, start0, ctr0)
     env.close()
     replay.close()
+
+
+def test_hs_rollout_refuses_what_it_cannot_run():
+    """hs_rollout fails loudly (HsimError with the reason) for an fp32 batch and for a policy whose
+    obs width is not the batch's, and PPO falls back to the per-step path for them."""
+    import ctypes as C
+
+    from mujocoposelearning_amd import _lib
+    from mujocoposelearning_amd._lib import HsimError
+    from mujocoposelearning_amd.model import HsModel
+    from mujocoposelearning_amd.ppo import PPO
+    from mujocoposelearning_amd.vec_env import HumanoidVecEnv
+    env32 = HumanoidVecEnv({"model_path": XML, "duration": 10.0, "reward_config": {"type": "stand"}, "frame_skip": 3},
+                           n_envs=64, model=HsModel(XML), seed=0, precision="fp32")
+    assert env32.rollout_handle() is None
+    p32 = PPO(env32, n_steps=4, **KW)
+    p32.policy.pack_heads()
+    assert p32._fused_rollout_args() is None
+    env = _env(64)
+    p = PPO(env, n_steps=4, **KW)
+    p.policy.pack_heads()
+    h, pol, keep = p._fused_rollout_args()
+    b = p.buf
+    rb = _lib.hs_rollout_bufs(b["obs"].data_ptr(), p.obs.data_ptr(), b["act"].data_ptr(), b["logp"].data_ptr(),
+                              b["start"].data_ptr(), b["rew"].data_ptr(), b["done"].data_ptr(), b["epret"].data_ptr(),
+                              b["boot"].data_ptr(), b["tobs"].data_ptr(), p.ep_acc.data_ptr(),
+                              p.episode_start.data_ptr(), p._act_clip.data_ptr(), p._noise_ctr.data_ptr(), 1, 0)
+    bad = _lib.hs_policy(*[t.data_ptr() for t in keep], 512, 348, 21)          # obs width != the batch's
+    with pytest.raises(HsimError, match="policy shape"):
+        _lib.check(_lib.lib().hs_rollout(h, C.byref(bad), C.byref(rb), 0, 4, 4, None))
+    h32 = env32.batch._groups[0][0]
+    with pytest.raises(HsimError, match="fp64"):
+        _lib.check(_lib.lib().hs_rollout(h32, C.byref(pol), C.byref(rb), 0, 4, 4, None))
+    with pytest.raises(HsimError, match="n_steps"):
+        _lib.check(_lib.lib().hs_rollout(h, C.byref(pol), C.byref(rb), 0, 5, 4, None))
+    env.close()
+    env32.close()

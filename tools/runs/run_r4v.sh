@@ -1,0 +1,12 @@
+# round 4 v: checkpoint after tape launches and fused rollouts -- GPU suite, smoke, default bench line, rocprof trace +
+# PMC passes of the fp64 step kernel (profiles/collect.sh r4v)
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out/r4v
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --maxfail=8 --timeout 300 --timeout-method thread > gpurun_out/r4v/gputest.log 2>&1
+rc=$?
+echo "pytest rc=$rc" >> gpurun_out/r4v/gputest.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r4v/smoke.log 2>&1 || exit 5
+timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > gpurun_out/r4v/bench.log 2>&1 || exit 6
+bash profiles/collect.sh r4v fp64 > gpurun_out/collect_r4v.log 2>&1 || exit 7
+exit $rc
