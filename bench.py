@@ -19,9 +19,10 @@ N GPUs run N independent env shards (weak scaling, no data-path collective).  ``
 without a launcher spawns the N ranks itself (torch.distributed.run, 127.0.0.1); under an
 external launcher WORLD_SIZE must equal N.  Rank 0 prints one JSON line.
 
-Extra keys: fp32 sim-only, full-episode legs on tapes T0/T1/T2, rollout / train /
-GAE, configs[3]/[4], the step-kernel roofline (HBM bytes vs 8 TB/s, live HIP events on the
-launch stream) and the CPU baseline (the reference's n_envs=8 SubprocVecEnv path, on the
+Extra keys: fp32 sim-only, the same window as one open-loop tape launch (hs_step_tape),
+full-episode legs on tapes T0/T1/T2, rollout (+ PPO.collect_rollouts fused vs
+per-step) / train / GAE, configs[3]/[4] (+ tape and fused-collect variants), the step-kernel
+roofline (HBM bytes vs 8 TB/s, live HIP events on the launch stream) and the CPU baseline (the reference's n_envs=8 SubprocVecEnv path, on the
 oracle's fp64 C restatement of mj_step because MuJoCo is not installable: kind "port").
 """
 import argparse
