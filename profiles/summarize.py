@@ -87,8 +87,11 @@ def resource_lines(kernel_name, out):
         res = code_object_resources()
         mangled = next((k for k in res if k in kernel_name), None)
         if mangled is None:   # rocprofv3 prints demangled names: match on the instance's template arguments
-            want = ("step_kernel_queue" if "queue" in kernel_name else "step_kernel") + \
-                   ("Id" if "double" in kernel_name else "If") + "Li27ELb" + ("1" if "true" in kernel_name else "0")
+            # step_kernel_queue<T, 27, PGS, ROLL>: the per-step instance has ROLL = false (the fused-rollout
+            # instance, ROLL = true, never runs in the profiled bench legs)
+            queue = "queue" in kernel_name
+            want = ("step_kernel_queue" if queue else "step_kernel") + ("Id" if "double" in kernel_name else "If") + \
+                "Li27ELb" + ("1" if "true" in kernel_name.split(",")[2] else "0") + ("ELb0E" if queue else "E")
             mangled = next((k for k in res if want in k and "wide" not in k), None)
         r = res.get(mangled)
         if r:
