@@ -22,8 +22,9 @@ external launcher WORLD_SIZE must equal N.  Rank 0 prints one JSON line.
 Extra keys: fp32 sim-only, the same window as one open-loop tape launch (hs_step_tape),
 full-episode legs on tapes T0/T1/T2, rollout (+ PPO.collect_rollouts fused vs
 per-step) / train / GAE, configs[3]/[4] (+ tape and fused-collect variants), the step-kernel
-roofline (HBM bytes vs 8 TB/s, live HIP events on the launch stream) and the CPU baseline (the reference's n_envs=8 SubprocVecEnv path, on the
-oracle's fp64 C restatement of mj_step because MuJoCo is not installable: kind "port").
+roofline (HBM bytes vs 8 TB/s, live HIP events on the launch stream) and the CPU baseline (the
+reference's n_envs=8 SubprocVecEnv path, on the oracle's fp64 C restatement of mj_step because
+MuJoCo is not installable: kind "port").
 """
 import argparse
 import json
@@ -296,7 +297,9 @@ def main():
     def timed_tape(e, tape, steps, warmup, offset=0):
         """The same window as ``timed`` as ONE tape launch (HsBatch.step_tape: K env steps, each env
         pair's step t + 1 starting once its own step t is committed); open loop, bitwise the step
-        loop's results (tests/test_gpu_tape.py).  Returns (wall seconds max over ranks, ms per env step)."""
+        loop's results (tests/test_gpu_tape.py).  Every step's obs / reward / done flags are written
+        (per-step output slices), as the per-step launches write them.  Returns (wall seconds max over
+        ranks, ms per env step)."""
         for k in range(warmup):
             e.step_tensors(tape[(offset + k) % tape.shape[0]])
         idx = torch.arange(offset + warmup, offset + warmup + steps, device=dev) % tape.shape[0]
@@ -305,7 +308,7 @@ def main():
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         ev0.record(stream)
-        e.batch.step_tape(tp, outputs=False)
+        e.batch.step_tape(tp, outputs=True)
         ev1.record(stream)
         barrier()
         return max_over_ranks(time.perf_counter() - t0), ev0.elapsed_time(ev1) / steps
@@ -374,8 +377,9 @@ def main():
         tape_leg = dict(value=n * args.steps * ranks / el, unit="env_steps/s", dtype="f64" if args.precision == "fp64"
                         else "f32", steps=args.steps, ms_per_env_step=ms, tape_aborts=e.batch.tape_aborts(),
                         note="same workload, window and action tape as the headline, all timed env steps in ONE "
-                             "hs_step_tape launch (open loop: each env pair's step t+1 starts when its own step t "
-                             "is committed, so steps do not end on their slowest pair); bitwise the per-step results")
+                             "hs_step_tape launch with every step's obs / reward / done written (open loop: each env "
+                             "pair's step t+1 starts when its own step t is committed, so steps do not end on their "
+                             "slowest pair); bitwise the per-step results")
         e.close()
 
     # ---- full episodes from a synchronized reset on tapes T0 / T1 / T2, per phase
