@@ -128,3 +128,36 @@ def test_step_tape_overflow_replays_step_by_step(model):
     _same("per-step", per_a, per_b)
     _same("final", fin_a, fin_b)
     _same("after", aft_a, aft_b)
+
+
+def test_step_tape_pgs_instance_bitwise_equals_step_loop(tmp_path):
+    """The <option solver="PGS"> kernel instance takes the same tape path (its own queue kernel):
+    bitwise the step loop at 4096 fp64 envs (more pairs than the PGS instance's resident waves)."""
+    import torch
+    from mujocoposelearning_amd.batch import HsBatch
+    from mujocoposelearning_amd.model import HsModel
+    from test_gpu_pgs import _pgs_xml
+    model = HsModel(_pgs_xml(tmp_path, 100, 1e-8))
+    n, K = 4096, 8
+    g = torch.Generator(device="cuda").manual_seed(31)
+    acts = torch.rand(K, n, 21, device="cuda", generator=g) * 2 - 1
+    t0 = np.floor(np.arange(n) * 667 / n) * 0.015 + 0.005
+    outs = []
+    for tape in (True, False):
+        b = HsBatch(model, n, precision="fp64", seed=3)
+        b.configure(frame_skip=3, duration=10.0, reward_id=0, autoreset=1, max_steps=750)
+        b.reset()
+        b.set_state(time=t0)
+        if tape:
+            obs = b.step_tape(acts)[0].clone()
+        else:
+            o = []
+            for k in range(K):
+                b.step(acts[k])
+                o.append(b.obs.clone())
+            obs = torch.stack(o)
+        outs.append([obs, b.qpos.clone(), b.qvel.clone(), b.qacc_warmstart.clone(), b.warning.clone()])
+        if tape:
+            assert b.tape_aborts() == 0
+        b.close()
+    _same("pgs", outs[0], outs[1])
