@@ -25,11 +25,14 @@ KW = dict(batch_size=1024, n_epochs=1, seed=0,
           policy_kwargs={"activation_fn": "ReLU", "net_arch": {"pi": [256, 256], "vf": [256, 256]}})
 
 
-def _env(n, seed=0):
+def _env(n, seed=0, full_state=False):
     from mujocoposelearning_amd.model import HsModel
     from mujocoposelearning_amd.vec_env import HumanoidVecEnv
-    return HumanoidVecEnv({"model_path": XML, "duration": 10.0, "reward_config": {"type": "stand"}, "frame_skip": 3},
-                          n_envs=n, model=HsModel(XML), seed=seed, precision="fp64")
+    cfg = {"model_path": XML, "duration": 10.0, "frame_skip": 3,
+           "reward_config": {"type": "kneeling" if full_state else "stand"}}
+    if full_state:
+        cfg["full_state_obs"] = True        # BASELINE.json configs[4]: 448-value obs
+    return HumanoidVecEnv(cfg, n_envs=n, model=HsModel(XML), seed=seed, precision="fp64")
 
 
 def _stagger(env):
@@ -80,10 +83,10 @@ def _copy_env(src, dst):
         dst.batch.t[k].copy_(v)
 
 
-@pytest.mark.parametrize("n,T", [(4096, 20), (777, 30)])
-def test_fused_rollout_matches_env_replay_and_policy(n, T):
+@pytest.mark.parametrize("n,T,full", [(4096, 20, False), (777, 30, False), (1024, 16, True)])
+def test_fused_rollout_matches_env_replay_and_policy(n, T, full):
     from mujocoposelearning_amd.ppo import PPO
-    env, replay = _env(n), _env(n)
+    env, replay = _env(n, full_state=full), _env(n, full_state=full)
     ppo = PPO(env, n_steps=T, **KW)
     ppo.policy.pack_heads()
     assert ppo._fused_rollout_args() is not None
