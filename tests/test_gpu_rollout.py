@@ -163,3 +163,41 @@ def test_hs_rollout_refuses_what_it_cannot_run():
         _lib.check(_lib.lib().hs_rollout(h, C.byref(pol), C.byref(rb), 0, 5, 4, None))
     env.close()
     env32.close()
+
+
+def _fused_world2_worker(rank, world, port, out_dir):
+    import os
+    import torch.distributed as dist
+    from mujocoposelearning_amd.ppo import PPO
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)     # both ranks share the one GPU
+    try:
+        env = _env(512, seed=10 + rank)
+        ppo = PPO(env, n_steps=16, batch_size=2048, n_epochs=2, seed=0,
+                  policy_kwargs={"activation_fn": "ReLU", "net_arch": {"pi": [256, 256], "vf": [256, 256]}})
+        ppo.learn(3 * 16 * 512 * world)
+        flat = torch.cat([q.detach().reshape(-1) for q in ppo.policy.parameters()]).cpu()
+        torch.save({"w": flat, "fused": ppo._fused_rollout_args() is not None,
+                    "fallbacks": getattr(ppo, "fused_fallbacks", 0), "steps": ppo.num_timesteps},
+                   os.path.join(out_dir, f"r{rank}.pt"))
+        env.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_fused_rollouts_multi_rank_lockstep(tmp_path):
+    """world 2 (gloo rehearsal, two ranks on one GPU, different env seeds): PPO.learn with fused
+    rollouts on both ranks, one gradient all-reduce per optimizer step -- both ranks end with the
+    same weights (train_sb3.py:203's envs sharded over GPUs)."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.start_processes(_fused_world2_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    r = [torch.load(tmp_path / f"r{i}.pt", weights_only=True) for i in range(2)]
+    assert r[0]["fused"] and r[1]["fused"] and r[0]["fallbacks"] == r[1]["fallbacks"] == 0
+    assert r[0]["steps"] == r[1]["steps"] == 3 * 16 * 512 * 2
+    assert torch.equal(r[0]["w"], r[1]["w"]), "ranks diverged"
