@@ -25,19 +25,19 @@ KW = dict(batch_size=1024, n_epochs=1, seed=0,
           policy_kwargs={"activation_fn": "ReLU", "net_arch": {"pi": [256, 256], "vf": [256, 256]}})
 
 
-def _env(n, seed=0, full_state=False):
+def _env(n, seed=0, full_state=False, duration=10.0):
     from mujocoposelearning_amd.model import HsModel
     from mujocoposelearning_amd.vec_env import HumanoidVecEnv
-    cfg = {"model_path": XML, "duration": 10.0, "frame_skip": 3,
+    cfg = {"model_path": XML, "duration": duration, "frame_skip": 3,
            "reward_config": {"type": "kneeling" if full_state else "stand"}}
     if full_state:
         cfg["full_state_obs"] = True        # BASELINE.json configs[4]: 448-value obs
     return HumanoidVecEnv(cfg, n_envs=n, model=HsModel(XML), seed=seed, precision="fp64")
 
 
-def _stagger(env):
+def _stagger(env, episode_len=667):
     n = env.num_envs
-    k = np.floor(np.arange(n) * 667 / n)
+    k = np.floor(np.arange(n) * episode_len / n)
     env.batch.t["time"].copy_(torch.as_tensor(k * 0.015 + 0.005, dtype=env.batch.dtype, device=env.device))
     env.batch.t["step_count"].copy_(torch.as_tensor(k, dtype=torch.int32, device=env.device))
 
@@ -83,14 +83,20 @@ def _copy_env(src, dst):
         dst.batch.t[k].copy_(v)
 
 
-@pytest.mark.parametrize("n,T,full", [(4096, 20, False), (777, 30, False), (1024, 16, True)])
-def test_fused_rollout_matches_env_replay_and_policy(n, T, full):
+@pytest.mark.parametrize("n,T,full,duration", [(4096, 20, False, 10.0), (777, 30, False, 10.0),
+                                               (1024, 16, True, 10.0), (512, 80, False, 0.5)])
+def test_fused_rollout_matches_env_replay_and_policy(n, T, full, duration):
+    """The last case: 0.5 s episodes (33 env steps), so hs_rollout_max_steps is 32 and the 80-step
+    rollout is three launches, with every env auto-resetting two or three times."""
     from mujocoposelearning_amd.ppo import PPO
-    env, replay = _env(n, full_state=full), _env(n, full_state=full)
+    env, replay = _env(n, full_state=full, duration=duration), _env(n, full_state=full, duration=duration)
     ppo = PPO(env, n_steps=T, **KW)
     ppo.policy.pack_heads()
     assert ppo._fused_rollout_args() is not None
-    _stagger(env)
+    if duration < 1.0:
+        from mujocoposelearning_amd import _lib
+        assert _lib.check(_lib.lib().hs_rollout_max_steps(env.rollout_handle())) < T // 2
+    _stagger(env, round(duration / 0.015))
     for it in range(2):            # the second rollout continues from the first (obs, ep_acc, starts, noise)
         _copy_env(env, replay)
         ep_acc0, start0, ctr0 = ppo.ep_acc.clone(), ppo.episode_start.clone(), int(ppo._noise_ctr.item())
