@@ -2206,13 +2206,9 @@ __device__ __forceinline__ void write_obs(MPtr<T> m, const Scratch<T, C>& s, int
 // and two LDS broadcasts (the two envs' inputs).  The head: sub-lane sl < A of each half owns action
 // sl of its half's env.  The obs rows and hidden activations are staged in each half's scratch union
 // (free after the env step).  Returns the action mean of (this half's env, sub-lane sl), 0 for sl >= A.
-#ifndef HS_POL_UNROLL
-#define HS_POL_UNROLL 4
-#endif
-#ifndef HS_POL_HEAD_UNROLL
-#define HS_POL_HEAD_UNROLL 16
-#endif
-constexpr int kPolUnroll = HS_POL_UNROLL, kPolHeadUnroll = HS_POL_HEAD_UNROLL;
+// unroll of the hidden layers' loads (groups of 4 rows) and of the head's: measured 1 / 2 / 4 / 8 in
+// profiles/ab/ab_r4u_policy_unroll.log (4 and 8 tie), a rolling 16-row ring in ab_r4ae_policy_ring.log
+constexpr int kPolUnroll = 4, kPolHeadUnroll = 16;
 template <typename T, typename C>
 __device__ __forceinline__ float policy_mean(KPtr<T> k, const float* obs, Scratch<T, C>* smem, int lane) {
   const bool up = lane >= HL;
