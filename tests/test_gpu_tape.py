@@ -23,11 +23,12 @@ def model():
     return HsModel(XML)
 
 
-def _run(model, n, prec, acts, t0, tape, full_state=False, reward_id=0, lying=None, outputs=True, pre_step=True):
+def _run(model, n, prec, acts, t0, tape, full_state=False, reward_id=0, lying=None, outputs=True, pre_step=True,
+         duration=10.0, max_steps=750):
     import torch
     from mujocoposelearning_amd.batch import HsBatch
     b = HsBatch(model, n, precision=prec, seed=3, full_state=full_state)
-    b.configure(frame_skip=3, duration=10.0, reward_id=reward_id, autoreset=1, max_steps=750)
+    b.configure(frame_skip=3, duration=duration, reward_id=reward_id, autoreset=1, max_steps=max_steps)
     b.reset()
     b.set_state(time=t0)
     if lying is not None:
@@ -89,6 +90,31 @@ def test_step_tape_bitwise_equals_step_loop(model, prec, n, full, reward):
     per_b, fin_b, aft_b, info_b = _run(model, n, prec, acts, t0, False, full, reward)
     assert info_a["aborts"] == 0 and info_a["reruns"] == info_b["reruns"]
     assert int(torch.stack([x for x in per_b[2]]).sum()) > 0     # episodes ended inside the tape
+    _same("per-step", per_a, per_b)
+    _same("final", fin_a, fin_b)
+    _same("after", aft_a, aft_b)
+
+
+@pytest.mark.parametrize("duration,max_steps", [(0.5, 750), (10.0, 20)], ids=["short-episodes", "truncation"])
+def test_step_tape_longer_than_an_episode_is_split(model, duration, max_steps):
+    """A tape longer than the shortest episode runs as several launches (the host splits it at
+    hs_rollout_max_steps, so each env finishes at most one episode per launch): 0.5 s episodes
+    (33 env steps, termination at duration) and max_steps 20 (TimeLimit truncation), 80 steps each,
+    every env resetting two to four times inside the tape -- bitwise the step loop."""
+    import torch
+    n, K = 1024, 80
+    g = torch.Generator(device="cuda").manual_seed(12)
+    acts = torch.rand(K + 2, n, 21, device="cuda", generator=g) * 2 - 1
+    L = min(max_steps, round(duration / 0.015))
+    t0 = np.floor(np.arange(n) * L / n) * 0.015 + 0.005 if max_steps >= 750 else np.zeros(n) + 0.005
+    kw = dict(duration=duration, max_steps=max_steps)
+    per_a, fin_a, aft_a, info_a = _run(model, n, "fp64", acts, t0, True, **kw)
+    per_b, fin_b, aft_b, info_b = _run(model, n, "fp64", acts, t0, False, **kw)
+    assert info_a["aborts"] == 0
+    ends = per_b[2].int() + per_b[3].int()
+    assert int(ends.sum(0).min()) >= 2                               # every env reset at least twice
+    if max_steps < 750:
+        assert int(per_b[3].sum()) > 0                               # TimeLimit truncations inside the tape
     _same("per-step", per_a, per_b)
     _same("final", fin_a, fin_b)
     _same("after", aft_a, aft_b)
