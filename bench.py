@@ -190,6 +190,8 @@ def main():
                     help="time from a synchronized reset (standing humanoids only) instead of the staggered mix")
     ap.add_argument("--free-groups", type=int, default=0, help="extra sim-only leg: this many free-running stream "
                                                                 "groups (0: skip)")
+    ap.add_argument("--protocol-tape", action="store_true",
+                    help="with --protocol: time the 10000 steps as hs_step_tape calls of 500 steps (open loop)")
     ap.add_argument("--protocol", action="store_true",
                     help="SURVEY 8d protocol instead of the default run: 1000 warm-up + 10000 timed env steps "
                          "per tape T0/T1/T2 and base seed {0,1,2} (~2 min per precision)")
@@ -294,21 +296,24 @@ def main():
         barrier()
         return max_over_ranks(time.perf_counter() - t0), ev0.elapsed_time(ev1) / steps
 
-    def timed_tape(e, tape, steps, warmup, offset=0):
+    def timed_tape(e, tape, steps, warmup, offset=0, chunk=None):
         """The same window as ``timed`` as ONE tape launch (HsBatch.step_tape: K env steps, each env
         pair's step t + 1 starting once its own step t is committed); open loop, bitwise the step
         loop's results (tests/test_gpu_tape.py).  Every step's obs / reward / done flags are written
-        (per-step output slices), as the per-step launches write them.  Returns (wall seconds max over
-        ranks, ms per env step)."""
+        (per-step output slices), as the per-step launches write them.  ``chunk``: step_tape calls of
+        at most that many steps (bounds the per-step output slices of long windows).  Returns (wall
+        seconds max over ranks, ms per env step)."""
         for k in range(warmup):
             e.step_tensors(tape[(offset + k) % tape.shape[0]])
         idx = torch.arange(offset + warmup, offset + warmup + steps, device=dev) % tape.shape[0]
         tp = tape.index_select(0, idx).contiguous()
+        chunk = chunk or steps
         barrier()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         ev0.record(stream)
-        e.batch.step_tape(tp, outputs=True)
+        for c in range(0, steps, chunk):
+            e.batch.step_tape(tp[c:c + chunk], outputs=True)
         ev1.record(stream)
         barrier()
         return max_over_ranks(time.perf_counter() - t0), ev0.elapsed_time(ev1) / steps
@@ -342,7 +347,8 @@ def main():
                     fallen_frac=float((e.batch.qpos[:, 2] < 0.8).double().mean()), **warn_stats(e))
 
     if args.protocol:
-        return run_protocol(args, rank, world, ranks, make_env, make_tape, precondition, timed, stats_of)
+        tfn = (lambda e, tp, steps, warmup: timed_tape(e, tp, steps, warmup, chunk=500)) if args.protocol_tape else timed
+        return run_protocol(args, rank, world, ranks, make_env, make_tape, precondition, tfn, stats_of)
 
     # ---- headline: configs[1], fp64, staggered whole-episode mix
     tape = make_tape("T1", 1024, n, 1 + rank)
@@ -691,6 +697,7 @@ def run_protocol(args, rank, world, ranks, make_env, make_tape, precondition, ti
     if rank == 0:
         vals = [r["value"] for r in res.values()]
         print(json.dumps({"protocol": "SURVEY 8d: 1000 warm-up + 10000 timed env steps", "precision": args.precision,
+                          "launches": "hs_step_tape, 500 steps per call" if args.protocol_tape else "one per env step",
                           "n_envs_per_gpu": args.envs, "n_gpus": ranks, "mean_value": float(np.mean(vals)),
                           "min_value": float(np.min(vals)), "runs": res}))
     if world > 1:
