@@ -251,7 +251,8 @@ class HsBatch:
         launch does not end every step on its slowest pair).  Bitwise the results of K ``step``
         calls.  outputs=True returns the per-step (obs [K, N, obs_dim], reward [K, N], terminated,
         truncated [K, N] uint8); the batch's own buffers hold the last step either way.  Open loop:
-        benchmarks, trajectory evaluation -- a policy in the loop steps with ``step``.  Synchronous;
+        benchmarks, trajectory evaluation -- a policy in the loop steps with ``step`` (or, for the PPO pi
+        net, inside the launch: hs_rollout, PPO._rollout_fused).  Synchronous;
         one stream group only."""
         torch = _torch()
         if len(self._groups) != 1:
