@@ -48,8 +48,18 @@ enum { ST_KIN = 0, ST_COM, ST_TENDON, ST_CRB, ST_COLLISION, ST_CONSTRAINT, ST_CO
  * the restatement.  1: pyramidal R without MuJoCo's 2 mu^2 / impratio scale; 2: Euler without the
  * implicit damping (H = M instead of M + h B); 4: friction mixed by min instead of max;
  * 8: Newton stopped by MuJoCo's tolerance rule (scale * improvement or scale * |grad| below
- * opt.tolerance) instead of at the exact active set -- not wrong, a sensitivity check. */
+ * opt.tolerance) instead of at the exact active set -- not wrong, a sensitivity check.
+ * Mixed-precision Newton candidates (the round-5 CPU gate; built with oracle/precemu.h
+ * and the solver_hessian / solver_cholesky stages in fp32, so H, its factor and the triangular
+ * solves round to float while the gradient, cost and line search stay fp64):
+ * 16: the factor is a preconditioner -- kept while the active set is unchanged (refinement steps
+ *     reuse it) and the solve stops only when scale * |grad| < orc_mp_tol.
+ * Without 16 the same fp32 stages keep the exact-active-set stop: no refinement, so the first
+ * inexact step that leaves the active set unchanged ends the solve. */
 int orc_variant = 0;
+double orc_mp_tol = 1e-13;
+int orc_mp_euler_refine = 1;   /* 64: Euler's (M + h B) solve with an fp32 factor and this many fp64 refinements */
+long orc_stat_nfactor = 0;   /* Newton factorizations since the last reset (statistics only) */
 
 int orc_sizeof_model(void) { return (int)sizeof(OrcModel); }
 int orc_sizeof_data(void) { return (int)sizeof(OrcData); }
@@ -746,7 +756,8 @@ static void solve_newton(const OrcModel* m, OrcData* d) {
   memcpy(x, cs < cw ? d->qacc_smooth : d->qacc_warmstart, sizeof(double) * nv);
   double cost = eval_cost(m, d, x, jar);
   double scale = 1.0 / (m->meaninertia * (nv > 1 ? nv : 1));
-  int it;
+  const int mp_refine = orc_variant & 16;
+  int it, refine = 0;
   for (it = 0; it < m->iterations; it++) {
     unsigned char act[OMAXEFC];
     for (int r = 0; r < ne; r++) act[r] = jar[r] < 0;
@@ -757,7 +768,7 @@ static void solve_newton(const OrcModel* m, OrcData* d) {
       g[i] = t;
     }
     ORC_SUBSTAGE(ST_SOLVER_HESS);
-    memcpy(H, d->qM, sizeof H);
+    if (!refine) memcpy(H, d->qM, sizeof H);
     for (int r = 0; r < ne; r++) {
       if (!act[r]) continue;
       double Dr = d->efc_D[r], *Jr = d->efc_J[r];
@@ -765,17 +776,23 @@ static void solve_newton(const OrcModel* m, OrcData* d) {
         ORC_SUBSTAGE(ST_SOLVER);
         g[i] += Dr * jar[r] * Jr[i];
         ORC_SUBSTAGE(ST_SOLVER_HESS);
-        if (Jr[i] == 0) continue;
+        if (refine || Jr[i] == 0) continue;
         for (int k = 0; k <= i; k++) H[i][k] += Dr * Jr[i] * Jr[k];
       }
     }
-    for (int i = 0; i < nv; i++) for (int k = i + 1; k < nv; k++) H[i][k] = H[k][i];
+    if (!refine) {
+      for (int i = 0; i < nv; i++) for (int k = 0; k <= i; k++) H[i][k] *= 1.0;   /* rounds in fp32 stages */
+      for (int i = 0; i < nv; i++) for (int k = i + 1; k < nv; k++) H[i][k] = H[k][i];
+    }
     ORC_SUBSTAGE(ST_SOLVER);
     double gn = 0;
     for (int i = 0; i < nv; i++) gn += g[i] * g[i];
-    if (scale * sqrt(gn) < 1e-14) break;
+    if (scale * sqrt(gn) < (mp_refine ? orc_mp_tol : 1e-14)) break;
     ORC_SUBSTAGE(ST_SOLVER_CHOL);
-    if (chol(L, H, nv)) break;
+    if (!refine) {
+      if (chol(L, H, nv)) break;
+      orc_stat_nfactor++;
+    }
     chol_solve(s, L, g, nv);
     for (int i = 0; i < nv; i++) s[i] = -s[i];
     ORC_SUBSTAGE(ST_SOLVER_LS);
@@ -787,6 +804,11 @@ static void solve_newton(const OrcModel* m, OrcData* d) {
     for (int r = 0; r < ne; r++) if ((jar[r] < 0) != act[r]) { same = 0; break; }
     double improvement = cost - newcost;
     cost = newcost;
+    if (mp_refine) {                              /* preconditioned: only the gradient test ends it */
+      refine = same;
+      if (scale * improvement < 1e-16 && same) { it++; break; }
+      continue;
+    }
     if (same || scale * improvement < 1e-16) { it++; break; }
     if (orc_variant & 8) {                        /* MuJoCo's stop: improvement or gradient below tol */
       double g2 = 0;
@@ -917,8 +939,29 @@ static void euler(const OrcModel* m, OrcData* d) {
   if (!(orc_variant & 2))
     for (int i = 0; i < nv; i++) H[i][i] += h * m->dof_damping[i];
   for (int i = 0; i < nv; i++) f[i] = d->qfrc_smooth[i] + d->qfrc_constraint[i];
-  chol(L, H, nv);
-  chol_solve(a, L, f, nv);
+  if (orc_variant & 64) {                         /* fp32 factor + orc_mp_euler_refine fp64 refinements */
+    static double Hf[OMAXV][OMAXV];
+    ORC_SUBSTAGE(ST_SOLVER_CHOL);
+    for (int i = 0; i < nv; i++) for (int k = 0; k < nv; k++) Hf[i][k] = H[i][k] * 1.0;
+    chol(L, Hf, nv);
+    chol_solve(a, L, f, nv);
+    ORC_SUBSTAGE(ST_EULER);
+    for (int r = 0; r < orc_mp_euler_refine; r++) {
+      double res[OMAXV], da[OMAXV];
+      for (int i = 0; i < nv; i++) {
+        double t = f[i];
+        for (int k = 0; k < nv; k++) t -= H[i][k] * a[k];
+        res[i] = t;
+      }
+      ORC_SUBSTAGE(ST_SOLVER_CHOL);
+      chol_solve(da, L, res, nv);
+      ORC_SUBSTAGE(ST_EULER);
+      for (int i = 0; i < nv; i++) a[i] += da[i];
+    }
+  } else {
+    chol(L, H, nv);
+    chol_solve(a, L, f, nv);
+  }
   for (int i = 0; i < nv; i++) d->qvel[i] += h * a[i];
   for (int j = 0; j < m->njnt; j++) {             /* mj_integratePos */
     int qa = m->jnt_qposadr[j], da = m->jnt_dofadr[j];

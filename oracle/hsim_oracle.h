@@ -88,6 +88,9 @@ void orc_forward(const OrcModel* m, OrcData* d);
 void orc_step(const OrcModel* m, OrcData* d);
 void orc_step_n(const OrcModel* m, OrcData* d, const double* ctrl, int nsub);
 extern int orc_variant;   /* known-wrong physics switches (hsim_oracle.c), 0 = the restatement */
+extern double orc_mp_tol;          /* gradient stop of the mixed-precision Newton variant (16) */
+extern long orc_stat_nfactor;      /* Newton factorizations so far (statistics) */
+extern int orc_mp_euler_refine;    /* refinements of the fp32-factored Euler solve (variant 64) */
 /* full-state option: after mj_forward, the contact part of mj_rnePostConstraint (cfrc_ext) and
  * mj_subtreeVel (subtree_linvel), i.e. what MuJoCo computes when those fields are requested;
  * the reference never requests them (zeros), so this is hsim's opt-in "full_state" mode. */
