@@ -488,3 +488,24 @@ def test_precision_emulation_build_mask0_is_the_oracle_bitwise():
     P.set_mask(0)
     d = np.abs(a.qvel - b.qvel).max()
     assert 0 < d < 1e-2 * (1 + np.abs(a.qvel).max())       # fp32 arithmetic: close, not equal
+
+
+def test_mixed_precision_newton_gate_fails():
+    """The round-5 CPU gate for an fp32 Hessian / Cholesky / triangular-solve Newton under fp64
+    state, gradient and line search (tools/probes/mixed_newton_gate.py, profiles/mixed_newton_r5.md):
+    the fp32 factor with the exact-active-set stop leaves the zero tape above 1e-6 (contact flips),
+    and as a preconditioner it needs more than one extra Newton iteration per substep to reach the
+    kernel's 1e-13 stop.  So the kernel keeps its fp64 solve."""
+    import mixed_newton_gate as G
+    from oracle import precision as P
+    o = P.PrecOracle(XML)
+    HC = P.mask_of(["solver_hessian", "solver_cholesky"])
+    q, v, rng = G.initial(o.M, 4)
+    zero = np.zeros((G.NSUB, 21), np.float32)
+    ref, it0, _ = G.run(o, q, v, zero, (0, 0))
+    norefine, it1, _ = G.run(o, q, v, zero, (HC, 0))
+    refine, it2, nf2 = G.run(o, q, v, zero, (HC, 16, 1e-13))
+    assert np.abs(norefine - ref).max() > 1e-6
+    assert np.abs(refine - ref).max() < 1e-8
+    assert abs(it1 - it0) < 0.1 and abs(nf2 - it0) < 0.1      # same factorizations as the exact solve
+    assert it2 - it0 > 1.0                                    # ... plus more than one refinement each
