@@ -186,6 +186,8 @@ def main():
     ap.add_argument("--no-fp32", action="store_true", help="skip the fp32 sim-only leg")
     ap.add_argument("--no-tape", action="store_true", help="skip the open-loop tape leg (hs_step_tape)")
     ap.add_argument("--no-episodes", action="store_true", help="skip the full-episode T0/T1/T2 legs")
+    ap.add_argument("--no-dropin", action="store_true",
+                    help="skip the drop-in leg (SB3 VecEnv step_async/step_wait in numpy mode, HumanoidEnv.step)")
     ap.add_argument("--no-precondition", action="store_true",
                     help="time from a synchronized reset (standing humanoids only) instead of the staggered mix")
     ap.add_argument("--free-groups", type=int, default=0, help="extra sim-only leg: this many free-running stream "
@@ -482,6 +484,58 @@ def main():
                                         "env kernel, one launch per rollout), per_step = one HIP graph of per-step "
                                         "launches")
 
+    # ---- drop-in leg: the north star's unchanged call sites (train_sb3.py:203 SubprocVecEnv ->
+    # HumanoidVecEnv, numpy actions in, numpy obs / rewards / dones / infos out; custom_env.py:152-230
+    # HumanoidEnv.step for one env), PCIe-inclusive
+    dropin = None
+    if not args.no_dropin:
+        from mujocoposelearning_amd.env import HumanoidEnv
+        dropin = {}
+        rng_np = np.random.default_rng(3 + rank)
+        for n_x, ks in ((8, 200), (n, 30)):
+            e = make_env(args.precision, 9000, n_x=n_x)
+            precondition(e, tape[:, :n_x])
+            acts_np = rng_np.uniform(-1, 1, (ks + 5, n_x, model.nu)).astype(np.float32)
+            for k in range(5):
+                e.step_async(acts_np[k])
+                e.step_wait()
+            res = {}
+            for consume in (False, True):
+                barrier()
+                t0 = time.perf_counter()
+                for k in range(ks):
+                    e.step_async(acts_np[k % ks])
+                    obs_, rew_, done_, infos_ = e.step_wait()
+                    if consume:      # SB3 collect_rollouts' per-step reads (_update_info_buffer, TimeLimit bootstrap)
+                        for i, info in enumerate(infos_):
+                            info.get("episode")
+                            if done_[i] and info.get("terminal_observation") is not None:
+                                info.get("TimeLimit.truncated", False)
+                barrier()
+                el = max_over_ranks(time.perf_counter() - t0)
+                res["with_sb3_info_reads" if consume else "step_wait"] = dict(
+                    value=n_x * ks * ranks / el, unit="env_steps/s", ms_per_step=el / ks * 1e3)
+            dropin[f"vec_env_{n_x}"] = dict(n_envs_per_gpu=n_x, steps=ks, **res)
+            e.close()
+        he = HumanoidEnv({"model_path": XML, "duration": DURATION, "reward_config": {"type": "stand"},
+                          "frame_skip": FRAME_SKIP, "device": dev_index, "precision": args.precision})
+        ha = rng_np.uniform(-1, 1, (300, model.nu)).astype(np.float32)
+        for k in range(20):
+            he.step(ha[k])
+        t0 = time.perf_counter()
+        for k in range(200):
+            _, _, term_, trunc_, _ = he.step(ha[20 + k])
+            if term_ or trunc_:
+                he.reset()
+        hl = (time.perf_counter() - t0) / 200
+        he.close()
+        dropin["humanoid_env_step"] = dict(ms_per_step=hl * 1e3, value=1.0 / hl, unit="env_steps/s", n_envs=1)
+        dropin["note"] = ("numpy surfaces of the reference's call sites, PCIe-inclusive: HumanoidVecEnv.step_async / "
+                          "step_wait (SB3 VecEnv API, SubprocVecEnv semantics; obs / rewards / dones / final-step info "
+                          "in one packed pinned copy, infos built lazily) at configs[0]'s 8 envs and configs[1]'s "
+                          "4096, from staggered episode clocks; with_sb3_info_reads also touches every info as SB3's "
+                          "collect_rollouts does; humanoid_env_step: the single-env Gym step() latency")
+
     # ---- extra sim-only leg: free-running stream groups (opt-in)
     grouped = None
     if args.free_groups > 1:
@@ -661,6 +715,11 @@ def main():
                          "schedule": ("chunk queue: persistent grid of resident waves, two items per env step "
                                       "(DESIGN.md 3.1)" if queued else "one wave per env pair"),
                          "algo_bytes_per_env_step": abytes, "valu_busy": issue, "valu_flops": vflops,
+                         # flat copies of the nested figures (the driver's record keeps flat keys only)
+                         "valu_flops_frac": vflops["frac"] if vflops else None,
+                         "valu_busy_frac": issue["frac"] if issue else None,
+                         "wait_frac": issue["wait_frac"] if issue else None,
+                         "traffic_over_algo": traffic / (abytes * n) if traffic else None,
                          "note": "latency-bound kernel (see valu_busy and DESIGN.md 3.1); HBM fraction reported per "
                                  "BASELINE.json; HIP events over the timed steps on the launch stream (the step "
                                  "kernel + the wide-tier launch, which exits at once when no env overflowed)"},
@@ -673,6 +732,7 @@ def main():
             "gae": gae_res,
             "sim_only_stream_groups": grouped,
             "sim_only_tape": tape_leg,
+            "dropin": dropin,
             "other_configs": config_legs,
         }
         print(json.dumps(out))

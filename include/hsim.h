@@ -44,10 +44,12 @@
  * model is immutable and shareable; a batch owns (or is bound to) device buffers; every call
  * takes an optional HIP stream (NULL = default stream) and is asynchronous unless noted; a
  * batch is not re-entrant.  No torch types cross this boundary.
- * Launches of ONE batch (hs_reset / hs_step / hs_physics_step) must be ordered: issue them on one
- * stream, or order the streams (event wait).  Like one mjData, a batch is a single state: two
- * unordered launches race on every buffer, and on the chunk-queue schedule they also share the
- * batch's claim counters and cost-ordered claim lists, so pairs could be stepped twice or skipped.
+ * Launches of ONE batch are ordered by the library: like one mjData, a batch is a single state (two
+ * unordered launches would race on every buffer, and on the chunk-queue schedule share the batch's
+ * claim counters, so pairs could be stepped twice or skipped).  A call on another stream than the
+ * batch's previous call first makes its stream wait for everything already issued on the old one
+ * (an event; counted by hs_stream_orders).  Streams in graph capture are not joined this way: the
+ * capturing framework orders a capture against its origin stream.
  */
 #ifndef HSIM_H
 #define HSIM_H
@@ -69,7 +71,12 @@ enum { HS_FP32 = 0, HS_FP64 = 1 };
  * read the real foot forces / com velocity.  Off (default) = the reference's zeros. */
 enum { HS_FULL_STATE = 0x100 };
 enum { HS_REWARD_NONE = -1, HS_REWARD_STAND = 0, HS_REWARD_KNEELING = 1, HS_REWARD_WALK = 2 };
-enum { HS_WARN_BADQPOS = 0, HS_WARN_BADQVEL = 1, HS_WARN_BADQACC = 2, HS_WARN_OVERFLOW = 3, HS_NWARN = 4 };
+/* Per-env warning counters (hs_buffers.warning): MuJoCo's mj_checkPos / mj_checkVel / mj_checkAcc
+ * resets (mj_step's mju_warning + mj_resetData, custom_env.py:160), contacts dropped past the wide
+ * tier, and HS_WARN_HANDOFF: a lost chunk-queue hand-off (a scheduling failure -- e.g. more concurrent
+ * queued batches than the GPU holds -- after which the env was reset like a bad state). */
+enum { HS_WARN_BADQPOS = 0, HS_WARN_BADQVEL = 1, HS_WARN_BADQACC = 2, HS_WARN_OVERFLOW = 3, HS_WARN_HANDOFF = 4,
+       HS_NWARN = 5 };
 #define HS_AUXDIM 40   /* per env aux row: qacc[32], com[3], ncon, nefc, newton iterations, pad */
 /* Optional per-env outputs (hs_env_config.outputs).  HS_OUT_AUX: the aux row (qacc, subtree com,
  * contact / row counts, solver iterations) that data views and statistics read.  HS_OUT_CTRL: the
@@ -183,12 +190,15 @@ typedef struct hs_tape_out {
  * does not end every step on its slowest pair.  out = NULL: only the batch's buffers (last step);
  * otherwise every step's outputs, and the batch buffers as after the last step.  If an env overflows
  * the resident contact tier the launch stops and the tape is replayed step by step (counted by
- * hs_tape_aborts).  Synchronizes the stream.  1 <= K <= 511.  With HS_SCHED_DIRECT / SINGLE, or
+ * hs_tape_aborts).  Synchronizes the stream.  K >= 1: the host splits the tape into launches of at
+ * most min(the shortest episode, 511) steps (hs_rollout_max_steps).  With HS_SCHED_DIRECT / SINGLE, or
  * K = 1, it runs the K hs_step calls.  Open-loop stepping (a given action tape: benchmarks,
  * trajectory evaluation); a policy in the loop steps with hs_step. */
 int hs_step_tape(hs_batch* b, const float* actions, int n_steps, const hs_tape_out* out, void* stream);
 /* tape launches of this batch that were replayed step by step (resident-tier overflow) */
 int hs_tape_aborts(const hs_batch* b, uint64_t* n);
+/* cross-stream waits the library inserted to keep this batch's launches ordered (diagnostics) */
+int hs_stream_orders(const hs_batch* b, uint64_t* n);
 
 /* Fused PPO rollout (the fp64 Newton engine).  The SB3 MlpPolicy's pi net -- two hidden layers of
  * 256, ReLU, then the action head, fp32 -- with [in][out] row-major weights (w1 [obs_dim][ld1],
@@ -230,7 +240,7 @@ typedef struct hs_rollout_bufs {
  * next obs row, episode_start) -- on each env's wave, each env pair's step t + 1 starting when its
  * own step t is done.  Replaces the per-step loop of SB3 collect_rollouts (train_sb3.py:229 ->
  * on_policy_algorithm.py) for envs stepped by this engine; values are evaluated after the rollout.
- * n_steps <= hs_rollout_max_steps(b) (the shortest episode).  Returns 0, or 1 when an env overflowed
+ * n_steps <= hs_rollout_max_steps(b) (the shortest episode, at most 511 steps).  Returns 0, or 1 when an env overflowed
  * the resident contact tier: the env state, ep_acc, episode_start and actions_clipped are restored
  * to the call's start, and the caller collects these steps step by step (hs_step).  Synchronizes. */
 int hs_rollout(hs_batch* b, const hs_policy* pol, const hs_rollout_bufs* rb, int t_begin, int n_steps, int t_total,
@@ -250,9 +260,9 @@ int hs_set_autoreset_noise(hs_batch* b, const void* qpos_noise, const void* qvel
  * hs_physics_step(ctrl = NULL) and an hs_state_io get of ctrl fail instead of using it. */
 int hs_physics_step(hs_batch* b, const float* ctrl, int nsub, void* stream);
 /* Test hook of the chunk-queue schedule (never used on the product path): from the next launch on,
- * the hand-off of env `env`'s pair (env / 2) is treated as lost by its last-substep item, exactly as
- * if its bounded wait had timed out -- the env is poisoned (qpos[2] = NaN), so mj_checkPos resets it
- * (MuJoCo's warning path: HS_WARN_BADQPOS += 1, qpos0, time 0) and the step continues from there.
+ * the hand-off of env `env`'s pair (env / 2) is treated as lost by its consumer item, exactly as
+ * if its bounded wait had timed out -- both envs of the pair are reset as mj_checkPos resets a bad
+ * state (qpos0, qvel 0, time 0), HS_WARN_HANDOFF += 1, and the step continues from there.
  * env = -1 turns it off.  Only launches on the queued schedule consult it. */
 int hs_debug_lose_handoff(hs_batch* b, int env);
 

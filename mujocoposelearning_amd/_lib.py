@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("HSIM_LIB", os.path.join(HERE, "libhsim.so"))   # HSIM
 HS_FP32, HS_FP64 = 0, 1
 HS_FULL_STATE = 0x100      # OR-ed into hs_batch_create's precision: cfrc_ext / subtree_linvel + 448-dim obs
 HS_REWARD_NONE, HS_REWARD_STAND, HS_REWARD_KNEELING, HS_REWARD_WALK = -1, 0, 1, 2
-HS_NWARN = 4
+HS_NWARN = 5
 HS_AUXDIM = 40
 HS_OUT_AUX, HS_OUT_CTRL = 1, 2   # hs_env_config.outputs bits
 HS_SCHED_AUTO, HS_SCHED_DIRECT, HS_SCHED_SINGLE, HS_SCHED_FIXED_ORDER = 0, 1, 2, 3   # hs_env_config.schedule
@@ -92,6 +92,7 @@ def lib():
         "hs_step": (i, [vp, vp, vp]),
         "hs_step_tape": (i, [vp, vp, i, vp, vp]),
         "hs_tape_aborts": (i, [vp, vp]),
+        "hs_stream_orders": (i, [vp, vp]),
         "hs_rollout": (i, [vp, vp, vp, i, i, i, vp]),
         "hs_rollout_max_steps": (i, [vp]),
         "hs_set_autoreset_noise": (i, [vp, vp, vp]),
@@ -132,7 +133,7 @@ def lib():
 
 
 EXPORTED = ("hs_model_load", "hs_model_free", "hs_model_field", "hs_batch_create", "hs_batch_destroy",
-            "hs_batch_get_info", "hs_get_buffers", "hs_set_config", "hs_set_seed", "hs_get_config", "hs_reset", "hs_step", "hs_step_tape", "hs_tape_aborts", "hs_rollout", "hs_rollout_max_steps", "hs_set_autoreset_noise",
+            "hs_batch_get_info", "hs_get_buffers", "hs_set_config", "hs_set_seed", "hs_get_config", "hs_reset", "hs_step", "hs_step_tape", "hs_tape_aborts", "hs_stream_orders", "hs_rollout", "hs_rollout_max_steps", "hs_set_autoreset_noise",
             "hs_physics_step", "hs_state_io", "hs_kinematics", "hs_set_debug", "hs_debug_lose_handoff", "hs_get_debug", "hs_synchronize", "hs_batch_counters", "hs_gae",
             "hs_ppo_act", "hs_ppo_post", "hs_gauss_logp", "hs_gauss_logp_grad",
             "hs_ppo_loss_workspace", "hs_ppo_loss", "hs_ppo_loss_grad", "hs_adam_workspace", "hs_adam_clip",

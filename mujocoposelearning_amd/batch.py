@@ -274,11 +274,48 @@ class HsBatch:
             return res
         return self.t["obs"], self.t["reward"], self.t["terminated"], self.t["truncated"]
 
+    # -- host copies of a step's outputs (the Gym / SB3 numpy surfaces) ----------------------
+    _HOST_COLS = ("reward", "terminated", "truncated", "total_reward", "step_count", "terminal_step_count",
+                  "terminal_total_reward")
+
+    def host_outputs(self, ncols=3):
+        """One step's outputs on the host in ONE device-to-host copy: the obs and the first ``ncols``
+        of (reward, terminated, truncated, total_reward, step_count, terminal_step_count,
+        terminal_total_reward), packed on the device into one float64 buffer, copied into pinned
+        host memory and synchronized once.  Returns (obs [N, obs_dim] float64, cols [ncols, N]
+        float64), views of a fresh pinned block (torch's caching host allocator recycles it once
+        both are dropped)."""
+        torch = _torch()
+        N, D = self.n, self.obs_dim
+        size = N * D + ncols * N
+        dev = self.__dict__.get("_pack_dev")
+        if dev is None or dev.numel() != size:
+            dev = self._pack_dev = torch.empty(size, dtype=torch.float64, device=self.device)
+        dev[:N * D].view(N, D).copy_(self.t["obs"])
+        cols = dev[N * D:].view(ncols, N)
+        for k in range(ncols):
+            cols[k].copy_(self.t[self._HOST_COLS[k]])
+        host = torch.empty(size, dtype=torch.float64, pin_memory=True)
+        host.copy_(dev, non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
+        a = host.numpy()
+        return a[:N * D].reshape(N, D), a[N * D:].reshape(ncols, N)
+
     def tape_aborts(self):
         """Tape launches replayed step by step because an env overflowed the resident tier."""
         v = C.c_uint64(0)
         check(lib().hs_tape_aborts(self._groups[0][0], C.byref(v)))
         return int(v.value)
+
+    def stream_orders(self):
+        """Cross-stream waits the library inserted because calls of this batch came on different
+        streams (include/hsim.h: one batch's launches are always ordered)."""
+        tot = 0
+        for h, _, _ in self._groups:
+            v = C.c_uint64(0)
+            check(lib().hs_stream_orders(h, C.byref(v)))
+            tot += int(v.value)
+        return tot
 
     def physics_step(self, ctrl=None, nsub=1):
         """nsub raw mj_step's with the given ctrl [N, nu] (None keeps the current ctrl)."""
@@ -344,7 +381,8 @@ class HsBatch:
 
     def debug_lose_handoff(self, env):
         """Test hook (hs_debug_lose_handoff): the chunk-queue hand-off of ``env``'s pair is treated
-        as lost in the following queued launches (the env is poisoned and mj_checkPos resets it);
+        as lost in the following queued launches (the pair is reset as mj_checkPos resets a bad state
+        and counted in the HS_WARN_HANDOFF column of ``warning``);
         ``env=None`` turns it off."""
         for h, lo, hi in self._groups:
             inside = env is not None and lo <= int(env) < hi

@@ -39,6 +39,10 @@ struct hs_batch {
   void* tape_backup = nullptr;               // hs_step_tape / hs_rollout: the state before a tape launch (replay on abort)
   size_t tape_backup_bytes = 0;
   unsigned long long tape_aborts = 0;        // tape launches replayed step by step (resident-tier overflow)
+  hipStream_t last_stream = nullptr;         // stream of the batch's previous launch (order_streams)
+  bool last_valid = false;
+  hipEvent_t order_ev = nullptr;
+  unsigned long long stream_orders = 0;      // cross-stream waits inserted (diagnostics)
 };
 
 namespace {
@@ -68,41 +72,68 @@ struct DeviceGuard {
 
 // Uncached device memory (the chunk queue's hand-off rows, claim / exit / epoch words and pair
 // flags) is recycled only as uncached memory: freed blocks go to a per-device list instead of
-// hipFree.  Round-3 finding: after a batch was destroyed, its hipFree'd UNCACHED hand-off rows were
-// handed back out as ordinary memory -- torch tensors of the next batch -- and a few hundred obs rows
-// of that batch intermittently read back stale values (tests/gpu_queue_wide_probe.py: 3 of 3 runs
-// before, none after); keeping UC memory out of the general pool removes that path.
+// hipFree, for the life of the process.  Round-3 finding: after a batch was destroyed, its hipFree'd
+// UNCACHED hand-off rows were handed back out as ordinary memory -- torch tensors of the next batch --
+// and a few hundred obs rows of that batch intermittently read back stale values
+// (tools/probes/gpu_queue_wide_probe.py: 3 of 3 runs before, none after); keeping UC memory out of the
+// general pool removes that path.  Sizes are rounded up to a power of two (>= 64 KB), and a request
+// takes a free block of exactly its size class, so batches of any mix of sizes reuse blocks and the
+// pool holds at most the peak of concurrently live uncached memory per class -- it never has to
+// give a block back (a bounded list did, round 4, and re-opened the hazard for workloads with many
+// batch sizes).
 struct UcBlock { int device; size_t bytes; void* ptr; };
 std::mutex g_uc_mu;
 std::vector<UcBlock> g_uc_free;
 
+size_t uc_class(size_t bytes) {
+  size_t c = (size_t)64 << 10;
+  while (c < bytes) c <<= 1;
+  return c;
+}
+
 bool uc_alloc(int device, size_t bytes, void** out) {
+  const size_t cls = uc_class(bytes);
   {
     std::lock_guard<std::mutex> lk(g_uc_mu);
     for (size_t i = 0; i < g_uc_free.size(); i++)
-      if (g_uc_free[i].device == device && g_uc_free[i].bytes >= bytes && g_uc_free[i].bytes <= 2 * bytes + 4096) {
+      if (g_uc_free[i].device == device && g_uc_free[i].bytes == cls) {
         *out = g_uc_free[i].ptr;
         g_uc_free.erase(g_uc_free.begin() + (long)i);
         return true;
       }
   }
-  return hipExtMallocWithFlags(out, bytes, hipDeviceMallocUncached) == hipSuccess;
+  return hipExtMallocWithFlags(out, cls, hipDeviceMallocUncached) == hipSuccess;
 }
 
-// The free list is bounded: past kUcKeep blocks the oldest block goes back to the runtime (the
-// stale-obs path above needs a UC block to be handed out again as cached memory while this process
-// still steps batches; a bounded list keeps the common create/destroy cycles inside the pool).
-constexpr size_t kUcKeep = 64;
 void uc_release(int device, size_t bytes, void* ptr) {
   if (!ptr) return;
   std::lock_guard<std::mutex> lk(g_uc_mu);
-  g_uc_free.push_back({device, bytes, ptr});
-  if (g_uc_free.size() > kUcKeep) {
-    DeviceGuard g(g_uc_free.front().device);
-    (void)hipDeviceSynchronize();
-    (void)hipFree(g_uc_free.front().ptr);
-    g_uc_free.erase(g_uc_free.begin());
+  g_uc_free.push_back({device, uc_class(bytes), ptr});
+}
+
+// Launches of one batch are ordered across streams (include/hsim.h): when a call comes on another
+// stream than the batch's previous one, the new stream first waits for everything issued on the old
+// one (an event recorded there now).  Streams in graph capture are left alone -- the capturing
+// framework orders the capture against the streams it forked from, and an event recorded outside a
+// capture cannot be waited on inside it.
+int order_streams(hs_batch* b, hipStream_t st) {
+  if (b->last_valid && st != b->last_stream) {
+    hipStreamCaptureStatus cn = hipStreamCaptureStatusNone, co = hipStreamCaptureStatusNone;
+    if (!hip_ok(hipStreamIsCapturing(st, &cn), "hipStreamIsCapturing") ||
+        !hip_ok(hipStreamIsCapturing(b->last_stream, &co), "hipStreamIsCapturing"))
+      return -1;
+    if (cn == hipStreamCaptureStatusNone && co == hipStreamCaptureStatusNone) {
+      if (!b->order_ev && !hip_ok(hipEventCreateWithFlags(&b->order_ev, hipEventDisableTiming), "hipEventCreate"))
+        return -1;
+      if (!hip_ok(hipEventRecord(b->order_ev, b->last_stream), "stream order (record)") ||
+          !hip_ok(hipStreamWaitEvent(st, b->order_ev, 0), "stream order (wait)"))
+        return -1;
+      b->stream_orders++;
+    }
   }
+  b->last_stream = st;
+  b->last_valid = true;
+  return 0;
 }
 
 int obs_dim_of(const hs::HostModel& m) { return (m.nq - 2) + m.nv + 10 * m.nbody + 6 * m.nbody + m.nv; }
@@ -163,6 +194,7 @@ int launch(hs_batch* b, int mode, const float* act, const uint8_t* mask, const v
            void* stream, int nsteps = 1, const hs_tape_out* tape = nullptr, const hs::RolloutArgs* ro = nullptr) {
   if (!b) return fail("null batch");
   DeviceGuard g(b->device);
+  if (order_streams(b, (hipStream_t)stream)) return -1;
   hipError_t e;
   auto p = params_of(b, mode, nsub);
   p.nsteps = nsteps;
@@ -473,6 +505,7 @@ void hs_batch_destroy(hs_batch* b) {
   if (b->mid) uc_release(b->device, (size_t)b->n * hs::MIDDIM * (b->precision == HS_FP64 ? 8 : 4), b->mid);
   if (b->qsync) uc_release(b->device, hs::qsync_words(b->n) * sizeof(int), b->qsync);
   if (b->tape_backup) (void)hipFree(b->tape_backup);
+  if (b->order_ev) (void)hipEventDestroy(b->order_ev);
   delete b;
 }
 
@@ -550,11 +583,11 @@ int hs_step(hs_batch* b, const float* actions, void* stream) {
 int hs_step_tape(hs_batch* b, const float* actions, int n_steps, const hs_tape_out* out, void* stream) {
   if (!b) return fail("null batch");
   if (!actions) return fail("hs_step_tape: actions must not be NULL");
-  if (n_steps < 1 || n_steps > hs::QTAG_STEPS)
-    return fail("hs_step_tape: n_steps must be in [1, " + std::to_string(hs::QTAG_STEPS) + "]");
+  if (n_steps < 1) return fail("hs_step_tape: n_steps must be >= 1");
   if (out && (!out->obs || !out->reward || !out->terminated || !out->truncated))
     return fail("hs_step_tape: pass all four per-step output arrays, or out = NULL");
   DeviceGuard g(b->device);
+  if (order_streams(b, (hipStream_t)stream)) return -1;
   const auto& h = b->model->host;
   const size_t N = (size_t)b->n, es = b->precision == HS_FP64 ? 8 : 4, nu = (size_t)h.nu;
   hipStream_t st = (hipStream_t)stream;
@@ -585,7 +618,8 @@ int hs_step_tape(hs_batch* b, const float* actions, int n_steps, const hs_tape_o
   // without auto-reset a finished env keeps rewriting its terminal info every step (one launch
   // must write each batch address once, see hs_kernels.hip step_pair): step by step
   if (n_steps == 1 || !tape_sched || !b->cfg.autoreset || resident <= 0 || !b->mid || !b->qsync) return per_step();
-  const int min_len = min_episode_len(b);
+  // one launch covers at most the shortest episode and at most QTAG_STEPS steps (its hand-off tags)
+  const int min_len = std::min(min_episode_len(b), hs::QTAG_STEPS);
   if (n_steps > min_len) {
     for (int t0 = 0; t0 < n_steps; t0 += min_len) {
       const int k = std::min(min_len, n_steps - t0);
@@ -628,7 +662,7 @@ int hs_step_tape(hs_batch* b, const float* actions, int n_steps, const hs_tape_o
 
 int hs_rollout_max_steps(const hs_batch* b) {
   if (!b) return fail("null batch");
-  return min_episode_len(b);
+  return std::min(min_episode_len(b), hs::QTAG_STEPS);
 }
 
 int hs_rollout(hs_batch* b, const hs_policy* pol, const hs_rollout_bufs* rb, int t_begin, int n_steps, int t_total,
@@ -660,6 +694,7 @@ int hs_rollout(hs_batch* b, const hs_policy* pol, const hs_rollout_bufs* rb, int
                         (const void*)rb->counter_base})
     if (!q) return fail("hs_rollout: every policy weight and rollout buffer must be given");
   DeviceGuard g(b->device);
+  if (order_streams(b, (hipStream_t)stream)) return -1;
   const int resident = hs::resident_waves<double>(false);
   if (resident <= 0 || !b->mid || !b->qsync) return fail("hs_rollout: no resident-wave count / queue buffers");
   hs::RolloutArgs ro{};
@@ -939,6 +974,12 @@ int hs_batch_counters(const hs_batch* b, uint64_t* wide_reruns) {
 int hs_tape_aborts(const hs_batch* b, uint64_t* n) {
   if (!b || !n) return fail("null argument");
   *n = b->tape_aborts;
+  return 0;
+}
+
+int hs_stream_orders(const hs_batch* b, uint64_t* n) {
+  if (!b || !n) return fail("null argument");
+  *n = b->stream_orders;
   return 0;
 }
 

@@ -12,10 +12,11 @@ constexpr int AUXDIM = MAXDOF + 8;   // per env: qacc[nv], com[3], ncon, nefc, n
 constexpr int DBGDIM = 32768;        // stage dump (env 0 only) for parity debugging
 // hand-off row of a queued env step (qpos, qvel, qacc_warmstart, time, warning counters, and the
 // env bookkeeping a tape launch carries from one env step to the next: step count, episode, return)
+constexpr int MID_NWARN = 5;   // == NWARN (static_assert below)
 constexpr int MID_Q = 0, MID_V = MAXQ, MID_WS = MAXQ + MAXDOF, MID_TIME = MAXQ + 2 * MAXDOF, MID_W = MID_TIME + 1;
-constexpr int MID_SC = MID_W + 4, MID_EP = MID_W + 5, MID_TOT = MID_W + 6;
+constexpr int MID_SC = MID_W + MID_NWARN, MID_EP = MID_SC + 1, MID_TOT = MID_SC + 2;
 // a fused rollout (hs_rollout) also hands over the next step's clipped action and the episode return
-constexpr int MID_ACT = MID_W + 7, MID_EPACC = MID_ACT + 32;
+constexpr int MID_ACT = MID_TOT + 1, MID_EPACC = MID_ACT + 32;
 constexpr int MIDDIM = MID_EPACC + 1;
 // chunk-queue sync words (uncached device memory): claim counter, exit counter, launch epoch,
 // per-pair flags.  A pair's flag holds the tag of the launch whose first chunk last handed its state
@@ -49,7 +50,11 @@ constexpr size_t qsync_words(int n_envs) { return qs_ord((n_envs + 1) / 2, 2); }
 
 enum StepMode { MODE_ENV_STEP = 0, MODE_RESET = 1, MODE_PHYSICS = 2 };
 enum RewardId { REWARD_NONE = -1, REWARD_STAND = 0, REWARD_KNEELING = 1, REWARD_WALK = 2 };
-enum Warn { WARN_BADQPOS = 0, WARN_BADQVEL = 1, WARN_BADQACC = 2, WARN_OVERFLOW = 3, NWARN = 4 };
+// per-env warning counters: MuJoCo's mj_checkPos / mj_checkVel / mj_checkAcc resets, contacts past the
+// wide tier, and a lost chunk-queue hand-off (a scheduling failure, not physics: the env is reset the
+// same way and the trainer raises on it)
+enum Warn { WARN_BADQPOS = 0, WARN_BADQVEL = 1, WARN_BADQACC = 2, WARN_OVERFLOW = 3, WARN_HANDOFF = 4, NWARN = 5 };
+static_assert(NWARN == MID_NWARN, "hand-off row warning slots");
 
 template <typename T>
 struct EnvBuffers {

@@ -2346,7 +2346,7 @@ __device__ __forceinline__ void commit(MPtr<T> m, KPtr<T> k, const Stepper<T, NV
 template <typename T, int NV, bool PGS, typename C, bool ROLL = false>
 __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCache<T, C>* pcache, int idx,
                                           int nidx, const int* list, int s0, int s1, int pair, bool ghost = false,
-                                          int wait_tag = 0, int set_tag = 0, int tstep = 0) {
+                                          int wait_tag = 0, int set_tag = 0, int tstep = 0, bool tape_launch = false) {
   constexpr bool WIDE = C::WIDE;
   const int lane = opaque_v(threadIdx.x);   // (no lane-derived value hoisted out of the chunk-queue loop)
   const bool up = lane >= HL;
@@ -2369,7 +2369,7 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
   const int nq = m->nq, nv = m->nv, nu = m->nu;
   Stepper<T, NV, C> st(m, s, lane);
   if (ka->b.dbg && env_id == 0 && active) st.dbg = ka->b.dbg;
-  int warn[NWARN] = {0, 0, 0, 0};
+  int warn[NWARN] = {0, 0, 0, 0, 0};
   T time, xws;
   int step_count;
   uint32_t episode;
@@ -2408,9 +2408,15 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
         if (sl < nu) act_row = row_ld(r + MID_ACT + sl);
         epacc = (double)row_ld(r + MID_EPACC);
       }
-      // never seen in practice; if it were, the state is poisoned so that mj_checkPos resets the
-      // env and counts HS_WARN_BADQPOS -- loud, like MuJoCo's warning path, never silent
-      if (lost && sl == 2) s.qpos[2] = T(NAN);
+      // never seen in practice; if it were, the state is poisoned so that the substep's mj_checkPos
+      // resets the env (mj_resetData, ctrl 0 for that substep) -- counted in its own slot,
+      // HS_WARN_HANDOFF, not as a bad state (the -1 cancels the HS_WARN_BADQPOS count the poisoned
+      // qpos draws); the trainer raises on it: loud, never silent
+      if (lost) {
+        warn[WARN_HANDOFF]++;
+        warn[WARN_BADQPOS]--;
+        if (sl == 2) s.qpos[2] = T(NAN);
+      }
     } else {
       time = ka->b.time[env_id];
       xws = (sl < nv) ? ka->b.qacc_ws[(size_t)env_id * nv + sl] : T(0);
@@ -2688,15 +2694,21 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
       }
     }
   }
-  if (tape_handoff) {   // the pair's next env step may start: rows in memory, then the flag
+  // A tape launch never runs the wide tier, so an env deferred on ANY of its steps -- the last one
+  // included, which hands nothing over -- stops the launch: the host restores the saved state and
+  // replays the tape step by step (hs_api.cpp guarded_tape).  Otherwise the pair's next env step may
+  // start: rows in memory, then the flag.
+  if (tape_handoff || tape_launch) {
     KPtr<T> k = opaque(ka);
     const bool any_deferred = __ballot(deferred) != 0;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) {
-      if (any_deferred)   // an env overflowed the resident tier: stop the whole tape launch
-        __hip_atomic_store(k->b.qsync + QS_ABORT, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else
-        __hip_atomic_store(k->b.qsync + QS_FLAG + pair, set_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tape_handoff || any_deferred) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) {
+        if (any_deferred)
+          __hip_atomic_store(k->b.qsync + QS_ABORT, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+          __hip_atomic_store(k->b.qsync + QS_FLAG + pair, set_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
 }
@@ -2800,7 +2812,7 @@ __global__ __launch_bounds__(64, 1) void step_kernel_queue(KArgs<T> /* read via 
     const int wait_tag = tape ? (t > 0 ? qtag(epoch, t - 1, 1) : 0) : (last ? qtag(epoch, 0, 0) : 0);
     const int set_tag = tape ? (t < K - 1 ? qtag(epoch, t, 1) : 0) : (last ? 0 : qtag(epoch, 0, 0));
     step_pair<T, NV, PGS, Resident<T>, ROLL>(k, smem, pcache, env, k->nenv, nullptr, s0, s1, pair, false, wait_tag,
-                                             set_tag, t);
+                                             set_tag, t, tape);
     // the pair's duration for the next launch's order: the first chunk's is kept in qcost (its
     // store trails the hand-off, but the last substep reads it ~100 us later; a stale value only
     // makes the order less exact, never the results different); a tape launch times the pair's

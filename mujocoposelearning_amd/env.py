@@ -227,21 +227,22 @@ class HumanoidEnv(Env):
         import torch
         self.step_count += 1
         a = torch.as_tensor(np.asarray(action, dtype=np.float32).reshape(1, -1), device=self._batch.device)
-        obs_t, rew_t, term_t, trunc_t = self._batch.step(a)
-        state = obs_t[0].double().cpu().numpy()
+        self._batch.step(a)
+        obs, cols = self._batch.host_outputs(ncols=3)      # obs, reward and done flags in one copy
+        state = obs[0]
         height = state[0]
-        truncated = bool(trunc_t[0].item())
+        truncated = bool(cols[2, 0])
         truncation_info = {}
         if truncated:
             truncation_info['reason'] = 'timeout'
             reward = 0.0
         else:
-            reward = float(rew_t[0].item()) if self._reward_dev is not None else self._compute_reward()
+            reward = float(cols[0, 0]) if self._reward_dev is not None else self._compute_reward()
             params = self.reward_config.get('params')
             if params is not None and self._reward_dev in (0, 2):
                 params["previous_qpos"] = self.data.qpos.copy()   # stand/walk side effect (reward_functions.py:208)
         self.total_reward += reward
-        terminated = bool(term_t[0].item())
+        terminated = bool(cols[1, 0])
         info = {
             'reward_components': getattr(self, 'reward_components', {}),
             'height': height,

@@ -728,11 +728,48 @@ class PPO:
         pg, vf = (self._g_stats / n).tolist()
         return dict(policy_loss=pg, value_loss=vf)
 
+    WARN_KINDS = ("Nan, Inf or huge value in QPOS", "Nan, Inf or huge value in QVEL",
+                  "Nan, Inf or huge value in QACC", "contacts dropped past the wide contact tier",
+                  "chunk-queue hand-off lost")
+
+    def _check_env_warnings(self):
+        """Once per rollout: the env's warning counters (include/hsim.h HS_WARN_*) since the last
+        check, summed over ranks.  Bad-state resets are reported the way MuJoCo's mj_step reports
+        them (mju_warning: the state was reset with mj_resetData and the run goes on; custom_env.py:160);
+        a lost chunk-queue hand-off is a scheduling failure, not physics, so it raises on every
+        rank.  Returns the new counts (also in ``logger["env_warnings"]``)."""
+        fn = getattr(self.env, "warning_counts", None)
+        if fn is None:
+            return None
+        tot = np.asarray(fn(), dtype=np.int64)
+        prev = getattr(self, "_warn_seen", None)
+        new = np.maximum(tot - prev, 0) if prev is not None and prev.shape == tot.shape else tot
+        self._warn_seen = tot
+        if self.world_size > 1:
+            import torch.distributed as dist
+            t = torch.as_tensor(new, dtype=torch.int64, device=self._comm_device())
+            dist.all_reduce(t)
+            new = t.cpu().numpy()
+        self._warn_new = new
+        if len(new) > 4 and new[4] > 0:
+            from ._lib import HsimError
+            raise HsimError(f"{self.WARN_KINDS[4]} in {int(new[4])} env step(s) of this rollout: a scheduling "
+                            "failure of the step kernel (e.g. more concurrent queued batches than the GPU holds "
+                            "waves for), not physics -- those envs were reset and the rollout is not valid")
+        for k in range(min(4, len(new))):
+            if new[k] > 0:
+                import warnings
+                warnings.warn(f"mj_step warning: {self.WARN_KINDS[k]} in {int(new[k])} env step(s) of this "
+                              "rollout" + (" -- those envs were reset (mj_resetData)" if k < 3 else ""),
+                              RuntimeWarning, stacklevel=3)
+        return new
+
     def learn(self, total_timesteps, callback=None, log_interval=1):
         it = 0
         while self.num_timesteps < total_timesteps:
             t0 = time.perf_counter()
             adv, ret = self.collect_rollouts()
+            warn = self._check_env_warnings()
             t1 = time.perf_counter()
             st = self.train(adv, ret)
             t2 = time.perf_counter()
@@ -740,6 +777,8 @@ class PPO:
             mean_ret = float(np.mean(self.ep_returns[-100:])) if self.ep_returns else float("nan")
             self.logger = dict(iteration=it, timesteps=self.num_timesteps, rollout_s=t1 - t0, train_s=t2 - t1,
                                ep_rew_mean=mean_ret, **st)
+            if warn is not None:
+                self.logger["env_warnings"] = [int(x) for x in warn]
             if self._agree_stop(callback is not None and callback(self) is False):
                 break
         return self

@@ -21,6 +21,7 @@ seed + i and the worker's global numpy stream continues across auto-resets).
 from __future__ import annotations
 
 import copy
+from collections.abc import Sequence
 
 import numpy as np
 
@@ -221,42 +222,50 @@ class HumanoidVecEnv(_Base):
         self._next_noise[1][t] = torch.as_tensor(vn[idx], device=self.batch.device, dtype=self.batch.dtype)
 
     def step_async(self, actions):
-        self._actions = np.asarray(actions, dtype=np.float32).reshape(self.num_envs, -1)
+        """SB3 VecEnv.step_async: the actions go to the device through a pinned staging buffer."""
+        import torch
+        a = np.asarray(actions, dtype=np.float32).reshape(self.num_envs, -1)
+        pin = getattr(self, "_act_pin", None)
+        if pin is None or tuple(pin.shape) != a.shape:
+            pin = self._act_pin = torch.empty(a.shape, dtype=torch.float32, pin_memory=True)
+            self._act_dev = torch.empty(a.shape, dtype=torch.float32, device=self.batch.device)
+        torch.cuda.current_stream(self.batch.device).synchronize()   # the previous upload has left the pinned buffer
+        pin.numpy()[...] = a
+        self._act_dev.copy_(pin, non_blocking=True)
+        self._actions = self._act_dev
 
     def step_wait(self):
+        """SB3 VecEnv.step_wait: (obs, rewards, dones, infos) as numpy with SubprocVecEnv's
+        auto-reset semantics (train_sb3.py:203; custom_env.py:216-230 info keys).  The step's
+        outputs come back in ONE packed device-to-host copy; ``infos`` is a lazy sequence whose
+        dicts are built on first access (``StepInfos``) -- equal to the per-env info dicts
+        SubprocVecEnv returns, including ``terminal_observation`` and ``TimeLimit.truncated``."""
         import torch
-        a = torch.as_tensor(self._actions, device=self.batch.device)
-        obs, rew, term, trunc = self.step_tensors(a)
-        rew = rew.clone()
-        obs_np = obs.double().cpu().numpy()
-        rew_np = rew.double().cpu().numpy()
-        term_np = term.cpu().numpy().astype(bool)
-        trunc_np = trunc.cpu().numpy().astype(bool)
+        a = self._actions
+        if not isinstance(a, torch.Tensor):
+            a = torch.as_tensor(a, device=self.batch.device)
+        self.step_tensors(a)
+        obs_np, cols = self.batch.host_outputs(ncols=7)
+        rew_np = cols[0].copy()
+        term_np, trunc_np = cols[1] != 0, cols[2] != 0
         dones = term_np | trunc_np
-        tot = self.batch.total_reward.double().cpu().numpy()
-        step_count = self.batch.step_count.cpu().numpy()
+        idx = np.flatnonzero(dones)
         term_obs = None
-        if dones.any():
+        step_count, tot = cols[4], cols[3]
+        if idx.size:
             # the finished episodes' final info (SubprocVecEnv returns the last step's info before
             # the worker resets: step_count 667 / 750, the episode's total_reward; custom_env.py:216-224)
-            term_obs = self.batch.terminal_obs.double().cpu().numpy()
-            tsc = self.batch.terminal_step_count.cpu().numpy()
-            ttr = self.batch.terminal_total_reward.double().cpu().numpy()
-            step_count = np.where(dones, tsc, step_count)
-            tot = np.where(dones, ttr, tot)
-        infos = []
-        for i in range(self.num_envs):
-            info = {"height": None, "step_count": int(step_count[i]), "truncated": bool(trunc_np[i]),
-                    "truncation_info": {"reason": "timeout"} if trunc_np[i] else {}, "terminated": bool(term_np[i]),
-                    "total_reward": float(tot[i]), "reward_components": {}}
-            if dones[i]:
-                info["terminal_observation"] = term_obs[i]
-                info["TimeLimit.truncated"] = bool(trunc_np[i] and not term_np[i])
-                info["height"] = float(term_obs[i][0])
-            else:
-                info["height"] = float(obs_np[i][0])
-            infos.append(info)
-        return obs_np, rew_np, dones, infos
+            rows = torch.as_tensor(idx, device=self.batch.device)
+            term_obs = self.batch.terminal_obs.index_select(0, rows).double().cpu().numpy()
+            step_count = np.where(dones, cols[5], step_count)
+            tot = np.where(dones, cols[6], tot)
+        return obs_np, rew_np, dones, StepInfos(obs_np, term_np, trunc_np, step_count, tot, idx, term_obs)
+
+    def warning_counts(self):
+        """The per-env warning counters (include/hsim.h HS_WARN_*: bad qpos / qvel / qacc resets,
+        contacts dropped past the wide tier, lost chunk-queue hand-offs) summed over the envs, as a
+        host int64 array -- cumulative since the batch was created."""
+        return self.batch.warning.sum(0).cpu().numpy().astype(np.int64)
 
     def close(self):
         self.batch.close()
@@ -310,6 +319,62 @@ class HumanoidVecEnv(_Base):
         if isinstance(indices, int):
             return [indices]
         return indices
+
+
+class StepInfos(Sequence):
+    """The ``infos`` of one ``step_wait``: a read-only sequence of the per-env info dicts
+    SubprocVecEnv returns (custom_env.py:216-230 keys; for a finished env also
+    ``terminal_observation`` and ``TimeLimit.truncated``), each built on first access and then kept
+    (a consumer may annotate it, as SB3's VecMonitor does with ``episode``).  Building 4096 dicts
+    eagerly costs milliseconds per step, more than the physics; consumers that read only a few
+    (or none) pay only for those."""
+
+    __slots__ = ("_h", "_term", "_trunc", "_sc", "_tot", "_pos", "_tobs", "_cache")
+
+    def __init__(self, obs, term, trunc, step_count, total, done_idx, term_obs):
+        n = len(term)
+        self._term, self._trunc = term.tolist(), trunc.tolist()
+        self._sc, self._tot = step_count.astype(np.int64).tolist(), total.tolist()
+        h = obs[:, 0].copy()
+        if done_idx.size:
+            h[done_idx] = term_obs[:, 0]
+        self._h = h.tolist()
+        self._pos = {int(i): k for k, i in enumerate(done_idx)}
+        self._tobs = term_obs
+        self._cache = [None] * n
+
+    def __len__(self):
+        return len(self._cache)
+
+    def _build(self, i):
+        tr, te = self._trunc[i], self._term[i]
+        info = {"height": self._h[i], "step_count": self._sc[i], "truncated": tr,
+                "truncation_info": {"reason": "timeout"} if tr else {}, "terminated": te,
+                "total_reward": self._tot[i], "reward_components": {}}
+        k = self._pos.get(i)
+        if k is not None:
+            info["terminal_observation"] = self._tobs[k]
+            info["TimeLimit.truncated"] = tr and not te
+        self._cache[i] = info
+        return info
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(len(self)))]
+        n = len(self._cache)
+        if i < 0:
+            i += n
+        if not 0 <= i < n:
+            raise IndexError(i)
+        info = self._cache[i]
+        return info if info is not None else self._build(i)
+
+    def __iter__(self):
+        for i in range(len(self._cache)):
+            yield self[i]
+
+    def __repr__(self):
+        return f"StepInfos({len(self)} envs)"
 
 
 def _config_of_factory(fn):

@@ -781,7 +781,9 @@ static void solve_newton(const OrcModel* m, OrcData* d) {
       }
     }
     if (!refine) {
-      for (int i = 0; i < nv; i++) for (int k = 0; k <= i; k++) H[i][k] *= 1.0;   /* rounds in fp32 stages */
+#ifdef ORC_PREC_SUBSTAGES   /* precision-emulating build: H enters the factorization rounded (fp32 stages) */
+      for (int i = 0; i < nv; i++) for (int k = 0; k <= i; k++) H[i][k] *= 1.0;
+#endif
       for (int i = 0; i < nv; i++) for (int k = i + 1; k < nv; k++) H[i][k] = H[k][i];
     }
     ORC_SUBSTAGE(ST_SOLVER);

@@ -408,3 +408,75 @@ def test_vecenv_seeded_worker_streams_match_golden(model):
         obs, _, dones, infos = venv.step_wait()
         assert dones.all() and all(inf["step_count"] == 667 for inf in infos)
     venv.close()
+
+
+def _reference_step_wait(env, actions):
+    """The round-4 step_wait (one blocking copy per field, eager info dicts), kept as the reference the
+    packed / lazy version must equal: obs, rewards, dones and every info dict."""
+    import torch
+    obs, rew, term, trunc = env.step_tensors(torch.as_tensor(actions, device=env.batch.device))
+    obs_np = obs.double().cpu().numpy()
+    rew_np = rew.double().cpu().numpy()
+    term_np = term.cpu().numpy().astype(bool)
+    trunc_np = trunc.cpu().numpy().astype(bool)
+    dones = term_np | trunc_np
+    tot = env.batch.total_reward.double().cpu().numpy()
+    step_count = env.batch.step_count.cpu().numpy()
+    term_obs = env.batch.terminal_obs.double().cpu().numpy()
+    step_count = np.where(dones, env.batch.terminal_step_count.cpu().numpy(), step_count)
+    tot = np.where(dones, env.batch.terminal_total_reward.double().cpu().numpy(), tot)
+    infos = []
+    for i in range(env.num_envs):
+        info = {"height": None, "step_count": int(step_count[i]), "truncated": bool(trunc_np[i]),
+                "truncation_info": {"reason": "timeout"} if trunc_np[i] else {}, "terminated": bool(term_np[i]),
+                "total_reward": float(tot[i]), "reward_components": {}}
+        if dones[i]:
+            info["terminal_observation"] = term_obs[i]
+            info["TimeLimit.truncated"] = bool(trunc_np[i] and not term_np[i])
+            info["height"] = float(term_obs[i][0])
+        else:
+            info["height"] = float(obs_np[i][0])
+        infos.append(info)
+    return obs_np, rew_np, dones, infos
+
+
+@pytest.mark.parametrize("prec", ["fp64", "fp32"])
+def test_vecenv_step_wait_equals_the_reference_path_on_episode_boundaries(model, prec):
+    """step_wait's packed single copy and lazy StepInfos equal the eager per-field path on steps where
+    envs terminate (time >= duration), are truncated (750 steps: TimeLimit.truncated) or run on:
+    obs, rewards, dones, and every info dict key by key, with the same Python types."""
+    from mujocoposelearning_amd.vec_env import HumanoidVecEnv
+    n = 64
+    envs = [HumanoidVecEnv(CFG, n_envs=n, model=model, seed=5, precision=prec) for _ in range(2)]
+    for e in envs:
+        e.reset()
+        st = e.batch.get_state()
+        t = st["time"].copy()
+        t[: n // 2] += 0.015 * (664 - np.arange(n // 2) % 3)      # these reach duration within 3 steps
+        e.batch.set_state(time=t)
+        e.batch.step_count[n // 2: 3 * n // 4].fill_(748)           # these hit max_steps (750)
+    rng = np.random.default_rng(1)
+    ends = set()
+    for k in range(4):
+        a = rng.uniform(-1, 1, (n, 21)).astype(np.float32)
+        envs[0].step_async(a)
+        o1, r1, d1, i1 = envs[0].step_wait()
+        o2, r2, d2, i2 = _reference_step_wait(envs[1], a)
+        np.testing.assert_array_equal(o1, o2)
+        np.testing.assert_array_equal(r1, r2)
+        np.testing.assert_array_equal(d1, d2)
+        assert len(i1) == len(i2) == n and type(d1[0]) is type(d2[0])
+        for i in range(n):
+            x, y = i1[i], i2[i]
+            assert x.keys() == y.keys(), (k, i)
+            for key in y:
+                if key == "terminal_observation":
+                    np.testing.assert_array_equal(x[key], y[key])
+                else:
+                    assert x[key] == y[key] and type(x[key]) is type(y[key]), (k, i, key, x[key], y[key])
+            if d2[i]:
+                ends.add("trunc" if y["TimeLimit.truncated"] else "term")
+        assert [a["step_count"] for a in i1[-3:]] == [b["step_count"] for b in i2[-3:]]   # slices
+    assert ends == {"trunc", "term"}
+    for e in envs:
+        e.close()

@@ -530,3 +530,34 @@ def test_fused_mlp_forward_matches_gemm_chain(N, D):
     for a, b in zip(outs[True], outs[False]):
         assert a.shape == b.shape
         assert torch.allclose(a, b, rtol=1e-4, atol=1e-4 * (1 + float(b.abs().max()))), float((a - b).abs().max())
+
+
+def test_learn_raises_on_a_lost_handoff_and_warns_on_bad_states():
+    """PPO.learn reduces the env's warning counters once per rollout (include/hsim.h HS_WARN_*): a
+    lost chunk-queue hand-off (forced with the hs_debug_lose_handoff hook on a queued 4096-env fp64
+    batch) raises, because it is a scheduling failure, not physics; before it, a bad-state reset is
+    reported as MuJoCo reports it (a warning) and training goes on."""
+    import warnings
+    from mujocoposelearning_amd._lib import HsimError
+    from mujocoposelearning_amd.model import HsModel
+    from mujocoposelearning_amd.ppo import PPO
+    from mujocoposelearning_amd.vec_env import HumanoidVecEnv
+    env = HumanoidVecEnv({"model_path": XML, "duration": 10.0, "frame_skip": 3, "reward_config": {"type": "stand"}},
+                         n_envs=4096, model=HsModel(XML), seed=0, precision="fp64")
+    ppo = PPO(env, n_steps=4, batch_size=4096, n_epochs=1, seed=0,
+              policy_kwargs={"activation_fn": "ReLU", "net_arch": {"pi": [256, 256], "vf": [256, 256]}})
+    assert env.batch.queued()
+    ppo.learn(4 * 4096)                                          # clean: no warning, counts logged
+    assert ppo.logger["env_warnings"] == [0, 0, 0, 0, 0]
+    q = env.batch.qpos
+    q[5, 2] = float("nan")                                       # a bad state: mj_checkPos resets it
+    with warnings.catch_warnings(record=True) as rec:
+        warnings.simplefilter("always")
+        ppo.learn(8 * 4096)
+    assert ppo.logger["env_warnings"][0] == 1
+    assert any("QPOS" in str(w.message) for w in rec)
+    env.batch.debug_lose_handoff(1234)
+    with pytest.raises(HsimError, match="hand-off lost"):
+        ppo.learn(12 * 4096)
+    env.batch.debug_lose_handoff(None)
+    env.close()

@@ -109,11 +109,14 @@ def test_fused_rollout_matches_env_replay_and_policy(n, T, full, duration):
     replay.close()
 
 
-def test_fused_rollout_overflow_falls_back_step_by_step():
+@pytest.mark.parametrize("T", [6, 1])
+def test_fused_rollout_overflow_falls_back_step_by_step(T):
+    """T = 1: a one-step rollout launch, whose only step is also its last (it hands nothing over):
+    the overflow must still undo the launch."""
     from oracle.oracle import Oracle
     from test_gpu_contacts import lying_states
     from mujocoposelearning_amd.ppo import PPO
-    n, T = 4096, 6
+    n = 4096
     q = np.stack(lying_states(Oracle(XML), 16, seed=11))
     idx = np.arange(16) * 255 + 7
     env, replay = _env(n), _env(n)

@@ -187,3 +187,77 @@ def test_step_tape_pgs_instance_bitwise_equals_step_loop(tmp_path):
             assert b.tape_aborts() == 0
         b.close()
     _same("pgs", outs[0], outs[1])
+
+
+def test_step_tape_overflow_on_the_last_step_replays(model, tmp_path):
+    """An env whose contacts overflow the resident tier only on the tape's LAST step (which hands
+    nothing over) must still stop the launch: the tape is replayed step by step and the results are
+    bitwise the step loop's.  Two lying humanoids under 100 g (a <option gravity> variant) land flat:
+    their contacts stay inside the tier for two env steps and pass it in the third (found with the
+    oracle; the step loop's wide-tier counter confirms it on the GPU)."""
+    import re
+    import torch
+    from mujocoposelearning_amd.batch import HsBatch
+    from mujocoposelearning_amd.model import HsModel
+    from oracle.oracle import Oracle
+    from test_gpu_contacts import lying_states
+    src = re.sub(r"<option[^>]*/>", '<option timestep="0.005" gravity="0 0 -1000"/>', open(XML).read(), count=1)
+    p = tmp_path / "heavy.xml"
+    p.write_text(src)
+    heavy, o = HsModel(str(p)), Oracle(str(p))
+    qs = lying_states(Oracle(XML), 20, seed=11)
+    q = []
+    for i in (17, 18):            # lowest geom brought to the floor, then 2 mm up
+        lo, hi = qs[i][2], qs[i][2] + 0.5
+        for _ in range(30):
+            z = 0.5 * (lo + hi)
+            o.reset_data()
+            o.qpos[:] = np.r_[qs[i][:2], z, qs[i][3:]]
+            o.forward()
+            lo, hi = (lo, z) if o.d.ncon == 0 else (z, hi)
+        q.append(np.r_[qs[i][:2], hi + 0.002, qs[i][3:]])
+    n, K = 2, 3
+    acts = torch.zeros(K + 1, n, 21, device="cuda")
+    outs, info = [], []
+    for tape in (True, False):
+        b = HsBatch(heavy, n, precision="fp64", seed=3)
+        b.configure(frame_skip=3, duration=10.0, reward_id=0, autoreset=1, max_steps=750)
+        b.reset()
+        b.set_state(qpos=np.stack(q), qvel=0.0, qacc_warmstart=0.0, time=0.005)
+        if tape:
+            per = [x.clone() for x in b.step_tape(acts[:K])]
+        else:
+            o_, r_, te_, tr_, reruns = [], [], [], [], []
+            for k in range(K):
+                b.step(acts[k])
+                o_.append(b.obs.clone()); r_.append(b.reward.clone()); te_.append(b.terminated.clone())
+                tr_.append(b.truncated.clone())
+                reruns.append(b.wide_reruns())
+            per = [torch.stack(o_), torch.stack(r_), torch.stack(te_), torch.stack(tr_)]
+            assert reruns[K - 2] == 0 and reruns[K - 1] >= 1, reruns     # overflow on the last step only
+        fin = [b.qpos.clone(), b.qvel.clone(), b.qacc_warmstart.clone(), b.time.clone(), b.warning.clone(),
+               b.step_count.clone(), b.total_reward.clone()]
+        b.step(acts[K])
+        outs.append((per, fin, [b.qpos.clone(), b.obs.clone()]))
+        info.append(b.tape_aborts())
+        b.close()
+    assert info[0] == 1, info
+    _same("per-step", outs[0][0], outs[1][0])
+    _same("final", outs[0][1], outs[1][1])
+    _same("after", outs[0][2], outs[1][2])
+
+
+def test_step_tape_longer_than_511_steps(model):
+    """A tape longer than QTAG_STEPS (511, the most steps one launch's hand-off tags can name) runs as
+    several launches (hs_step_tape splits it), bitwise the step loop: 600 steps of 64 envs with
+    episodes of 10 s (667 steps), so the 511-step limit is the one that splits it."""
+    import torch
+    n, K = 64, 600
+    g = torch.Generator(device="cuda").manual_seed(5)
+    acts = torch.rand(K + 2, n, 21, device="cuda", generator=g) * 2 - 1
+    t0 = np.zeros(n) + 0.005
+    _, fin_a, aft_a, info_a = _run(model, n, "fp64", acts, t0, True, outputs=False)
+    _, fin_b, aft_b, _ = _run(model, n, "fp64", acts, t0, False)
+    assert info_a["aborts"] == 0
+    _same("final", fin_a, fin_b)
+    _same("after", aft_a, aft_b)
