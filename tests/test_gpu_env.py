@@ -95,7 +95,7 @@ def test_full_size_determinism_and_batch_invariance(model):
     for x, y in zip(*outs):
         assert torch.equal(x, y)
     assert torch.isfinite(outs[0][2]).all()
-    assert warn == [0, 0, 0, 0]
+    assert warn == [0, 0, 0, 0, 0]
     assert int(aux[:, 35].max()) >= 1 and int(aux[:, 36].max()) >= 4      # contacts are being solved
     # batch-composition invariance
     b1 = _batch(model, 1, seed=9)

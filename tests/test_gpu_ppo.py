@@ -4,6 +4,7 @@ rollout's buffers against the policy they were sampled from.  SB3 itself is not 
 so parity with SB3 is unpinned; these pin the kernels to the torch path's formulas."""
 import math
 
+import numpy as np
 import pytest
 import torch
 
@@ -560,4 +561,31 @@ def test_learn_raises_on_a_lost_handoff_and_warns_on_bad_states():
     with pytest.raises(HsimError, match="hand-off lost"):
         ppo.learn(12 * 4096)
     env.batch.debug_lose_handoff(None)
+    env.close()
+
+
+@pytest.mark.slow
+def test_trainer_still_learns_the_stand_task():
+    """Learning regression (README.md:160-164 is the reference's one training outcome): bench.py's
+    train config -- 4096 fp64 envs, fused hs_rollout rollouts, n_steps 32, batch 32768, 4 epochs,
+    lr 3e-4, ent_coef 0, MLP[256,256] ReLU -- seed 0 for 40 M env steps (~11 s).  A humanoid that falls
+    at once scores ~18; this config reaches ~43 by 20 M on all five seeds of profiles/learning_curve_r4.md
+    (r4y), and its log_std falls (exploitation: -0.3 by 80 M).  Guards the fused rollout's sampling and
+    bookkeeping and the graphed update against silent breaks the bitwise replay tests would not see."""
+    from mujocoposelearning_amd.model import HsModel
+    from mujocoposelearning_amd.ppo import PPO
+    from mujocoposelearning_amd.vec_env import HumanoidVecEnv
+    env = HumanoidVecEnv({"model_path": XML, "duration": 10.0, "frame_skip": 3, "reward_config": {"type": "stand"}},
+                         n_envs=4096, model=HsModel(XML), seed=0, precision="fp64")
+    ppo = PPO(env, n_steps=32, batch_size=32768, n_epochs=4, learning_rate=3e-4, seed=0,
+              policy_kwargs={"activation_fn": "ReLU", "net_arch": {"pi": [256, 256], "vf": [256, 256]}})
+    ppo.policy.pack_heads()
+    assert ppo._fused_rollout_args() is not None
+    ppo.learn(40_000_000)
+    ret = float(np.mean(ppo.ep_returns[-200:]))
+    log_std = float(ppo.policy.log_std.mean())
+    print(f"40 M env steps: return {ret:.2f}, log_std {log_std:.3f}, fallbacks {getattr(ppo, 'fused_fallbacks', 0)}")
+    assert getattr(ppo, "fused_fallbacks", 0) == 0 and ppo.logger["env_warnings"][4] == 0
+    assert ret >= 35.0, ret
+    assert log_std < -0.02, log_std
     env.close()
