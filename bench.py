@@ -492,12 +492,12 @@ def main():
         from mujocoposelearning_amd.env import HumanoidEnv
         dropin = {}
         rng_np = np.random.default_rng(3 + rank)
-        for n_x, ks in ((8, 200), (n, 30)):
+        for n_x, ks in ((8, 400), (n, 30)):
             e = make_env(args.precision, 9000, n_x=n_x)
             precondition(e, tape[:, :n_x])
             acts_np = rng_np.uniform(-1, 1, (ks + 5, n_x, model.nu)).astype(np.float32)
-            for k in range(5):
-                e.step_async(acts_np[k])
+            for k in range(ks):                  # warm-up: pinned staging blocks, clocks
+                e.step_async(acts_np[k % ks])
                 e.step_wait()
             res = {}
             for consume in (False, True):

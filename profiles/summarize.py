@@ -179,10 +179,10 @@ def main(tag="r2a", precision="fp64", n_envs=4096, timed=50, src=None):
               f"- algorithmic {algo / 1e6:,.2f} MB ({algo_env} B/env step x {n_envs}); traffic/algo = "
               f"{corrected / algo:.2f}x"] + ([
               f"- chunk-queue schedule: + the hand-off of each env between its two items (qpos, qvel, warm start, "
-              f"time, 4 warning counters = 87 values written once and read once: {2 * 87 * es} B/env, "
-              f"{2 * 87 * es * n_envs / 1e6:.2f} MB/launch) through UNCACHED memory, whose 8-byte lane accesses the "
+              f"time, 5 warning counters = 88 values written once and read once: {2 * 88 * es} B/env, "
+              f"{2 * 88 * es * n_envs / 1e6:.2f} MB/launch) through UNCACHED memory, whose 8-byte lane accesses the "
               f"TCC counters report at ~4-5x (r2c: +16 MB WRITE_SIZE, +7 MB FETCH_SIZE vs the one-wave-per-pair "
-              f"kernel r2a); traffic/(algo + hand-off) = {corrected / (algo + 2 * 87 * es * n_envs):.2f}x; "
+              f"kernel r2a); traffic/(algo + hand-off) = {corrected / (algo + 2 * 88 * es * n_envs):.2f}x; "
               f"{corrected / (statistics.mean(win) * 1e-3) / 1e9:.0f} GB/s of the 8 TB/s HBM"]
               if "queue" in row["Kernel_Name"] else []) + ["",
               "## Resources", ""] + resource_lines(row["Kernel_Name"], out)
