@@ -35,7 +35,7 @@ struct hs_batch {
   int* qsync = nullptr;                      // chunk queue claim / exit counters, pair flags (qsync_words)
   hs_env_config cfg{};
   bool ctrl_stale = false;                   // env steps ran with HS_OUT_CTRL off: buf.ctrl is not data.ctrl
-  int lose_pair1 = 0;                        // hs_debug_lose_handoff test hook (pair + 1; 0 = off)
+  int lose_env1 = 0;                         // hs_debug_lose_handoff test hook (env + 1; 0 = off)
   void* tape_backup = nullptr;               // hs_step_tape / hs_rollout: the state before a tape launch (replay on abort)
   size_t tape_backup_bytes = 0;
   unsigned long long tape_aborts = 0;        // tape launches replayed step by step (resident-tier overflow)
@@ -186,7 +186,7 @@ hs::StepParams params_of(const hs_batch* b, int mode, int nsub) {
   p.solver = b->model->host.solver == 1 ? hs::SOLVER_PGS : hs::SOLVER_NEWTON;
   p.outputs = b->cfg.outputs;
   p.schedule = b->cfg.schedule;
-  p.dbg_lose_pair1 = b->lose_pair1;
+  p.dbg_lose_pair1 = b->lose_env1;          // (launch_step maps it to the queue unit)
   return p;
 }
 
@@ -724,7 +724,7 @@ int hs_rollout(hs_batch* b, const hs_policy* pol, const hs_rollout_bufs* rb, int
 int hs_debug_lose_handoff(hs_batch* b, int env) {
   if (!b) return fail("null batch");
   if (env < -1 || env >= b->n) return fail("env index out of range");
-  b->lose_pair1 = env < 0 ? 0 : env / 2 + 1;
+  b->lose_env1 = env < 0 ? 0 : env + 1;
   return 0;
 }
 

@@ -46,7 +46,9 @@ constexpr size_t qs_cnt(int npairs, int par) { return QS_FLAG + 2 * (size_t)npai
 constexpr size_t qs_ord(int npairs, int par) {
   return QS_FLAG + 2 * (size_t)npairs + 2 * QNB + (size_t)par * QNB * npairs;
 }
-constexpr size_t qsync_words(int n_envs) { return qs_ord((n_envs + 1) / 2, 2); }
+// sized for n_envs units: the queue's unit is an env pair, or one env in the single-env mode of
+// small-batch tape launches (launch_step)
+constexpr size_t qsync_words(int n_envs) { return qs_ord(n_envs, 2); }
 
 enum StepMode { MODE_ENV_STEP = 0, MODE_RESET = 1, MODE_PHYSICS = 2 };
 enum RewardId { REWARD_NONE = -1, REWARD_STAND = 0, REWARD_KNEELING = 1, REWARD_WALK = 2 };
@@ -105,8 +107,10 @@ struct StepParams {
   int queue;             // set by launch_step: 1 = chunk-queue schedule (persistent grid), 0 = one wave per pair
   int qmul;              // chunk-queue fallback claim order: item i -> pair (i * qmul) mod npairs (coprime)
   int qorder;            // chunk queue: 1 = cost-ordered claims (QNB buckets), 0 = the qmul permutation only
-  int dbg_lose_pair1;    // test hook (hs_debug_lose_handoff): pair + 1 whose hand-off is treated as lost; 0 = off
+  int dbg_lose_pair1;    // test hook (hs_debug_lose_handoff): env + 1 from the host; launch_step turns it into the
+                         // queue unit (pair or env) + 1 whose hand-off is treated as lost; 0 = off
   int single;            // set by launch_step: 1 = one env per wave (upper half-wave a ghost), 0 = env pairs
+                         // (also the chunk queue's unit for small-batch tape launches)
   int nsteps;            // env steps per launch: 1, or a tape launch of nsteps (MODE_ENV_STEP, chunk queue)
 };
 // per-step outputs of a tape launch ([nsteps][N][...] each; null: the batch's own buffers, last step wins)

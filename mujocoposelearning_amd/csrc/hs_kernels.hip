@@ -2380,7 +2380,7 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
       int seen = 0, abort = 0;
       if (lane == 0) {   // bounded (~0.5 s): a broken hand-off must not hang the GPU
         int w = 0;
-        if (pair + 1 != ka->p.dbg_lose_pair1)   // test hook: treat this pair's hand-off as lost
+        if (pair + 1 != ka->p.dbg_lose_pair1)   // test hook: treat this unit's hand-off as lost
           while ((seen = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != wait_tag &&
                  ++w < (1 << 22)) {
             // a tape launch that aborted (overflow) never hands this pair over: leave at once
@@ -2759,11 +2759,13 @@ __global__ __launch_bounds__(64, 1) void step_kernel_queue(KArgs<T> /* read via 
     __shared__ PgsCache<T, Resident<T>> pgs_smem[2];
     pcache = &pgs_smem[threadIdx.x >= HL ? 1 : 0];
   }
-  // claim order: prefix sums of the previous launch's bucket counts (qpre[QNB] == npairs: valid)
+  // claim order: prefix sums of the previous launch's bucket counts (qpre[QNB] == nunits: valid).
+  // A unit is an env pair, or one env (upper half-wave a ghost) in the single-env mode of small
+  // batches (p.single: every env gets a wave of its own)
   __shared__ int qpre[QNB + 1];
   {
-    const int npairs = (ka->nenv + 1) / 2, lane = threadIdx.x;
-    int c = (ka->p.qorder && lane < QNB) ? ka->b.qsync[qs_cnt(npairs, epoch & 1) + lane] : 0;
+    const int nunits = ka->p.single ? ka->nenv : (ka->nenv + 1) / 2, lane = threadIdx.x;
+    int c = (ka->p.qorder && lane < QNB) ? ka->b.qsync[qs_cnt(nunits, epoch & 1) + lane] : 0;
 #pragma unroll
     for (int d = 1; d < QNB; d <<= 1) {
       const int y = __shfl_up(c, d);
@@ -2775,7 +2777,8 @@ __global__ __launch_bounds__(64, 1) void step_kernel_queue(KArgs<T> /* read via 
   }
   for (;;) {
     const KPtr<T> k = opaque(ka);       // nothing uniform kept live across items
-    const int nsub = k->p.nsub, npairs = (k->nenv + 1) / 2, K = k->p.nsteps;
+    const bool single = k->p.single != 0;
+    const int nsub = k->p.nsub, npairs = single ? k->nenv : (k->nenv + 1) / 2, K = k->p.nsteps;   // (units)
     int* qs = k->b.qsync;
     int i = 0;
     if (threadIdx.x == 0) i = atomicAdd(&qs[QS_HEAD], 1);
@@ -2804,15 +2807,16 @@ __global__ __launch_bounds__(64, 1) void step_kernel_queue(KArgs<T> /* read via 
       pair = (int)((uint64_t)ii * (uint32_t)k->p.qmul % (uint32_t)npairs);
     }
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    const int env = 2 * pair + (opaque_v(threadIdx.x) >= HL ? 1 : 0);
+    const bool upper = opaque_v(threadIdx.x) >= HL;
+    const int env = single ? pair : 2 * pair + (upper ? 1 : 0);
     // ONE step_pair call site (the whole pipeline is inlined): a tape item is env step t, waiting for
     // the pair's step t - 1 and handing over to its step t + 1; otherwise the first chunk hands over
     // to the last substep
     const int s0 = last ? nsub - 1 : 0, s1 = (tape || last) ? nsub : nsub - 1;
     const int wait_tag = tape ? (t > 0 ? qtag(epoch, t - 1, 1) : 0) : (last ? qtag(epoch, 0, 0) : 0);
     const int set_tag = tape ? (t < K - 1 ? qtag(epoch, t, 1) : 0) : (last ? 0 : qtag(epoch, 0, 0));
-    step_pair<T, NV, PGS, Resident<T>, ROLL>(k, smem, pcache, env, k->nenv, nullptr, s0, s1, pair, false, wait_tag,
-                                             set_tag, t, tape);
+    step_pair<T, NV, PGS, Resident<T>, ROLL>(k, smem, pcache, env, k->nenv, nullptr, s0, s1, pair, single && upper,
+                                             wait_tag, set_tag, t, tape);
     // the pair's duration for the next launch's order: the first chunk's is kept in qcost (its
     // store trails the hand-off, but the last substep reads it ~100 us later; a stale value only
     // makes the order less exact, never the results different); a tape launch times the pair's
@@ -2836,8 +2840,8 @@ __global__ __launch_bounds__(64, 1) void step_kernel_queue(KArgs<T> /* read via 
   int lastout = 0;
   if (threadIdx.x == 0) lastout = atomicAdd(&qs[QS_EXIT], 1) == (int)gridDim.x - 1;
   if (__builtin_amdgcn_readfirstlane(lastout)) {
-    const int npairs = (ka->nenv + 1) / 2;
-    if (threadIdx.x < QNB) qs[qs_cnt(npairs, epoch & 1) + threadIdx.x] = 0;
+    const int nunits = ka->p.single ? ka->nenv : (ka->nenv + 1) / 2;
+    if (threadIdx.x < QNB) qs[qs_cnt(nunits, epoch & 1) + threadIdx.x] = 0;
     if (threadIdx.x == 0) {
       qs[QS_HEAD] = 0;
       qs[QS_EXIT] = 0;
@@ -2949,6 +2953,11 @@ hipError_t launch_step(const DevModel<T>* dmodel, int nv, const EnvBuffers<T>& b
       return hipErrorInvalidValue;
     args.p.queue = 1;
   }
+  // a tape launch of a small batch (every env fits a resident wave of its own) queues single envs,
+  // not pairs: twice the waves, each env's steps back to back (configs[4]'s 1024 envs would otherwise
+  // leave half of the resident wave slots idle)
+  const bool qsingle = tape_launch && may_queue && nenv <= resident;
+  const int nunits = qsingle ? nenv : npairs;
   args.p.qorder = p.schedule == SCHED_AUTO ? 1 : 0;
   // fallback claim order (first queued launch, SCHED_FIXED_ORDER): a fixed multiplicative
   // permutation of the pairs (the same for both chunk kinds, so a pair's last substep is still
@@ -2958,16 +2967,18 @@ hipError_t launch_step(const DevModel<T>* dmodel, int nv, const EnvBuffers<T>& b
   args.p.qmul = 1;
   if (args.p.queue) {
     auto gcd = [](uint32_t a, uint32_t b) { while (b) { uint32_t t = a % b; a = b; b = t; } return a; };
-    uint32_t q = (uint32_t)(0.6180339887 * npairs) | 1u;
-    while (gcd(q, (uint32_t)npairs) != 1u) q += 2;
-    args.p.qmul = (int)(q % (uint32_t)npairs == 0 ? 1 : q);
+    uint32_t q = (uint32_t)(0.6180339887 * nunits) | 1u;
+    while (gcd(q, (uint32_t)nunits) != 1u) q += 2;
+    args.p.qmul = (int)(q % (uint32_t)nunits == 0 ? 1 : q);
   }
   // single-env schedule: one wave per env (the upper half-wave a ghost of the lower) when every
   // env gets a resident wave of its own -- small batches (configs[4]'s 1024 envs per GPU) would
   // otherwise leave SIMDs idle with one wave per env pair
-  args.p.single = (!args.p.queue && (p.schedule == SCHED_SINGLE ||
-                                     (p.schedule == 0 && resident > 0 && nenv <= resident))) ? 1 : 0;
-  const dim3 grid(args.p.queue ? (tape_launch ? std::min(resident, npairs) : resident) : (args.p.single ? nenv : npairs)),
+  args.p.single = qsingle || (!args.p.queue && (p.schedule == SCHED_SINGLE ||
+                                                (p.schedule == 0 && resident > 0 && nenv <= resident))) ? 1 : 0;
+  // the lost-hand-off test hook names an env (+ 1); the kernel compares it with its queue unit
+  if (args.p.dbg_lose_pair1 > 0 && !qsingle) args.p.dbg_lose_pair1 = (args.p.dbg_lose_pair1 - 1) / 2 + 1;
+  const dim3 grid(args.p.queue ? (tape_launch ? std::min(resident, nunits) : resident) : (args.p.single ? nenv : npairs)),
       block(WAVE);
   // the wide tier's grid: enough waves for a few deferred envs at once, few enough that the
   // common no-overflow launch (every wave reads the count and exits) costs a few microseconds
