@@ -330,15 +330,16 @@ class StepInfos(Sequence):
     annotate one, as SB3's VecMonitor does with ``episode``); a consumer that reads none pays
     nothing.  Building 4096 dicts in Python costs ~5 ms per step, more than the physics."""
 
-    __slots__ = ("_cols", "_pos", "_tobs", "_cache", "_n")
+    __slots__ = ("_cols", "_idx", "_tobs", "_cache", "_n")
 
     def __init__(self, obs, term, trunc, step_count, total, done_idx, term_obs):
         h = obs[:, 0].copy()
         if done_idx.size:
             h[done_idx] = term_obs[:, 0]
         self._n = len(term)
-        self._cols = (h.tolist(), step_count.astype(np.int64).tolist(), trunc.tolist(), term.tolist(), total.tolist())
-        self._pos = {int(i): k for k, i in enumerate(done_idx)}
+        # numpy columns until the first access (their conversion to Python scalars is deferred too)
+        self._cols = (h, step_count.copy(), trunc.copy(), term.copy(), total.copy())
+        self._idx = done_idx
         self._tobs = term_obs
         self._cache = None
 
@@ -347,7 +348,10 @@ class StepInfos(Sequence):
 
     def _all(self):
         if self._cache is None:
-            self._cache = _hsinfo.build(*self._cols, self._pos, self._tobs, 0, self._n)
+            h, sc, tr, te, tot = self._cols
+            pos = {int(i): k for k, i in enumerate(self._idx)}
+            self._cache = _hsinfo.build(h.tolist(), sc.astype(np.int64).tolist(), tr.tolist(), te.tolist(),
+                                        tot.tolist(), pos, self._tobs, 0, self._n)
         return self._cache
 
     def __getitem__(self, i):
