@@ -55,7 +55,11 @@ enum { ST_KIN = 0, ST_COM, ST_TENDON, ST_CRB, ST_COLLISION, ST_CONSTRAINT, ST_CO
  * 16: the factor is a preconditioner -- kept while the active set is unchanged (refinement steps
  *     reuse it) and the solve stops only when scale * |grad| < orc_mp_tol.
  * Without 16 the same fp32 stages keep the exact-active-set stop: no refinement, so the first
- * inexact step that leaves the active set unchanged ends the solve. */
+ * inexact step that leaves the active set unchanged ends the solve.
+ * 32: MuJoCo's own Newton iteration -- its inexact line search (line_search_mujoco below) and only
+ *     its tolerance stop (improvement or gradient, as 8), a zero step ending the solve.  The
+ *     restatement's exact line search + exact-active-set stop is measured against it in
+ *     tests/test_oracle_physics.py and profiles/mujoco_linesearch_r5.md. */
 int orc_variant = 0;
 double orc_mp_tol = 1e-13;
 int orc_mp_euler_refine = 1;   /* 64: Euler's (M + h B) solve with an fp32 factor and this many fp64 refinements */
@@ -747,6 +751,96 @@ static double line_search(const OrcModel* m, const OrcData* d, const double* x, 
   return lo;
 }
 
+/* MuJoCo's inexact line search (orc_variant bit 32; engine_solver.c PrimalSearch / updateBracket,
+ * MuJoCo 3.2.5, restated from its published algorithm -- the source is not in this container).
+ * Points along x + alpha s carry the cost and its first two derivatives; one Newton step from
+ * alpha 0, then one-sided Newton steps while the slope keeps its sign, then a bracketed search
+ * over {Newton from each bracket end, midpoint}.  Every stage stops at the first point whose
+ * |slope| < gtol = tolerance * ls_tolerance * |s| / scale.  ls_tolerance 0.01 and ls_iterations 50
+ * are MuJoCo's defaults, which the reference's humanoid.xml keeps. */
+double orc_ls_tolerance = 0.01;
+int orc_ls_iterations = 50;
+long orc_stat_ls_evals = 0;   /* line-search cost evaluations since the last reset (statistics only) */
+
+typedef struct { double alpha, cost, d0, d1; } LsPnt;
+
+static void ls_eval(LsPnt* p, double A0, double B0, int ne, const double* jar, const double* Js, const double* D,
+                    int* nevals) {
+  double a = p->alpha, c = a * B0 + 0.5 * a * a * A0, d0 = B0 + a * A0, d1 = A0;
+  for (int r = 0; r < ne; r++) {
+    double v = jar[r] + a * Js[r];
+    if (v < 0) { c += 0.5 * D[r] * v * v; d0 += D[r] * v * Js[r]; d1 += D[r] * Js[r] * Js[r]; }
+  }
+  p->cost = c; p->d0 = d0; p->d1 = d1;
+  (*nevals)++;
+  orc_stat_ls_evals++;
+}
+
+static int ls_update_bracket(LsPnt* p, const LsPnt cand[3], LsPnt* next, double A0, double B0, int ne,
+                             const double* jar, const double* Js, const double* D, int* nevals) {
+  int flag = 0;
+  for (int i = 0; i < 3; i++) {
+    if (p->d0 < 0 && cand[i].d0 < 0 && p->d0 < cand[i].d0) { *p = cand[i]; flag = 1; }
+    else if (p->d0 > 0 && cand[i].d0 > 0 && p->d0 > cand[i].d0) { *p = cand[i]; flag = 2; }
+  }
+  if (flag) { next->alpha = p->alpha - p->d0 / p->d1; ls_eval(next, A0, B0, ne, jar, Js, D, nevals); }
+  return flag;
+}
+
+static double line_search_mujoco(const OrcModel* m, const OrcData* d, const double* x, const double* s,
+                                 const double* jar, double* Js, double scale) {
+  int nv = m->nv, ne = d->nefc, n = 0;
+  double Ms[OMAXV], A0 = 0, B0 = 0, snorm = 0;
+  for (int i = 0; i < nv; i++) snorm += s[i] * s[i];
+  snorm = sqrt(snorm);
+  if (snorm < MINVAL) return 0;
+  const double gtol = m->tolerance * orc_ls_tolerance * snorm / scale;
+  for (int i = 0; i < nv; i++) {
+    double t = 0;
+    for (int k = 0; k < nv; k++) t += d->qM[i][k] * s[k];
+    Ms[i] = t;
+  }
+  for (int i = 0; i < nv; i++) { A0 += s[i] * Ms[i]; B0 += (x[i] - d->qacc_smooth[i]) * Ms[i]; }
+  for (int r = 0; r < ne; r++) {
+    double v = 0;
+    for (int k = 0; k < nv; k++) v += d->efc_J[r][k] * s[k];
+    Js[r] = v;
+  }
+  const double* D = d->efc_D;
+  LsPnt p0 = {0}, p1, p2, pmid, p1n, p2n;
+  ls_eval(&p0, A0, B0, ne, jar, Js, D, &n);
+  p1.alpha = p0.alpha - p0.d0 / p0.d1;
+  ls_eval(&p1, A0, B0, ne, jar, Js, D, &n);
+  if (p0.cost < p1.cost) p1 = p0;
+  if (fabs(p1.d0) < gtol) return p1.alpha;
+  const int dir = p1.d0 < 0 ? 1 : -1;
+  while (p1.d0 * dir <= -gtol && n < orc_ls_iterations) {   /* one-sided Newton steps */
+    p2 = p1;
+    p1.alpha -= p1.d0 / p1.d1;
+    ls_eval(&p1, A0, B0, ne, jar, Js, D, &n);
+    if (fabs(p1.d0) < gtol) return p1.alpha;
+  }
+  if (n >= orc_ls_iterations) return p1.alpha;              /* could not bracket */
+  p2n = p1;
+  p1n.alpha = p1.alpha - p1.d0 / p1.d1;
+  ls_eval(&p1n, A0, B0, ne, jar, Js, D, &n);
+  while (n < orc_ls_iterations) {                            /* bracketed search */
+    pmid.alpha = 0.5 * (p1.alpha + p2.alpha);
+    ls_eval(&pmid, A0, B0, ne, jar, Js, D, &n);
+    LsPnt cand[3] = {p1n, p2n, pmid};
+    int best = -1;
+    for (int i = 0; i < 3; i++)
+      if (fabs(cand[i].d0) < gtol && (best < 0 || cand[i].cost < cand[best].cost)) best = i;
+    if (best >= 0) return cand[best].alpha;
+    int b1 = ls_update_bracket(&p1, cand, &p1n, A0, B0, ne, jar, Js, D, &n);
+    int b2 = ls_update_bracket(&p2, cand, &p2n, A0, B0, ne, jar, Js, D, &n);
+    if (!b1 && !b2) return pmid.alpha;                      /* no bracket update: numerical limit */
+  }
+  if (p1.cost <= p2.cost && p1.cost < p0.cost) return p1.alpha;
+  if (p2.cost <= p1.cost && p2.cost < p0.cost) return p2.alpha;
+  return 0;
+}
+
 static void solve_newton(const OrcModel* m, OrcData* d) {
   int nv = m->nv, ne = d->nefc;
   double x[OMAXV], jar[OMAXEFC], Js[OMAXEFC], g[OMAXV], s[OMAXV];
@@ -756,7 +850,7 @@ static void solve_newton(const OrcModel* m, OrcData* d) {
   memcpy(x, cs < cw ? d->qacc_smooth : d->qacc_warmstart, sizeof(double) * nv);
   double cost = eval_cost(m, d, x, jar);
   double scale = 1.0 / (m->meaninertia * (nv > 1 ? nv : 1));
-  const int mp_refine = orc_variant & 16;
+  const int mp_refine = orc_variant & 16, mj_ls = orc_variant & 32;
   int it, refine = 0;
   for (it = 0; it < m->iterations; it++) {
     unsigned char act[OMAXEFC];
@@ -798,7 +892,8 @@ static void solve_newton(const OrcModel* m, OrcData* d) {
     chol_solve(s, L, g, nv);
     for (int i = 0; i < nv; i++) s[i] = -s[i];
     ORC_SUBSTAGE(ST_SOLVER_LS);
-    double alpha = line_search(m, d, x, s, jar, Js);
+    double alpha = mj_ls ? line_search_mujoco(m, d, x, s, jar, Js, scale) : line_search(m, d, x, s, jar, Js);
+    if (mj_ls && alpha == 0) break;
     for (int i = 0; i < nv; i++) x[i] += alpha * s[i];
     double newcost = eval_cost(m, d, x, jar);
     ORC_SUBSTAGE(ST_SOLVER);
@@ -806,13 +901,14 @@ static void solve_newton(const OrcModel* m, OrcData* d) {
     for (int r = 0; r < ne; r++) if ((jar[r] < 0) != act[r]) { same = 0; break; }
     double improvement = cost - newcost;
     cost = newcost;
+    if (mj_ls) same = 0;                          /* inexact alpha: only MuJoCo's tolerance rule stops */
     if (mp_refine) {                              /* preconditioned: only the gradient test ends it */
       refine = same;
       if (scale * improvement < 1e-16 && same) { it++; break; }
       continue;
     }
-    if (same || scale * improvement < 1e-16) { it++; break; }
-    if (orc_variant & 8) {                        /* MuJoCo's stop: improvement or gradient below tol */
+    if (same || (!mj_ls && scale * improvement < 1e-16)) { it++; break; }
+    if (orc_variant & (8 | 32)) {                 /* MuJoCo's stop: improvement or gradient below tol */
       double g2 = 0;
       for (int i = 0; i < nv; i++) {
         double t = 0;

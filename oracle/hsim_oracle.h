@@ -91,6 +91,9 @@ extern int orc_variant;   /* known-wrong physics switches (hsim_oracle.c), 0 = t
 extern double orc_mp_tol;          /* gradient stop of the mixed-precision Newton variant (16) */
 extern long orc_stat_nfactor;      /* Newton factorizations so far (statistics) */
 extern int orc_mp_euler_refine;    /* refinements of the fp32-factored Euler solve (variant 64) */
+extern double orc_ls_tolerance;    /* MuJoCo's opt.ls_tolerance for the inexact line search (variant 32) */
+extern int orc_ls_iterations;      /* MuJoCo's opt.ls_iterations (variant 32) */
+extern long orc_stat_ls_evals;     /* inexact line-search cost evaluations so far (statistics) */
 /* full-state option: after mj_forward, the contact part of mj_rnePostConstraint (cfrc_ext) and
  * mj_subtreeVel (subtree_linvel), i.e. what MuJoCo computes when those fields are requested;
  * the reference never requests them (zeros), so this is hsim's opt-in "full_state" mode. */

@@ -404,8 +404,8 @@ def test_newton_tolerance_stop_gives_the_exact_trajectory():
     """MuJoCo's Newton also stops when scale*improvement or scale*|grad| falls below opt.tolerance
     (1e-8); the oracle (and the kernel) stop at the exact active set.  With the exact line search the
     tolerance rule never fires first: the oracle run with it (orc_variant bit 8) is bitwise the same
-    over 300 substeps of random torques with contacts.  (MuJoCo's own line search is inexact; that
-    part of its iteration is not restated.)"""
+    over 300 substeps of random torques with contacts.  (MuJoCo's inexact line search is bit 32:
+    test_mujoco_inexact_line_search_agrees_to_round_off.)"""
     from oracle import trajfit as T
     from oracle.oracle import Oracle
     M = T.make_model(XML)
@@ -428,6 +428,53 @@ def test_newton_tolerance_stop_gives_the_exact_trajectory():
     finally:
         T.set_variant(0)
     assert a.d.ncon > 0 or np.abs(a.qpos[2]) < 1.0      # it reached the floor
+
+
+def test_mujoco_inexact_line_search_agrees_to_round_off():
+    """MuJoCo 3.2.5's own Newton iteration (orc_variant 8|32: its Newton-bracketing line search with
+    ls_tolerance 0.01 and its opt.tolerance stop, restated in hsim_oracle.c line_search_mujoco)
+    against the restatement's exact line search + exact-active-set stop, which the kernel runs.
+    From the same mjData at every substep of a random-torque tape with contacts the qacc agree to
+    round-off, and the zero-tape trajectories stay far inside the north star's 1e-4 qpos bar
+    (profiles/mujoco_linesearch_r5.md has seeds 0-4 over 1000 substeps: <= 3.1e-11)."""
+    from oracle.oracle import Oracle
+    a, b = Oracle(XML), Oracle(XML)
+    rng = np.random.default_rng(0)
+    q = a.M["qpos0"].copy()
+    q[2], q[3:7] = 1.282, [1, 0, 0, 0]
+    q += rng.uniform(-0.01, 0.01, 28) * np.r_[1, 1, 0.1, 0, 0, 0, 0, np.ones(21)]
+    v = rng.uniform(-0.01, 0.01, 27)
+    var = C.c_int.in_dll(a.lib, "orc_variant")
+    evals = C.c_long.in_dll(a.lib, "orc_stat_ls_evals")
+    e0 = evals.value
+    a.qpos[:], a.qvel[:] = q, v
+    worst, ncon = 0.0, 0
+    try:
+        for n in range(150):
+            u = rng.uniform(-1, 1, 21)
+            C.memmove(C.byref(b.d), C.byref(a.d), C.sizeof(a.d))
+            var.value = 8 | 32
+            b.step(u, 1)
+            var.value = 0
+            a.step(u, 1)
+            qa = a.get("qacc")
+            worst = max(worst, np.abs(b.get("qacc") - qa).max() / max(1.0, np.abs(qa).max()))
+            ncon = max(ncon, a.d.ncon)
+        assert ncon > 0 and evals.value > e0          # contacts were active, and bit 32 ran
+        assert worst < 1e-12, worst
+        za, zb = Oracle(XML), Oracle(XML)
+        for o in (za, zb):
+            o.qpos[:], o.qvel[:] = q, v
+        dq = 0.0
+        for n in range(300):
+            var.value = 8 | 32
+            zb.step(None, 1)
+            var.value = 0
+            za.step(None, 1)
+            dq = max(dq, np.abs(za.qpos - zb.qpos).max())
+        assert dq < 1e-9, dq
+    finally:
+        var.value = 0
 
 
 def test_fp32_state_storage_alone_breaks_the_1e4_bound_through_contact_flips():
