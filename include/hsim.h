@@ -300,14 +300,15 @@ int hs_gae(const float* rewards, const float* values, const float* episode_start
  * uint64) is not NULL -- graph replays then draw fresh noise; z = 0 when deterministic != 0); writes
  * actions [N][A] (unclipped, the buffer copy), actions_clipped [N][A] (clip to [-1, 1], what the
  * env steps with), log_prob [N], values [N] and episode_starts_out [N].  Asynchronous on `stream`. */
-/* Fused forward of one packed 2-hidden-layer ReLU MLP (H = 256): out[N][A] = relu(relu(X W1 + b1) W2 + b2)
- * W3 + b3, weights as [in][out] row-major (W1 [D][ld1], W2 [256][256], W3 [256][ld3]); D <= 512,
- * A <= 32.  Replaces the three GEMMs of SB3's MlpPolicy forward (ActorCriticPolicy.forward ->
+/* Fused forward of one 2-hidden-layer ReLU MLP (H = 256): out[N][A] = relu(relu(X W1' + b1) W2' + b2)
+ * W3' + b3, weights as nn.Linear stores them, [out][in] row-major (W1 [256][ld1 >= D], W2 [256][ld2],
+ * W3 [A][ld3], ld2 / ld3 >= 256); D <= 512, A <= 32.  16-byte weight loads when every weight row
+ * is 16-byte aligned, element loads otherwise.  Replaces the three GEMMs of SB3's MlpPolicy forward (ActorCriticPolicy.forward ->
  * mlp_extractor -> action_net / value_net, policies.py, SB3 2.3.2) in the rollout: the pi net's mean
  * per env step and the vf net's values over the rollout buffer.  fp32 in, fp32 MFMA accumulation.
  * Asynchronous on `stream`. */
 int hs_mlp2_forward(const float* X, int ldx, int D, int N, const float* W1, int ld1, const float* b1, const float* W2,
-                    const float* b2, const float* W3, int ld3, const float* b3, int A, float* out, int ldo,
+                    int ld2, const float* b2, const float* W3, int ld3, const float* b3, int A, float* out, int ldo,
                     void* stream);
 int hs_ppo_act(const float* mean, int mean_ld, const float* value, int value_ld, const float* log_std,
                const float* episode_start, uint64_t seed, uint64_t counter, const uint64_t* counter_base,

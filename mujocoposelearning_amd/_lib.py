@@ -115,7 +115,7 @@ def lib():
         "hs_adam_workspace": (u64, [u64]),
         "hs_adam_clip": (i, [i, vp, vp, vp, vp, vp, vp, vp, C.c_float, C.c_double, C.c_double, C.c_double, C.c_double,
                              vp]),
-        "hs_mlp2_forward": (i, [vp, i, i, i, vp, i, vp, vp, vp, vp, i, vp, i, vp, i, vp]),
+        "hs_mlp2_forward": (i, [vp, i, i, i, vp, i, vp, vp, i, vp, vp, i, vp, i, vp, i, vp]),
         "hs_colsum_partial_rows": (u64, [u64, u64]),
         "hs_relu_grad_colsum": (i, [vp, vp, u64, u64, vp, vp, vp]),
         "hs_colsum_pair": (i, [vp, u64, u64, vp, vp, u64, u64, vp, vp]),

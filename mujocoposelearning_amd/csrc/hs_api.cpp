@@ -903,13 +903,15 @@ int hs_adam_clip(int nt, float* const* params, const float* const* grads, float*
 }
 
 int hs_mlp2_forward(const float* X, int ldx, int D, int N, const float* W1, int ld1, const float* b1, const float* W2,
-                    const float* b2, const float* W3, int ld3, const float* b3, int A, float* out, int ldo,
+                    int ld2, const float* b2, const float* W3, int ld3, const float* b3, int A, float* out, int ldo,
                     void* stream) {
-  if (N < 0 || D < 1 || D > 512 || A < 1 || A > 32 || ld1 < 256 || ld3 < A || ldx < D || ldo < A)
-    return fail("hs_mlp2_forward: need N >= 0, 1 <= D <= 512, 1 <= A <= 32, ld1 >= 256, ld3 >= A, ldx >= D, ldo >= A");
+  if (N < 0 || D < 1 || D > 512 || A < 1 || A > 32 || ld1 < D || ld2 < 256 || ld3 < 256 || ldx < D || ldo < A)
+    return fail("hs_mlp2_forward: need N >= 0, 1 <= D <= 512, 1 <= A <= 32, ld1 >= D, ld2 >= 256, ld3 >= 256, "
+                "ldx >= D, ldo >= A");
   if (N == 0) return 0;
   if (!X || !W1 || !b1 || !W2 || !b2 || !W3 || !b3 || !out) return fail("hs_mlp2_forward: null buffer");
-  return hip_ok(hs::launch_mlp2_fwd(X, ldx, D, N, W1, ld1, b1, W2, b2, W3, ld3, b3, A, out, ldo, (hipStream_t)stream),
+  return hip_ok(hs::launch_mlp2_fwd(X, ldx, D, N, W1, ld1, b1, W2, ld2, b2, W3, ld3, b3, A, out, ldo,
+                                    (hipStream_t)stream),
                 "mlp2_fwd_kernel")
              ? 0
              : -1;

@@ -195,7 +195,7 @@ hipError_t launch_ppo_post(const float* reward, const uint8_t* terminated, const
                            double* ep_return_out, float* episode_start, int N, hipStream_t stream);
 // fused 2-hidden-layer (H = 256) ReLU MLP forward of one packed policy net (ppo.hip mlp2_fwd_kernel)
 hipError_t launch_mlp2_fwd(const float* X, int ldx, int D, int N, const float* W1, int ld1, const float* b1,
-                           const float* W2, const float* b2, const float* W3, int ld3, const float* b3, int A,
+                           const float* W2, int ld2, const float* b2, const float* W3, int ld3, const float* b3, int A,
                            float* out, int ldo, hipStream_t stream);
 // column sums of a row-major [rows][cols] float32 matrix (ppo.hip); workspace of
 // colsum_workspace(rows, cols) floats (0: none needed)

@@ -521,83 +521,192 @@ __global__ __launch_bounds__(CS_COLS* CS_PHASES) void colsum_pair_kernel(const f
 
 
 // ------------------------------------------------------------------ fused 2-hidden-layer MLP forward
-// out = relu(relu(X W1 + b1) W2 + b2) W3 + b3 for one packed policy net (PPO rollout: the pi net's
-// mean per env step, the vf net's values once per rollout).  W1 [D][ld1], W2 [H][H], W3 [H][A] are
-// the packed ([in][out]) weights of ActorCritic.pack_heads, H = 256, A <= 32.  One workgroup (4 waves)
-// per 16 rows: the 16 x D input tile is staged in LDS, and each layer is v_mfma_f32_16x16x4_f32 tiles
-// (f32 in, f32 accumulate -- the fp32 GEMM's arithmetic in another summation order): wave w owns
-// output columns [64 w, 64 w + 64) of a hidden layer (4 accumulator tiles), B operands stream from
-// L2-resident weights, and the bias + ReLU epilogue writes the layer back to LDS for the next one.
+// out = relu(relu(X W1' + b1) W2' + b2) W3' + b3 for one policy net (PPO rollout: the pi net's mean per
+// env step, the vf net's values once per rollout).  The weights come as nn.Linear stores them,
+// [out][in] row-major (W1 [256][ld1], W2 [256][ld2], W3 [A][ld3]): the reduction index k is
+// contiguous, so one 16-byte load fetches a lane's B operand for four v_mfma_f32_16x16x4_f32 steps.
+// Within each group of 16 k the MFMA steps run over a permuted k (step j of lane group ak takes
+// k = 16 q + 4 ak + j) so that A (from LDS) and B (from global) are both one b128 per lane per
+// group -- the sum over k is the same, only its order differs from the GEMM's.
+// One workgroup per 16 RB rows, 8 waves: wave w owns output columns [32 w, 32 w + 32) of a hidden
+// layer for all the rows (RB row blocks x 2 column tiles of accumulators).  Its weight rows are read
+// by no other wave, so they stream straight into VGPRs (the MI355X guide's GEMV rule: no LDS round
+// trip), MLP_PF groups ahead of the MFMAs in a register ring, and each 16-byte weight load feeds RB
+// row blocks; the input tile and the hidden activations live in LDS (dynamic: sized to D).
+// RB = 1 for the per-step pi forward (4096 rows: 256 workgroups, every CU busy), RB = 2 for the
+// rollout-buffer vf pass (half the weight traffic per row).
 // Replaces three library GEMM launches and their two [N][256] HBM round trips.
-constexpr int MLP_H = 256, MLP_R = 16, MLP_TPB = 256, MLP_MAXD = 512;
+constexpr int MLP_H = 256, MLP_WAVES = 8, MLP_TPB = 64 * MLP_WAVES, MLP_MAXD = 512, MLP_PF = 4;
+// above this many rows two row blocks per wave (A/B with each forced, tools/probes/gpu_mlp2_fwd.py,
+// profiles/r5i: 4096 rows 23.5 vs 26.6 us, 8192 rows 40.2 vs 26.4 us)
+constexpr int MLP_RB2_ROWS = 6144;
+constexpr int MLP_SH = MLP_H + 4;   // LDS row stride (floats) of the hidden tiles: 16-byte aligned rows
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+template <bool VEC>
+__device__ __forceinline__ f32x4 mlp_ld4(const float* __restrict__ p) {
+  if constexpr (VEC) return *reinterpret_cast<const f32x4*>(p);
+  else return f32x4{p[0], p[1], p[2], p[3]};
+}
+
+// acc[rb][t] += A_rb[16 x 16] . B_t[16 x 16] for k-group g: a = LDS base of this lane's A row in
+// row block 0 (+ 4 ak), sa = the row-block stride (16 rows) in floats
+template <int RB>
+__device__ __forceinline__ void mlp_group(const float* a, int sa, int g, const f32x4& b0, const f32x4& b1,
+                                          f32x4 (&acc)[RB][2]) {
+  f32x4 x[RB];
+#pragma unroll
+  for (int rb = 0; rb < RB; rb++) x[rb] = *reinterpret_cast<const f32x4*>(a + rb * sa + 16 * g);
+#pragma unroll
+  for (int s = 0; s < 4; s++)
+#pragma unroll
+    for (int rb = 0; rb < RB; rb++) {
+      acc[rb][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[rb][s], b0[s], acc[rb][0], 0, 0, 0);
+      acc[rb][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[rb][s], b1[s], acc[rb][1], 0, 0, 0);
+    }
+}
+// the full k-groups [0, G) of one wave's two column tiles; w0 / w1 = this lane's weight rows (+ 4 ak).
+// Every ring refill is unconditional (the group index clamped to G - 1: the last refills re-read
+// it) and follows the MFMAs that consumed the slot, so the compiler's wait before a slot's use
+// counts only the loads issued after it and the ring needs no register copies.
+template <bool VEC, int RB>
+__device__ __forceinline__ void mlp_groups(const float* a, int sa, const float* __restrict__ w0,
+                                           const float* __restrict__ w1, int G, f32x4 (&acc)[RB][2]) {
+  if (G <= 0) return;
+  f32x4 bq[MLP_PF][2];
+#pragma unroll
+  for (int j = 0; j < MLP_PF; j++) {
+    const int g = j < G - 1 ? j : G - 1;
+    bq[j][0] = mlp_ld4<VEC>(w0 + 16 * g);
+    bq[j][1] = mlp_ld4<VEC>(w1 + 16 * g);
+  }
+  const int Gm = G - G % MLP_PF;
+  for (int g0 = 0; g0 < Gm; g0 += MLP_PF) {
+#pragma unroll
+    for (int j = 0; j < MLP_PF; j++) {
+      const int g = g0 + j;
+      mlp_group<RB>(a, sa, g, bq[j][0], bq[j][1], acc);
+      const int gn = g + MLP_PF < G - 1 ? g + MLP_PF : G - 1;
+      bq[j][0] = mlp_ld4<VEC>(w0 + 16 * gn);
+      bq[j][1] = mlp_ld4<VEC>(w1 + 16 * gn);
+      __builtin_amdgcn_sched_barrier(0);   // keep each refill in its group (the scheduler would batch them)
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < MLP_PF - 1; j++)   // the last G % MLP_PF groups, already in slots 0..
+    if (Gm + j < G) mlp_group<RB>(a, sa, Gm + j, bq[j][0], bq[j][1], acc);
+}
+
+// dynamic LDS of one workgroup: the input tile (row stride roundup16(D) + 4), later layer 2's output
+// (stride MLP_SH), then layer 1's output
+__host__ __device__ constexpr int mlp_xs_stride(int D) { return ((D + 15) & ~15) + 4 > MLP_SH ? ((D + 15) & ~15) + 4 : MLP_SH; }
+__host__ __device__ constexpr size_t mlp_lds_bytes(int RB, int D) { return (size_t)16 * RB * (mlp_xs_stride(D) + MLP_SH) * 4; }
+
+template <bool VEC, int RB>
 __global__ __launch_bounds__(MLP_TPB) void mlp2_fwd_kernel(const float* __restrict__ X, int ldx, int D, int N,
                                                            const float* __restrict__ W1, int ld1,
                                                            const float* __restrict__ b1,
-                                                           const float* __restrict__ W2, const float* __restrict__ b2,
+                                                           const float* __restrict__ W2, int ld2,
+                                                           const float* __restrict__ b2,
                                                            const float* __restrict__ W3, int ld3,
                                                            const float* __restrict__ b3, int A,
                                                            float* __restrict__ out, int ldo) {
-  // row strides padded by one float: the 16 rows of an A operand fall in 16 different banks
-  __shared__ float xs[MLP_R * (MLP_MAXD + 1)];
-  __shared__ float hbuf[2][MLP_R * (MLP_H + 1)];
+  constexpr int R = 16 * RB;
+  extern __shared__ __attribute__((aligned(16))) float mlp_lds[];
+  const int sx = mlp_xs_stride(D);
+  float* xs = mlp_lds;                 // X tile, then layer 2's output
+  float* hs = mlp_lds + R * sx;        // layer 1's output, then the head's partial sums
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int row0 = blockIdx.x * MLP_R;
-  const int Dp = (D + 3) & ~3, sx = Dp + 1, sh = MLP_H + 1;
-  for (int e = threadIdx.x; e < MLP_R * Dp; e += MLP_TPB) {
-    const int r = e / Dp, c = e - r * Dp;
-    xs[r * sx + c] = (row0 + r < N && c < D) ? X[(size_t)(row0 + r) * ldx + c] : 0.f;
+  const int ar = lane & 15, ak = lane >> 4;   // A: row ar, k 4 ak..; B: column ar, k 4 ak..; C: rows 4 ak.., column ar
+  const int row0 = blockIdx.x * R;
+  const int Gf = D >> 4, Dp = (D + 15) & ~15;
+  if ((D & 3) == 0 && (ldx & 3) == 0 && ((uintptr_t)X & 15) == 0) {   // 16-byte staging: 32 threads per row
+    for (int r = threadIdx.x >> 5; r < R; r += MLP_TPB / 32) {
+      const bool live = row0 + r < N;
+      const float* xr = X + (size_t)(live ? row0 + r : 0) * ldx;
+      for (int c = 4 * (threadIdx.x & 31); c < Dp; c += 128) {
+        const f32x4 v = (live && c < D) ? *reinterpret_cast<const f32x4*>(xr + c) : f32x4{0, 0, 0, 0};
+        *reinterpret_cast<f32x4*>(xs + r * sx + c) = v;
+      }
+    }
+  } else {
+    for (int e = threadIdx.x; e < R * Dp; e += MLP_TPB) {
+      const int r = e / Dp, c = e - r * Dp;
+      xs[r * sx + c] = (row0 + r < N && c < D) ? X[(size_t)(row0 + r) * ldx + c] : 0.f;
+    }
   }
   __syncthreads();
-  const int ar = lane & 15, ak = lane >> 4;        // A operand: row ar, k ak;  B: k ak, column ar
-  // hidden layer: dst = relu(src W + b), src in LDS (stride ss, K columns), W [K][ldw] global
-  auto hidden = [&](const float* src, int ss, int K, const float* __restrict__ W, int ldw,
-                    const float* __restrict__ bias, float* dst) {
-    const int c0 = wave * 64;
-    f32x4 acc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
-    const float* wp = W + (size_t)ak * ldw + c0 + ar;
-#pragma unroll 4
-    for (int k = 0; k < K; k += 4) {
-      const float a = src[ar * ss + k + ak];
-      const bool kin = k + ak < K;
+  const int c0 = wave * 32 + ar;   // this lane's column of tile 0 (tile 1: + 16)
+  auto epilogue = [&](const f32x4 (&acc)[RB][2], const float* __restrict__ bias, float* dst) {
 #pragma unroll
-      for (int t = 0; t < 4; t++) {
-        const float b = kin ? wp[(size_t)k * ldw + 16 * t] : 0.f;
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[t], 0, 0, 0);
-      }
-    }
+    for (int t = 0; t < 2; t++) {
+      const float bb = bias[c0 + 16 * t];
 #pragma unroll
-    for (int t = 0; t < 4; t++) {
-      const int col = c0 + 16 * t + ar;
-      const float bb = bias[col];
+      for (int rb = 0; rb < RB; rb++)
 #pragma unroll
-      for (int r = 0; r < 4; r++) dst[(ak * 4 + r) * sh + col] = fmaxf(acc[t][r] + bb, 0.f);
+        for (int r = 0; r < 4; r++)
+          dst[(16 * rb + 4 * ak + r) * MLP_SH + c0 + 16 * t] = fmaxf(acc[rb][t][r] + bb, 0.f);
     }
   };
-  hidden(xs, sx, D, W1, ld1, b1, hbuf[0]);
-  __syncthreads();
-  hidden(hbuf[0], sh, MLP_H, W2, MLP_H, b2, hbuf[1]);
-  __syncthreads();
-  // head: A <= 32 columns = 2 tiles, waves 0 and 1
-  if (wave < 2 && 16 * wave < A) {
-    const int col = 16 * wave + ar;
-    f32x4 acc = {0, 0, 0, 0};
-    const float* src = hbuf[1];
-#pragma unroll 4
-    for (int k = 0; k < MLP_H; k += 4) {
-      const float a = src[ar * sh + k + ak];
-      const float b = col < A ? W3[(size_t)(k + ak) * ld3 + col] : 0.f;
-      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
-    }
-    if (col < A) {
-      const float bb = b3[col];
+  {   // layer 1: K = D (full groups pipelined, a partial last group with masked loads)
+    f32x4 acc[RB][2] = {};
+    const float* w0 = W1 + (size_t)c0 * ld1 + 4 * ak;
+    const float* w1 = w0 + (size_t)16 * ld1;
+    const float* a = xs + ar * sx + 4 * ak;
+    mlp_groups<VEC, RB>(a, 16 * sx, w0, w1, Gf, acc);
+    if (D & 15) {
+      const int kb = 16 * Gf + 4 * ak;
+      f32x4 b0, b1v;
 #pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int row = row0 + ak * 4 + r;
-        if (row < N) out[(size_t)row * ldo + col] = acc[r] + bb;
+      for (int i = 0; i < 4; i++) {
+        b0[i] = kb + i < D ? w0[16 * Gf + i] : 0.f;
+        b1v[i] = kb + i < D ? w1[16 * Gf + i] : 0.f;
       }
+      mlp_group<RB>(a, 16 * sx, Gf, b0, b1v, acc);
     }
+    epilogue(acc, b1, hs);
+  }
+  __syncthreads();
+  {   // layer 2: K = 256, into xs (the X tile is dead)
+    f32x4 acc[RB][2] = {};
+    const float* w0 = W2 + (size_t)c0 * ld2 + 4 * ak;
+    mlp_groups<VEC, RB>(hs + ar * MLP_SH + 4 * ak, 16 * MLP_SH, w0, w0 + (size_t)16 * ld2, MLP_H / 16, acc);
+    epilogue(acc, b2, xs);
+  }
+  __syncthreads();
+  // head: A <= 32 columns = 2 tiles x 4 quarters of k over the 8 waves (every wave's 4 weight loads in
+  // flight at once), the quarters' partial sums added through LDS (hs is free after layer 2); a lane
+  // whose column is >= A reads row A - 1 and multiplies zeros
+  {
+    const int t = wave & 1, kq = wave >> 1, col = 16 * t + ar;
+    if (16 * t < A) {
+      const float* w = W3 + (size_t)(col < A ? col : A - 1) * ld3 + 4 * ak + 64 * kq;
+      const float keep = col < A ? 1.f : 0.f;
+      const float* a = xs + ar * MLP_SH + 4 * ak + 64 * kq;
+      f32x4 bw[4];
+#pragma unroll
+      for (int g = 0; g < 4; g++) bw[g] = mlp_ld4<VEC>(w + 16 * g) * keep;
+      f32x4 acc[RB] = {};
+#pragma unroll
+      for (int g = 0; g < 4; g++)
+#pragma unroll
+        for (int rb = 0; rb < RB; rb++) {
+          const f32x4 x = *reinterpret_cast<const f32x4*>(a + 16 * rb * MLP_SH + 16 * g);
+#pragma unroll
+          for (int s = 0; s < 4; s++) acc[rb] = __builtin_amdgcn_mfma_f32_16x16x4f32(x[s], bw[g][s], acc[rb], 0, 0, 0);
+        }
+#pragma unroll
+      for (int rb = 0; rb < RB; rb++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) hs[(kq * R + 16 * rb + 4 * ak + r) * 32 + col] = acc[rb][r];
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < R * A; e += MLP_TPB) {
+    const int r = e / A, c = e - r * A;
+    if (row0 + r < N)
+      out[(size_t)(row0 + r) * ldo + c] = b3[c] + ((hs[r * 32 + c] + hs[(R + r) * 32 + c]) +
+                                                   (hs[(2 * R + r) * 32 + c] + hs[(3 * R + r) * 32 + c]));
   }
 }
 
@@ -786,13 +895,31 @@ hipError_t launch_colsum_pair(const float* x0, size_t rows0, size_t cols0, float
 
 
 hipError_t launch_mlp2_fwd(const float* X, int ldx, int D, int N, const float* W1, int ld1, const float* b1,
-                           const float* W2, const float* b2, const float* W3, int ld3, const float* b3, int A,
+                           const float* W2, int ld2, const float* b2, const float* W3, int ld3, const float* b3, int A,
                            float* out, int ldo, hipStream_t stream) {
-  if (D < 1 || D > MLP_MAXD || A < 1 || A > 32 || N < 0 || ld1 < MLP_H || ld3 < A || ldx < D || ldo < A)
+  if (D < 1 || D > MLP_MAXD || A < 1 || A > 32 || N < 0 || ld1 < D || ld2 < MLP_H || ld3 < MLP_H || ldx < D || ldo < A)
     return hipErrorInvalidValue;
   if (N == 0) return hipSuccess;
-  mlp2_fwd_kernel<<<(N + MLP_R - 1) / MLP_R, MLP_TPB, 0, stream>>>(X, ldx, D, N, W1, ld1, b1, W2, b2, W3, ld3, b3, A,
-                                                                   out, ldo);
+  // 16-byte weight loads when every weight row starts 16-byte aligned; two row blocks per wave for
+  // large row counts (half the weight traffic; one-block workgroups keep every CU busy below)
+  auto al = [](const float* p, int ld) { return ((uintptr_t)p & 15) == 0 && (ld & 3) == 0; };
+  const bool vec = al(W1, ld1) && al(W2, ld2) && al(W3, ld3);
+  const int RB = N > MLP_RB2_ROWS ? 2 : 1;
+  const dim3 grid((N + 16 * RB - 1) / (16 * RB));
+  const size_t lds = mlp_lds_bytes(RB, D);
+  // dynamic LDS above 64 KiB needs the per-kernel opt-in (once per instance)
+#define MLP_LAUNCH(V, B)                                                                                     \
+  do {                                                                                                      \
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp2_fwd_kernel<V, B>), \
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,          \
+                                                       (int)mlp_lds_bytes(B, MLP_MAXD));                    \
+    if (attr != hipSuccess) return attr;                                                                    \
+    mlp2_fwd_kernel<V, B><<<grid, MLP_TPB, lds, stream>>>(X, ldx, D, N, W1, ld1, b1, W2, ld2, b2, W3, ld3, b3, \
+                                                          A, out, ldo);                                     \
+  } while (0)
+  if (vec) { if (RB == 2) MLP_LAUNCH(true, 2); else MLP_LAUNCH(true, 1); }
+  else { if (RB == 2) MLP_LAUNCH(false, 2); else MLP_LAUNCH(false, 1); }
+#undef MLP_LAUNCH
   return hipGetLastError();
 }
 

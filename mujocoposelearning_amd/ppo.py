@@ -30,6 +30,7 @@ from .ppo_ops import (Linear, _GaussLogpFn, _PPOLossFn, _SplitKLinearFn, _SplitK
                       ppo_loss, ppo_post)
 
 FUSED_MLP = True      # rollout forward through the fused hs_mlp2_forward kernel where it applies
+FUSED_MLP_MAX_ROWS = None   # ... up to this many rows (None: any)
 FUSED_ROLLOUT = True  # whole rollouts as hs_rollout launches (policy inside the env kernel) where they apply
 
 
@@ -143,6 +144,8 @@ class ActorCritic(nn.Module):
         if pk is None:
             mean, value = self(obs)
             return mean, value
+        if self._fused_mlp_ok(obs):                               # two fused launches beat the chain here
+            return self.net_forward(obs, 0), self.net_forward(obs, 1)
         w1, b1, mid, w3, b3 = pk
         n = obs.shape[0]
         # [N, 2H]: layer 1 of both nets, ReLU in the GEMM epilogue on a device
@@ -152,6 +155,18 @@ class ActorCritic(nn.Module):
             h = torch.baddbmm(b, h, w).relu_()
         out = torch.baddbmm(b3, h, w3)                            # [2, N, A]
         return out[0], out[1, :, 0]
+
+    def _fused_mlp_ok(self, obs):
+        """The fused hs_mlp2_forward kernel applies: packed equal pi / vf nets of two hidden layers of
+        256 (ReLU), <= 512 inputs and <= 32 actions, fp32 rows with unit stride on a device, and at
+        most FUSED_MLP_MAX_ROWS rows (above, the library GEMM chain is faster)."""
+        pk = getattr(self, "_packed", None)
+        if pk is None or not FUSED_MLP or not obs.is_cuda:
+            return False
+        w1, _, mid, w3, _ = pk
+        return (len(mid) == 1 and w1.shape[1] == 512 and obs.shape[1] <= 512 and w3.shape[2] <= 32
+                and obs.dtype == torch.float32 and obs.stride(1) == 1
+                and (FUSED_MLP_MAX_ROWS is None or obs.shape[0] <= FUSED_MLP_MAX_ROWS))
 
     @torch.no_grad()
     def net_forward(self, obs, which):
@@ -164,13 +179,12 @@ class ActorCritic(nn.Module):
             return self(obs)[which]
         w1, b1, mid, w3, b3 = pk
         H = w1.shape[1] // 2
-        if (FUSED_MLP and obs.is_cuda and len(mid) == 1 and H == 256 and obs.shape[1] <= 512
-                and w3.shape[2] <= 32 and obs.dtype == torch.float32 and obs.stride(1) == 1):
-            # one fused MFMA launch (ppo.hip mlp2_fwd_kernel) instead of three GEMMs
-            A = w3.shape[2] if which == 0 else 1
-            out = mlp2_forward(obs, w1[:, which * H:(which + 1) * H], b1[which * H:(which + 1) * H].contiguous(),
-                               mid[0][0][which], mid[0][1][which, 0].contiguous(), w3[which], b3[which, 0].contiguous(),
-                               A)
+        if self._fused_mlp_ok(obs):
+            # one fused MFMA launch (ppo.hip mlp2_fwd_kernel) instead of three GEMMs, reading the
+            # nn.Linear weights as they are ([out][in]: the reduction index contiguous)
+            net, head = (self.pi_net, self.action_net) if which == 0 else (self.vf_net, self.value_net)
+            l1, l2 = self._hidden(net)
+            out = mlp2_forward(obs, l1.weight, l1.bias, l2.weight, l2.bias, head.weight, head.bias)
             return out if which == 0 else out[:, 0]
         act = (lambda b, x, w: torch._addmm_activation(b, x, w)) if obs.is_cuda else (  # noqa: E731
             lambda b, x, w: torch.addmm(b, x, w).relu_())

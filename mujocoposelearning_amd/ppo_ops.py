@@ -264,17 +264,20 @@ def mlp_forward(seq, x):
     return x
 
 
-def mlp2_forward(x, w1, b1, w2, b2, w3, b3, out_cols):
-    """Fused forward of one packed 2-hidden-layer (256) ReLU MLP through hs_mlp2_forward
-    (ppo.hip: MFMA tiles, one launch): x [N, D] (row stride >= D), w1 [D, ld1] / w2 [256, 256] /
-    w3 [256, ld3] row-major [in][out] views of pack_heads' weights, out [N, out_cols] float32."""
+def mlp2_forward(x, w1, b1, w2, b2, w3, b3):
+    """Fused forward of one 2-hidden-layer (256) ReLU MLP through hs_mlp2_forward (ppo.hip: MFMA
+    tiles, one launch): x [N, D] (row stride >= D); w1 [256, D], w2 [256, 256], w3 [A, 256] in
+    nn.Linear's [out][in] layout (unit column stride), b1 / b2 [256], b3 [A] contiguous; returns
+    out [N, A] float32."""
     from . import _lib
     N, D = x.shape
-    assert x.stride(1) == 1 and w1.stride(1) == 1 and w2.is_contiguous() and w3.stride(1) == 1
-    out = torch.empty(N, out_cols, dtype=torch.float32, device=x.device)
+    A = w3.shape[0]
+    assert x.stride(1) == 1 and w1.stride(1) == 1 and w2.stride(1) == 1 and w3.stride(1) == 1
+    assert w1.shape == (256, D) and w2.shape == (256, 256) and w3.shape[1] == 256
+    out = torch.empty(N, A, dtype=torch.float32, device=x.device)
     _lib.check(_lib.lib().hs_mlp2_forward(x.data_ptr(), x.stride(0), D, N, w1.data_ptr(), w1.stride(0), b1.data_ptr(),
-                                          w2.data_ptr(), b2.data_ptr(), w3.data_ptr(), w3.stride(0), b3.data_ptr(),
-                                          out_cols, out.data_ptr(), out_cols,
+                                          w2.data_ptr(), w2.stride(0), b2.data_ptr(), w3.data_ptr(), w3.stride(0),
+                                          b3.data_ptr(), A, out.data_ptr(), A,
                                           torch.cuda.current_stream(x.device).cuda_stream))
     return out
 

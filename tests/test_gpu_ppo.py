@@ -508,11 +508,13 @@ def test_ppo_deep_net_arch_trains_on_gpu():
     env.close()
 
 
-@pytest.mark.parametrize("N,D", [(4096, 352), (1000, 350), (33, 7)])
+@pytest.mark.parametrize("N,D", [(4096, 352), (1000, 350), (33, 7), (257, 100), (20000, 352), (9001, 350)])
 def test_fused_mlp_forward_matches_gemm_chain(N, D):
-    """hs_mlp2_forward (ppo.hip mlp2_fwd_kernel: MFMA f32 tiles, one launch) == the packed GEMM chain
-    of ActorCritic.net_forward for the pi mean and the vf value; odd row counts and input widths
-    (the 16-row tile and the K padding)."""
+    """hs_mlp2_forward (ppo.hip mlp2_fwd_kernel: MFMA f32 tiles, one launch, the nn.Linear weights
+    read in place) == the packed GEMM chain of ActorCritic.net_forward (torch fp32) for the pi mean
+    and the vf value, within 1e-4 relative; odd row counts and input widths: the 16-row tile, a
+    partial last k-group (350, 7, 100), element loads for rows that are not 16-byte aligned (350, 7)
+    and no full k-group at all (7); above 8192 rows the two-row-block instance (20000, 9001)."""
     from mujocoposelearning_amd import ppo as P
     torch.manual_seed(0)
     pol = P.ActorCritic(D, 21, [256, 256], [256, 256], torch.nn.ReLU).cuda()
