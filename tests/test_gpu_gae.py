@@ -27,8 +27,10 @@ def _device(*xs):
     return [torch.tensor(x, device="cuda") for x in xs]
 
 
-@pytest.mark.parametrize("T,N", [(37, 300), (8, 64), (1, 5), (9, 257), (64, 1)])
+@pytest.mark.parametrize("T,N", [(37, 300), (8, 64), (1, 5), (9, 257), (64, 1), (257, 300), (1000, 70), (256, 1),
+                                 (2048, 130)])
 def test_gae_kernel_matches_sb3_restatement(T, N):
+    """T >= 256 takes the three-launch path (gae.hip GAE_SPLIT_T): (257, 300) ends on a one-step chunk."""
     from mujocoposelearning_amd.ppo import gae_device
     r, v, st, lv, ld = _inputs(T, N, seed=T * 1000 + N)
     ea, er = _sb3_gae(r.astype(np.float64), v.astype(np.float64), st.astype(np.float64),
