@@ -2864,6 +2864,9 @@ __global__ __launch_bounds__(64, 1) void step_kernel_wide(KArgs<T> /* read via k
   const KPtr<T> ka = (KPtr<T>)__builtin_amdgcn_kernarg_segment_ptr();
   int* redo = ka->b.redo;
   const int count = redo[0];
+  // nothing deferred (the usual case): every wave reads 0 and leaves; the list and its read counter
+  // are already clear, so no fence and no atomic (32 of them on one word cost ~2 us per launch)
+  if (count == 0) return;
   for (int base = 2 * blockIdx.x; base < count; base += 2 * gridDim.x)
     step_pair<T, NV, PGS, Wide>(ka, smem, pcache, base + (threadIdx.x >= HL ? 1 : 0), count, redo + 2, 0,
                                 ka->p.nsub, 0);
