@@ -43,12 +43,34 @@ def main():
         print("no epoch graph")
         return
     path = os.path.join(out, "epoch_graph.dot")
-    ge.debug_dump(path)
-    text = open(path).read()
+    try:
+        ge.debug_dump(path)
+        text = open(path).read()
+    except (RuntimeError, OSError) as e:   # the DOT dump is not available on every runtime
+        print("no DOT dump:", e)
+        text = ""
     kinds = collections.Counter(re.findall(r'(KERNEL|MEMSET|MEMCPY|EVENT_RECORD|WAIT_EVENT|EMPTY|HOST|GRAPH|'
                                            r'MEM_ALLOC|MEM_FREE)', text))
     print("node kinds:", dict(kinds))
     print("dot bytes:", len(text))
+    # host cost of a replay against its GPU time: is the update's graph replay submission-bound?
+    import time
+    perm = torch.randperm(ppo.n_steps * env.num_envs, device="cuda")
+    ppo._g_perm.copy_(perm)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(2):
+        ge.replay()
+    torch.cuda.synchronize()
+    ev0.record()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        ge.replay()
+    t1 = time.perf_counter()
+    ev1.record()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    print(f"5 epoch replays: host submit {1e3 * (t1 - t0):.2f} ms, GPU {ev0.elapsed_time(ev1):.2f} ms, "
+          f"wall {1e3 * (t2 - t0):.2f} ms; kernels per replay {kinds.get('KERNEL', 0)}")
     env.close()
 
 
