@@ -289,7 +289,8 @@ int hs_batch_counters(const hs_batch* b, uint64_t* wide_reruns);
 /* GAE(gamma, lambda) reverse scan over a device rollout buffer, SB3 semantics: [T][N] float32
  * rewards, values, episode_starts; [N] last_values, last_dones; writes [T][N] advantages and
  * returns (= advantages + values).  All pointers are device memory on the current device;
- * asynchronous on `stream`. */
+ * asynchronous on `stream`.  advantages / returns must not overlap the inputs: for T >= 256 the scan
+ * runs as three launches that keep their per-chunk maps and carries in those output rows. */
 int hs_gae(const float* rewards, const float* values, const float* episode_starts, const float* last_values,
            const float* last_dones, float* advantages, float* returns, int T, int N, float gamma, float gae_lambda,
            void* stream);
