@@ -94,6 +94,14 @@ def test_trainer_entry_points_validate_arguments():
     assert "null" in err(L.hs_relu_grad_colsum(None, None, 4, 4, None, None, None))
     assert "null" in err(L.hs_colsum_pair(None, 4, 4, None, None, 4, 4, None, None))
     assert "negative" in err(L.hs_gae(None, None, None, None, None, None, None, -1, 4, 0.99, 0.95, None))
+    # the fused policy forward: nn.Linear layouts (ld1 >= D, ld2 / ld3 >= 256), A <= 32, D <= 512
+    mlp = lambda D, N, ld1, ld2, ld3, A: L.hs_mlp2_forward(None, D, D, N, None, ld1, None, None, ld2, None,  # noqa: E731
+                                                           None, ld3, None, A, None, A, None)
+    assert "ld1 >= D" in err(mlp(352, 8, 256, 256, 256, 21))
+    assert "A <= 32" in err(mlp(352, 8, 352, 256, 256, 33))
+    assert "D <= 512" in err(mlp(600, 8, 600, 256, 256, 21))
+    assert "null" in err(mlp(352, 8, 352, 256, 256, 21))
+    assert mlp(352, 0, 352, 256, 256, 21) == 0
     # empty problems are no-ops, not errors
     assert L.hs_ppo_loss(None, None, None, None, None, None, 0, 0.2, None, None, None, None) == 0
     assert L.hs_colsum(None, 0, 0, None, None, None, None) == 0

@@ -535,6 +535,31 @@ def test_fused_mlp_forward_matches_gemm_chain(N, D):
         assert torch.allclose(a, b, rtol=1e-4, atol=1e-4 * (1 + float(b.abs().max()))), float((a - b).abs().max())
 
 
+def test_fused_mlp_abi_with_padded_strides():
+    """hs_mlp2_forward through the C ABI on strided operands: input rows of 400 floats holding 352
+    features, weight rows padded (ld1 = 360, ld2 = ld3 = 264), an output of stride 32 holding 21
+    columns (the padding untouched) -- against the fp32 torch chain on the same values."""
+    import torch
+    from mujocoposelearning_amd import _lib
+    torch.manual_seed(1)
+    N, D, H, A = 1000, 352, 256, 21
+    xs = torch.randn(N, 400, device="cuda")
+    w1s, w2s, w3s = (torch.randn(H, 360, device="cuda") * 0.05, torch.randn(H, 264, device="cuda") * 0.05,
+                     torch.randn(A, 264, device="cuda") * 0.05)
+    b1, b2, b3 = (torch.randn(H, device="cuda") * 0.1, torch.randn(H, device="cuda") * 0.1,
+                  torch.randn(A, device="cuda") * 0.1)
+    out = torch.full((N, 32), 7.0, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    assert _lib.lib().hs_mlp2_forward(xs.data_ptr(), 400, D, N, w1s.data_ptr(), 360, b1.data_ptr(), w2s.data_ptr(),
+                                      264, b2.data_ptr(), w3s.data_ptr(), 264, b3.data_ptr(), A, out.data_ptr(), 32,
+                                      st) == 0
+    x, w1, w2, w3 = xs[:, :D], w1s[:, :D], w2s[:, :H], w3s[:, :H]
+    ref = torch.relu(torch.relu(x @ w1.t() + b1) @ w2.t() + b2) @ w3.t() + b3
+    torch.cuda.synchronize()
+    assert torch.allclose(out[:, :A], ref, rtol=1e-4, atol=1e-4 * (1 + float(ref.abs().max())))
+    assert torch.all(out[:, A:] == 7.0)
+
+
 def test_learn_raises_on_a_lost_handoff_and_warns_on_bad_states():
     """PPO.learn reduces the env's warning counters once per rollout (include/hsim.h HS_WARN_*): a
     lost chunk-queue hand-off (forced with the hs_debug_lose_handoff hook on a queued 4096-env fp64
