@@ -612,7 +612,7 @@ def main():
     if args.train_iters > 0:
         from mujocoposelearning_amd.ppo import PPO
         e = make_env(args.precision, 8000)
-        tk = dict(n_steps=32, batch_size=32768, n_epochs=4, learning_rate=3e-4,
+        tk = dict(n_steps=32, batch_size=32768, n_epochs=4, learning_rate=3e-4, stagger_episodes=True,
                   policy_kwargs={"net_arch": {"pi": [256, 256], "vf": [256, 256]}, "activation_fn": "ReLU"})
         ppo = PPO(e, seed=0, world_size=world, rank=rank, **tk)
         ppo.learn(ppo.num_timesteps + n * tk["n_steps"] * world)          # warm-up iteration

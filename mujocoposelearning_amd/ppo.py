@@ -243,7 +243,7 @@ class PPO:
 
     def __init__(self, env, learning_rate=3e-4, n_steps=2048, batch_size=64, n_epochs=10, gamma=0.99,
                  gae_lambda=0.95, clip_range=0.2, ent_coef=0.0, vf_coef=0.5, max_grad_norm=0.5,
-                 policy_kwargs=None, seed=0, world_size=None, rank=None, sync_grads=None):
+                 policy_kwargs=None, seed=0, world_size=None, rank=None, sync_grads=None, stagger_episodes=False):
         import torch.distributed as dist
         if world_size is None:
             world_size = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
@@ -293,6 +293,10 @@ class PPO:
             self.buf.update(boot=torch.zeros(T, N, dtype=torch.bool, device=dev),
                             tobs=torch.zeros(T, N, D, dtype=f, device=dev))
         self.obs = env.reset_tensors().float().clone()
+        # stagger_episodes: spread the envs' episode clocks after this first reset (not an SB3 option;
+        # HumanoidVecEnv.stagger_episode_clocks) so that short rollouts see every episode phase
+        if stagger_episodes:
+            env.stagger_episode_clocks()
         self.episode_start = torch.ones(N, dtype=f, device=dev)
         self.num_timesteps = 0
         self.ep_returns = []

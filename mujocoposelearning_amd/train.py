@@ -96,7 +96,10 @@ def train_humanoid(env_kwargs: dict, ppo_kwargs: dict, xml_path: str = DEFAULT_X
     if env.graph_safe:     # device reward: the trainer reads neither the aux row nor the ctrl copy
         env.batch.configure(aux=False, ctrl=False)
     kw = _resolve_activation(ppo_kwargs)
-    model = PPO(env, seed=seed, world_size=world, rank=rank, **kw)
+    # env_kwargs["stagger_episodes"] (hsim option, off by default: SubprocVecEnv resets every env
+    # together): spread the episode clocks so that short rollouts see every episode phase
+    model = PPO(env, seed=seed, world_size=world, rank=rank,
+                stagger_episodes=bool(env_kwargs.get("stagger_episodes", False)), **kw)
     model.learn(total_timesteps=env_kwargs.get("total_timesteps", 20_000_000), callback=callback)
     if storage_path is not None and rank == 0:
         os.makedirs(storage_path, exist_ok=True)

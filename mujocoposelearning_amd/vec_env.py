@@ -194,6 +194,29 @@ class HumanoidVecEnv(_Base):
     def reset(self):
         return self.reset_tensors().double().cpu().numpy()
 
+    def episode_length(self):
+        """Env steps per episode: until time >= duration (custom_env.py:213; the reset's one mj_step
+        already took time to one timestep), at most the 750-step truncation (custom_env.py:203)."""
+        dt = self.model.opt.timestep
+        k = int(np.ceil((self.duration - dt) / (self.frame_skip * dt) - 1e-9))
+        return max(1, min(750, k))
+
+    def stagger_episode_clocks(self):
+        """Spread the envs' episode clocks over one episode: env i carries on as if it were
+        floor(i L / N) of the L env steps into its current episode (time and step count advanced,
+        state untouched), so its first episode ends early and from then on the envs reset at evenly
+        spread times.  A training-schedule choice, not SubprocVecEnv semantics: with n_steps x n_envs
+        rollouts far shorter than an episode (32 x 4096) it lets every rollout see every phase of an
+        episode, as the reference's 8 envs x 2048 steps (three whole episodes per env) do
+        (profiles/learning_curve_r5.md: all seeds stand with it, few without)."""
+        import torch
+        n, L = self.num_envs, self.episode_length()
+        k = np.floor(np.arange(n) * L / n)
+        dt = self.model.opt.timestep
+        t = self.batch.t
+        t["time"].copy_(torch.as_tensor(dt + k * self.frame_skip * dt, dtype=t["time"].dtype))
+        t["step_count"].copy_(torch.as_tensor(k, dtype=t["step_count"].dtype))
+
     # ---------------------------------------------------------------- host reset-noise streams
     def _draw_noise(self, envs):
         """The next reset's raw noise of each env in ``envs`` from its own stream, in
