@@ -297,6 +297,12 @@ class PPO:
         # HumanoidVecEnv.stagger_episode_clocks) so that short rollouts see every episode phase
         if stagger_episodes:
             env.stagger_episode_clocks()
+        elif hasattr(env, "episode_length") and N > 1 and 2 * n_steps < env.episode_length():
+            import warnings
+            warnings.warn(f"PPO: rollouts of n_steps={n_steps} cover a small part of the {env.episode_length()}-step "
+                          "episode and every env resets together, so each rollout sees one phase of it; "
+                          "stagger_episodes=True spreads the envs' episode clocks (profiles/learning_curve_r5.md)",
+                          RuntimeWarning, stacklevel=2)
         self.episode_start = torch.ones(N, dtype=f, device=dev)
         self.num_timesteps = 0
         self.ep_returns = []
