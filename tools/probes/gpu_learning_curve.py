@@ -1,7 +1,7 @@
 """Learning-curve sanity of the on-device PPO (SB3 is not importable, so the trainer
 is judged by the stand reward rising).  bench.py's train config: 4096 envs, n_steps 32,
 batch 32768, 4 epochs, lr 3e-4, MLP[256,256] ReLU (batch and epochs overridable).
-python tools/probes/gpu_learning_curve.py [iters] [stand|kneeling] [fp32|fp64] [seed] [batch] [epochs] [stagger]
+python tools/probes/gpu_learning_curve.py [iters] [stand|kneeling] [fp32|fp64] [seed] [batch] [epochs] [stagger] [lr]
 stagger = 1: spread the envs' episode clocks over the episode after the first reset (env i starts
 i/N into it, as bench.py's window and the reference's 8 envs x 2048 steps per rollout do); without it
 every env resets together and a 32-step rollout sees one phase of the episode."""
@@ -21,10 +21,10 @@ from mujocoposelearning_amd.vec_env import HumanoidVecEnv  # noqa: E402
 XML = os.path.join(ROOT, "mujocoposelearning_amd", "assets", "humanoid.xml")
 
 
-def main(iters=400, reward="stand", precision="fp32", seed=0, batch=32768, epochs=4, stagger=0):
+def main(iters=400, reward="stand", precision="fp32", seed=0, batch=32768, epochs=4, stagger=0, lr=3e-4):
     env = HumanoidVecEnv({"model_path": XML, "duration": 10.0, "reward_config": {"type": reward}, "frame_skip": 3},
                          n_envs=4096, model=HsModel(XML), seed=seed, precision=precision)
-    ppo = PPO(env, n_steps=32, batch_size=batch, n_epochs=epochs, learning_rate=3e-4, seed=seed,
+    ppo = PPO(env, n_steps=32, batch_size=batch, n_epochs=epochs, learning_rate=lr, seed=seed,
               policy_kwargs={"activation_fn": "ReLU", "net_arch": {"pi": [256, 256], "vf": [256, 256]}})
     if stagger:
         b, n, ep = env.batch, env.num_envs, 667
@@ -53,4 +53,4 @@ if __name__ == "__main__":
     main(int(sys.argv[1]) if len(sys.argv) > 1 else 400, sys.argv[2] if len(sys.argv) > 2 else "stand",
          sys.argv[3] if len(sys.argv) > 3 else "fp32", int(sys.argv[4]) if len(sys.argv) > 4 else 0,
          int(sys.argv[5]) if len(sys.argv) > 5 else 32768, int(sys.argv[6]) if len(sys.argv) > 6 else 4,
-         int(sys.argv[7]) if len(sys.argv) > 7 else 0)
+         int(sys.argv[7]) if len(sys.argv) > 7 else 0, float(sys.argv[8]) if len(sys.argv) > 8 else 3e-4)
