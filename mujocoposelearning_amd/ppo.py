@@ -578,13 +578,13 @@ class PPO:
         """SB3 PPO.train's per-minibatch loss (clipped surrogate + vf_coef MSE - ent_coef entropy)."""
         mean, v = self.policy(obs[idx])
         logp = self.policy._logp(mean, act[idx])
-        ent_mean = self.policy.entropy()            # = evaluate()'s per-sample entropy, averaged
         if logp.is_cuda:                            # fused HIP loss (same formulas as below)
             pg, vf = ppo_loss(logp, v, idx, adv, ret, old_logp, self.clip_range)
-            loss = pg + self.vf_coef * vf
-            if self.ent_coef:                       # SB3's default ent_coef 0: the term has no gradient
-                loss = loss - self.ent_coef * ent_mean
+            loss = torch.add(pg, vf, alpha=self.vf_coef)
+            if self.ent_coef:                       # SB3's default ent_coef 0: no term, no launches
+                loss = loss - self.ent_coef * self.policy.entropy()
             return loss, pg, vf
+        ent_mean = self.policy.entropy()            # = evaluate()'s per-sample entropy, averaged
         a = adv[idx]
         if a.numel() > 1:
             a = (a - a.mean()) / (a.std() + 1e-8)
