@@ -35,6 +35,8 @@
  *                           surrogate, value MSE (stable_baselines3 2.3.2 ppo/ppo.py) and its backward
  *   hs_adam_clip         <- torch.nn.utils.clip_grad_norm_(max_grad_norm) + torch.optim.Adam.step of
  *                           SB3 PPO.train (ppo.py: max_grad_norm 0.5, Adam eps 1e-5)
+ *   hs_dgrad_mask        <- the input gradient of each layer fed by a ReLU, fused with that ReLU's
+ *                           backward (same loss.backward())
  *   hs_relu_grad_colsum, hs_colsum_pair <- the ReLU backward + bias / weight-gradient sums of the
  *                           same loss.backward() (fewer passes and launches)
  *   hs_colsum            <- the bias-gradient and split-K weight-gradient reductions of the PPO
@@ -376,6 +378,19 @@ int hs_adam_clip(int nt, float* const* params, const float* const* grads, float*
 uint64_t hs_colsum_partial_rows(uint64_t rows, uint64_t cols);
 int hs_relu_grad_colsum(const float* g, const float* y, uint64_t rows, uint64_t cols, float* gm, float* partial,
                         void* stream);
+/* Input gradient of a Linear layer fed by a ReLU, fused with that ReLU's backward and the first
+ * pass of its bias gradient: GX[B][N] = (G W) masked by X > 0, partial[p][N] = column sums of GX
+ * over row block p, p < hs_dgrad_mask_partial_rows(B, K).  G [B][K] (row stride ldg) is the layer's
+ * output gradient, W [K][N] its weight as nn.Linear stores it ([out][in], row stride ldw), X [B][N]
+ * (ldx) its input = the previous layer's ReLU output; GX is contiguous.  N = 256; K <= 32 (a policy
+ * or value head) or K % 16 == 0, K <= 512 (a hidden layer: fp32 MFMA, G rows 16-byte aligned, and
+ * `workspace` of hs_dgrad_mask_workspace(K) floats for W transposed; may be NULL when that is 0).
+ * Replaces `g @ w` + threshold_backward + the bias sum's first read of SB3's loss.backward() through
+ * mlp_extractor (policies.py, SB3 2.3.2).  Asynchronous on `stream`. */
+uint64_t hs_dgrad_mask_partial_rows(int B, int K);
+uint64_t hs_dgrad_mask_workspace(int K);
+int hs_dgrad_mask(const float* G, int ldg, int K, const float* W, int ldw, const float* X, int ldx, int B, int N,
+                  float* GX, float* partial, float* workspace, void* stream);
 /* Two single-pass column sums in one launch: out0[c] = sum_r x0[r][c] ([rows0][cols0]) and
  * out1[c] = sum_r x1[r][c] ([rows1][cols1]) -- for short matrices (split-K slices, partials). */
 int hs_colsum_pair(const float* x0, uint64_t rows0, uint64_t cols0, float* out0, const float* x1, uint64_t rows1,

@@ -118,6 +118,9 @@ def lib():
         "hs_mlp2_forward": (i, [vp, i, i, i, vp, i, vp, vp, i, vp, vp, i, vp, i, vp, i, vp]),
         "hs_colsum_partial_rows": (u64, [u64, u64]),
         "hs_relu_grad_colsum": (i, [vp, vp, u64, u64, vp, vp, vp]),
+        "hs_dgrad_mask_partial_rows": (u64, [i, i]),
+        "hs_dgrad_mask_workspace": (u64, [i]),
+        "hs_dgrad_mask": (i, [vp, i, i, vp, i, vp, i, i, i, vp, vp, vp, vp]),
         "hs_colsum_pair": (i, [vp, u64, u64, vp, vp, u64, u64, vp, vp]),
         "hs_colsum_workspace": (u64, [u64, u64]),
         "hs_colsum": (i, [vp, u64, u64, vp, vp, vp, vp]),
@@ -137,7 +140,8 @@ EXPORTED = ("hs_model_load", "hs_model_free", "hs_model_field", "hs_batch_create
             "hs_physics_step", "hs_state_io", "hs_kinematics", "hs_set_debug", "hs_debug_lose_handoff", "hs_get_debug", "hs_synchronize", "hs_batch_counters", "hs_gae",
             "hs_ppo_act", "hs_ppo_post", "hs_gauss_logp", "hs_gauss_logp_grad",
             "hs_ppo_loss_workspace", "hs_ppo_loss", "hs_ppo_loss_grad", "hs_adam_workspace", "hs_adam_clip",
-            "hs_mlp2_forward", "hs_colsum_partial_rows", "hs_relu_grad_colsum", "hs_colsum_pair",
+            "hs_mlp2_forward", "hs_colsum_partial_rows", "hs_relu_grad_colsum", "hs_dgrad_mask_partial_rows",
+            "hs_dgrad_mask_workspace", "hs_dgrad_mask", "hs_colsum_pair",
             "hs_colsum_workspace", "hs_colsum", "hs_last_error", "hs_version")
 
 

@@ -927,6 +927,24 @@ int hs_relu_grad_colsum(const float* g, const float* y, uint64_t rows, uint64_t 
                                                                                                                  : -1;
 }
 
+uint64_t hs_dgrad_mask_partial_rows(int B, int K) { return hs::dgrad_mask_partial_rows(B, K); }
+uint64_t hs_dgrad_mask_workspace(int K) { return hs::dgrad_mask_workspace(K); }
+
+int hs_dgrad_mask(const float* G, int ldg, int K, const float* W, int ldw, const float* X, int ldx, int B, int N,
+                  float* GX, float* partial, float* workspace, void* stream) {
+  if (B < 0 || N != 256 || K < 1 || (K > 32 && (K % 16 != 0 || K > 512)) || ldg < K || ldw < N || ldx < N)
+    return fail("hs_dgrad_mask: need B >= 0, N == 256, K <= 32 or K % 16 == 0 with K <= 512, ldg >= K, ldw >= N, "
+                "ldx >= N");
+  if (B == 0) return 0;
+  if (!G || !W || !X || !GX || !partial) return fail("hs_dgrad_mask: null buffer");
+  if (K > 32 && (((uintptr_t)G & 15) || (ldg & 3))) return fail("hs_dgrad_mask: K > 32 needs 16-byte aligned G rows");
+  if (hs::dgrad_mask_workspace(K) && !workspace) return fail("hs_dgrad_mask: workspace required");
+  return hip_ok(hs::launch_dgrad_mask(G, ldg, K, W, ldw, X, ldx, B, N, GX, partial, workspace, (hipStream_t)stream),
+                "dgrad_mask kernel")
+             ? 0
+             : -1;
+}
+
 int hs_colsum_pair(const float* x0, uint64_t rows0, uint64_t cols0, float* out0, const float* x1, uint64_t rows1,
                    uint64_t cols1, float* out1, void* stream) {
   if ((cols0 && (!x0 || !out0)) || (cols1 && (!x1 || !out1))) return fail("hs_colsum_pair: null buffer");

@@ -223,6 +223,12 @@ hipError_t launch_adam_clip(int nt, float* const* p, const float* const* g, floa
                             double b1, double b2, double eps, hipStream_t stream);
 // ReLU-backward + bias-gradient first pass, and a paired single-pass column sum (ppo.hip)
 size_t colsum_partial_rows(size_t rows, size_t cols);
+// (G W) masked by X > 0 and its per-workgroup column sums (ppo.hip dgrad_mask_*_kernel): the input
+// gradient of a Linear layer fed by a ReLU, fused with that ReLU's backward; N = 256
+hipError_t launch_dgrad_mask(const float* G, int ldg, int K, const float* W, int ldw, const float* X, int ldx, int B,
+                             int N, float* GX, float* partial, float* workspace, hipStream_t stream);
+size_t dgrad_mask_partial_rows(int B, int K);
+size_t dgrad_mask_workspace(int K);
 hipError_t launch_relu_colsum(const float* g, const float* y, size_t rows, size_t cols, float* gm, float* partial,
                               hipStream_t stream);
 hipError_t launch_colsum_pair(const float* x0, size_t rows0, size_t cols0, float* out0, const float* x1, size_t rows1,

@@ -30,6 +30,7 @@
 #include <algorithm>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "hs_philox.h"
 
@@ -402,7 +403,7 @@ __global__ void adam_step_kernel(AdamArgs a) {
 // through LDS.  grid.y splits the rows into chunks whose partial rows a second launch
 // (grid.y = 1) sums: fixed summation order, so results are run-to-run deterministic (no float
 // atomics), and every lane's dependent-load chain stays short.
-constexpr int CS_COLS = 64, CS_PHASES = 16;
+constexpr int CS_COLS = 64, CS_PHASES = 16, CS_PAIR_COLS1 = 16;
 
 __global__ __launch_bounds__(CS_COLS* CS_PHASES) void colsum_kernel(const float* __restrict__ x, size_t rows,
                                                                      size_t cols, size_t rows_per_chunk,
@@ -493,32 +494,43 @@ __global__ __launch_bounds__(CS_COLS* CS_PHASES) void relu_colsum_kernel(const f
 }
 
 // Two single-pass column sums in one launch (blocks [0, tiles0) do x0, the rest x1): a layer's
-// split-K weight-gradient finish (S rows) and its bias-gradient finish (chunk rows).
+// split-K weight-gradient finish (S rows, many columns: 64 columns x 16 row phases per block) and its
+// bias-gradient finish (hundreds of partial rows of 256 columns: 16 columns x 64 row phases per
+// block, so that 16 blocks share the rows instead of 4 walking them).  Four independent
+// accumulators per thread keep four loads in flight.
 __global__ __launch_bounds__(CS_COLS* CS_PHASES) void colsum_pair_kernel(const float* __restrict__ x0, size_t rows0,
                                                                           size_t cols0, float* __restrict__ out0,
                                                                           const float* __restrict__ x1, size_t rows1,
                                                                           size_t cols1, float* __restrict__ out1,
                                                                           unsigned tiles0) {
-  __shared__ float part[CS_PHASES][CS_COLS];
+  __shared__ float part[CS_COLS * CS_PHASES];
   const bool second = blockIdx.x >= tiles0;
   const float* __restrict__ x = second ? x1 : x0;
   const size_t rows = second ? rows1 : rows0, cols = second ? cols1 : cols0;
   float* __restrict__ out = second ? out1 : out0;
-  const int lane = threadIdx.x, ph = threadIdx.y;
-  const size_t c = (size_t)(second ? blockIdx.x - tiles0 : blockIdx.x) * CS_COLS + lane;
-  float a = 0.f;
-  if (c < cols)
-    for (size_t r = ph; r < rows; r += CS_PHASES) a += x[r * cols + c];
-  part[ph][lane] = a;
+  const int t = threadIdx.y * CS_COLS + threadIdx.x;
+  const int w = second ? CS_PAIR_COLS1 : CS_COLS, nph = CS_COLS * CS_PHASES / w;   // columns, row phases per block
+  const int lane = t % w, ph = t / w;
+  const size_t c = (size_t)(second ? blockIdx.x - tiles0 : blockIdx.x) * w + lane;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (c < cols) {
+    size_t r = ph;
+    for (; r + 3 * nph < rows; r += 4 * nph) {
+      a0 += x[r * cols + c];
+      a1 += x[(r + nph) * cols + c];
+      a2 += x[(r + 2 * nph) * cols + c];
+      a3 += x[(r + 3 * nph) * cols + c];
+    }
+    for (; r < rows; r += nph) a0 += x[r * cols + c];
+  }
+  part[ph * w + lane] = (a0 + a1) + (a2 + a3);
   __syncthreads();
   if (ph == 0 && c < cols) {
-    float t = 0.f;
-#pragma unroll
-    for (int k = 0; k < CS_PHASES; k++) t += part[k][lane];
-    out[c] = t;
+    float s = 0.f;
+    for (int k = 0; k < nph; k++) s += part[k * w + lane];
+    out[c] = s;
   }
 }
-
 
 // ------------------------------------------------------------------ fused 2-hidden-layer MLP forward
 // out = relu(relu(X W1' + b1) W2' + b2) W3' + b3 for one policy net (PPO rollout: the pi net's mean per
@@ -710,6 +722,140 @@ __global__ __launch_bounds__(MLP_TPB) void mlp2_fwd_kernel(const float* __restri
   }
 }
 
+// ------------------------------------------------------------------ input gradient + ReLU mask
+// The backward of a Linear layer whose input x is the previous layer's ReLU output:
+//   GX = (G W) ⊙ (X > 0),  partial[wg][n] = sum of GX over the workgroup's rows
+// G [B][K] (ldg) is the layer's output gradient, W [K][N] its nn.Linear weight ([out][in]), X [B][N]
+// (ldx) its input.  The mask is the previous layer's ReLU backward and the partial sums its bias
+// gradient's first pass, so that layer needs no separate pass over [B][N] (autograd writes G W,
+// then threshold_backward reads it with X and writes it again, then the bias sum reads it).
+// N = 256 (the hidden width).
+// K % 16 == 0 (hidden layers, K = 256): the MFMA tiles of mlp2_fwd_kernel on Wt = W' ([N][K], k
+// contiguous: dg_transpose_kernel, once per call) so that a lane's B operand of a k-group is one
+// 16-byte load; the accumulators go through LDS so that the mask read of X, the GX store and the
+// column sums run on whole rows (16-byte accesses) instead of the MFMA's 64-byte column slivers.
+// K <= 32 (the heads: 21 actions, 1 value): VALU, the G tile in LDS, a float4 of columns per thread.
+constexpr int DG_N = 256, DG_RB4_ROWS = 16384;
+
+// Wt[n][k] = W[k][n] (W [K][ldw], Wt [N][K]): 32 x 32 tiles through LDS
+__global__ __launch_bounds__(256) void dg_transpose_kernel(const float* __restrict__ W, int ldw, int K, int N,
+                                                           float* __restrict__ Wt) {
+  __shared__ float t[32][33];
+  const int k0 = blockIdx.y * 32, n0 = blockIdx.x * 32, tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int r = ty; r < 32; r += 8)
+    if (k0 + r < K && n0 + tx < N) t[r][tx] = W[(size_t)(k0 + r) * ldw + n0 + tx];
+  __syncthreads();
+  for (int r = ty; r < 32; r += 8)
+    if (n0 + r < N && k0 + tx < K) Wt[(size_t)(n0 + r) * K + k0 + tx] = t[tx][r];
+}
+
+// mask, store and column-sum an [R][DG_N] gradient tile held in LDS (row stride st): thread t owns
+// columns 4 (t % 64) .. + 3 of rows t / 64 + TPB / 64 i; the per-thread sums reduce through `red`
+// ([TPB / 64][64] float4, may alias the tile after the barrier)
+template <int R, int TPB, bool XVEC>
+__device__ __forceinline__ void dg_finish(const float* tile, int st, const float* __restrict__ X, int ldx, int B,
+                                          int row0, float* __restrict__ GX, float* __restrict__ part, f32x4* red) {
+  constexpr int P = TPB / 64;
+  const int c4 = threadIdx.x & 63, rp = threadIdx.x >> 6;
+  f32x4 xv[R / P], gv[R / P];
+#pragma unroll
+  for (int i = 0; i < R / P; i++) {   // every X load of the thread in flight at once
+    const int row = row0 + rp + P * i;
+    const float* xr = X + (size_t)(row < B ? row : 0) * ldx + 4 * c4;
+    xv[i] = mlp_ld4<XVEC>(xr);
+    gv[i] = *reinterpret_cast<const f32x4*>(tile + (rp + P * i) * st + 4 * c4);
+  }
+  f32x4 cs = {0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < R / P; i++) {
+    const int row = row0 + rp + P * i;
+    f32x4 v;
+#pragma unroll
+    for (int q = 0; q < 4; q++) v[q] = xv[i][q] > 0.f ? gv[i][q] : 0.f;
+    if (row < B) {
+      *reinterpret_cast<f32x4*>(GX + (size_t)row * DG_N + 4 * c4) = v;
+      cs += v;
+    }
+  }
+  __syncthreads();   // the tile is read: red may alias it
+  red[rp * 64 + c4] = cs;
+  __syncthreads();
+  if (rp == 0) {
+    f32x4 tsum = red[c4];
+#pragma unroll
+    for (int p = 1; p < P; p++) tsum += red[p * 64 + c4];
+    *reinterpret_cast<f32x4*>(part + (size_t)blockIdx.x * DG_N + 4 * c4) = tsum;
+  }
+}
+
+__host__ __device__ constexpr int dg_stride(int K) { return (K > DG_N ? K : DG_N) + 4; }
+
+template <int RB, bool XVEC>
+__global__ __launch_bounds__(MLP_TPB) void dgrad_mask_mfma_kernel(const float* __restrict__ G, int ldg, int K,
+                                                                  const float* __restrict__ Wt,
+                                                                  const float* __restrict__ X, int ldx, int B,
+                                                                  float* __restrict__ GX, float* __restrict__ part) {
+  constexpr int R = 16 * RB;
+  extern __shared__ __attribute__((aligned(16))) float dg_lds[];
+  const int sg = dg_stride(K);                // G tile, then the output tile: 16-byte aligned rows
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int ar = lane & 15, ak = lane >> 4;
+  const int row0 = blockIdx.x * R;
+  for (int r = threadIdx.x >> 5; r < R; r += MLP_TPB / 32) {   // 32 threads per row, 16-byte loads
+    const bool live = row0 + r < B;
+    const float* gr = G + (size_t)(live ? row0 + r : 0) * ldg;
+    for (int c = 4 * (threadIdx.x & 31); c < K; c += 128)
+      *reinterpret_cast<f32x4*>(dg_lds + r * sg + c) = live ? *reinterpret_cast<const f32x4*>(gr + c)
+                                                            : f32x4{0, 0, 0, 0};
+  }
+  __syncthreads();
+  const int c0 = wave * 32 + ar;
+  f32x4 acc[RB][2] = {};
+  const float* w0 = Wt + (size_t)c0 * K + 4 * ak;
+  mlp_groups<true, RB>(dg_lds + ar * sg + 4 * ak, 16 * sg, w0, w0 + (size_t)16 * K, K >> 4, acc);
+  __syncthreads();   // every wave is done with the G tile
+#pragma unroll
+  for (int t = 0; t < 2; t++)
+#pragma unroll
+    for (int rb = 0; rb < RB; rb++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) dg_lds[(16 * rb + 4 * ak + r) * sg + c0 + 16 * t] = acc[rb][t][r];
+  __syncthreads();
+  dg_finish<R, MLP_TPB, XVEC>(dg_lds, sg, X, ldx, B, row0, GX, part, reinterpret_cast<f32x4*>(dg_lds));
+}
+
+// K <= 32: 32 rows per workgroup; the G tile in LDS (each wave's row of it read as a broadcast),
+// W[k][4 c4 .. + 3] one load per k, k outer over the thread's 8 rows
+constexpr int DG_SMALL_K = 32, DG_SMALL_R = 32, DG_SMALL_TPB = 256;
+template <bool XVEC>
+__global__ __launch_bounds__(DG_SMALL_TPB) void dgrad_mask_small_kernel(const float* __restrict__ G, int ldg, int K,
+                                                                        const float* __restrict__ W, int ldw,
+                                                                        const float* __restrict__ X, int ldx, int B,
+                                                                        float* __restrict__ GX,
+                                                                        float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) float gs[DG_SMALL_R][DG_SMALL_K + 1];
+  __shared__ __attribute__((aligned(16))) f32x4 tile[DG_SMALL_R * 64];   // [R][256] floats, row stride 256
+  const int c4 = threadIdx.x & 63, rp = threadIdx.x >> 6;
+  const int row0 = blockIdx.x * DG_SMALL_R;
+  for (int e = threadIdx.x; e < DG_SMALL_R * K; e += DG_SMALL_TPB) {
+    const int r = e / K, k = e - r * K;
+    gs[r][k] = row0 + r < B ? G[(size_t)(row0 + r) * ldg + k] : 0.f;
+  }
+  __syncthreads();
+  constexpr int P = DG_SMALL_TPB / 64, RR = DG_SMALL_R / P;
+  f32x4 v[RR] = {};
+  for (int k = 0; k < K; k++) {
+    const f32x4 w = mlp_ld4<XVEC>(W + (size_t)k * ldw + 4 * c4);
+#pragma unroll
+    for (int i = 0; i < RR; i++) v[i] += gs[rp + P * i][k] * w;
+  }
+#pragma unroll
+  for (int i = 0; i < RR; i++) tile[(rp + P * i) * 64 + c4] = v[i];
+  __syncthreads();
+  dg_finish<DG_SMALL_R, DG_SMALL_TPB, XVEC>(reinterpret_cast<const float*>(tile), DG_N, X, ldx, B, row0, GX, part,
+                                            tile);
+}
+
 }  // namespace
 
 // row chunks for colsum: enough workgroups to fill the chip (~1024) with >= 32 rows each;
@@ -886,7 +1032,8 @@ hipError_t launch_relu_colsum(const float* g, const float* y, size_t rows, size_
 
 hipError_t launch_colsum_pair(const float* x0, size_t rows0, size_t cols0, float* out0, const float* x1, size_t rows1,
                               size_t cols1, float* out1, hipStream_t stream) {
-  const unsigned t0 = (unsigned)((cols0 + CS_COLS - 1) / CS_COLS), t1 = (unsigned)((cols1 + CS_COLS - 1) / CS_COLS);
+  const unsigned t0 = (unsigned)((cols0 + CS_COLS - 1) / CS_COLS),
+                 t1 = (unsigned)((cols1 + CS_PAIR_COLS1 - 1) / CS_PAIR_COLS1);
   if (t0 + t1 == 0) return hipSuccess;
   hipLaunchKernelGGL(colsum_pair_kernel, dim3(t0 + t1), dim3(CS_COLS, CS_PHASES), 0, stream, x0, rows0, cols0, out0, x1,
                      rows1, cols1, out1, t0);
@@ -920,6 +1067,71 @@ hipError_t launch_mlp2_fwd(const float* X, int ldx, int D, int N, const float* W
   if (vec) { if (RB == 2) MLP_LAUNCH(true, 2); else MLP_LAUNCH(true, 1); }
   else { if (RB == 2) MLP_LAUNCH(false, 2); else MLP_LAUNCH(false, 1); }
 #undef MLP_LAUNCH
+  return hipGetLastError();
+}
+
+// row blocks per workgroup of the MFMA instance: 16 rows below MLP_RB2_ROWS, 32 to DG_RB4_ROWS,
+// 64 above (each workgroup streams all of Wt: more rows per workgroup, less L2 traffic per row).
+// HSIM_DG_RB=1|2|4 forces one (A/B probes).
+static int dg_rb(int B) {
+  static const int forced = [] {
+    const char* e = getenv("HSIM_DG_RB");
+    const int v = e ? atoi(e) : 0;
+    return v == 1 || v == 2 || v == 4 ? v : 0;
+  }();
+  if (forced) return forced;
+  return B > DG_RB4_ROWS ? 4 : B > MLP_RB2_ROWS ? 2 : 1;
+}
+
+size_t dgrad_mask_partial_rows(int B, int K) {
+  if (B <= 0) return 0;
+  const int R = K <= DG_SMALL_K ? DG_SMALL_R : 16 * dg_rb(B);
+  return (size_t)((B + R - 1) / R);
+}
+
+size_t dgrad_mask_workspace(int K) { return K <= DG_SMALL_K ? 0 : (size_t)DG_N * K; }
+
+hipError_t launch_dgrad_mask(const float* G, int ldg, int K, const float* W, int ldw, const float* X, int ldx, int B,
+                             int N, float* GX, float* partial, float* workspace, hipStream_t stream) {
+  if (B < 0 || N != DG_N || K < 1 || (K > DG_SMALL_K && (K % 16 != 0 || K > MLP_MAXD)) || ldg < K || ldw < N ||
+      ldx < N)
+    return hipErrorInvalidValue;
+  if (B == 0) return hipSuccess;
+  const bool xvec = ((uintptr_t)X & 15) == 0 && (ldx & 3) == 0;
+  if (K <= DG_SMALL_K) {
+    const bool vec = xvec && ((uintptr_t)W & 15) == 0 && (ldw & 3) == 0;   // X and W rows 16-byte aligned
+    if (vec)
+      hipLaunchKernelGGL(dgrad_mask_small_kernel<true>, dim3((B + DG_SMALL_R - 1) / DG_SMALL_R), dim3(DG_SMALL_TPB), 0,
+                         stream, G, ldg, K, W, ldw, X, ldx, B, GX, partial);
+    else
+      hipLaunchKernelGGL(dgrad_mask_small_kernel<false>, dim3((B + DG_SMALL_R - 1) / DG_SMALL_R), dim3(DG_SMALL_TPB),
+                         0, stream, G, ldg, K, W, ldw, X, ldx, B, GX, partial);
+    return hipGetLastError();
+  }
+  if (((uintptr_t)G & 15) || (ldg & 3) || !workspace) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(dg_transpose_kernel, dim3(DG_N / 32, (K + 31) / 32), dim3(256), 0, stream, W, ldw, K, N, workspace);
+  const int RB = dg_rb(B);
+  const size_t lds = (size_t)16 * RB * dg_stride(K) * 4;
+#define DG_LAUNCH(BB, XV)                                                                                     \
+  do {                                                                                                        \
+    static const hipError_t attr =                                                                            \
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&dgrad_mask_mfma_kernel<BB, XV>),                   \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)((size_t)16 * BB * dg_stride(MLP_MAXD) * 4)); \
+    if (attr != hipSuccess) return attr;                                                                      \
+    dgrad_mask_mfma_kernel<BB, XV><<<dim3((B + 16 * BB - 1) / (16 * BB)), MLP_TPB, lds, stream>>>(            \
+        G, ldg, K, workspace, X, ldx, B, GX, partial);                                                        \
+  } while (0)
+  if (RB == 4) {
+    if (xvec) DG_LAUNCH(4, true);
+    else DG_LAUNCH(4, false);
+  } else if (RB == 2) {
+    if (xvec) DG_LAUNCH(2, true);
+    else DG_LAUNCH(2, false);
+  } else {
+    if (xvec) DG_LAUNCH(1, true);
+    else DG_LAUNCH(1, false);
+  }
+#undef DG_LAUNCH
   return hipGetLastError();
 }
 

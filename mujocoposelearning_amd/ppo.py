@@ -26,8 +26,8 @@ import torch.nn as nn
 
 
 from .ppo_ops import (Linear, _GaussLogpFn, _PPOLossFn, _SplitKLinearFn, _SplitKLinearReLUFn,  # noqa: F401
-                      _SPLITK_ROWS, adam_clip_step, colsum, gae_device, mlp2_forward, mlp_forward, ppo_act,
-                      ppo_loss, ppo_post)
+                      _SPLITK_ROWS, adam_clip_step, colsum, gae_device, mlp2_forward, mlp_forward,
+                      mlp_head_forward, ppo_act, ppo_loss, ppo_post)
 
 FUSED_MLP = True      # rollout forward through the fused hs_mlp2_forward kernel where it applies
 FUSED_MLP_MAX_ROWS = None   # ... up to this many rows (None: any)
@@ -65,8 +65,8 @@ class ActorCritic(nn.Module):
                     nn.init.zeros_(m.bias)
 
     def forward(self, obs):
-        return (self.action_net(mlp_forward(self.pi_net, obs)),
-                self.value_net(mlp_forward(self.vf_net, obs)).squeeze(-1))
+        return (mlp_head_forward(self.pi_net, self.action_net, obs),
+                mlp_head_forward(self.vf_net, self.value_net, obs).squeeze(-1))
 
     def _logp(self, mean, actions):
         """DiagGaussian log_prob; on a device through hs_gauss_logp (+ its HIP backward)."""

@@ -7,7 +7,8 @@ restatement for CPU tensors (toy envs, tests).
   dones, returns, next obs), gae_device (GAE reverse scan)
 * update: _GaussLogpFn (log-prob fwd/bwd), _PPOLossFn / ppo_loss (clipped surrogate + value MSE
   fwd/bwd), _SplitKLinearFn / _SplitKLinearReLUFn / Linear / mlp_forward (split-K weight
-  gradients, ReLU in the GEMM epilogue), colsum (deterministic column sums), adam_clip_step
+  gradients, ReLU in the GEMM epilogue), _MLPChainFn / mlp_head_forward (a whole net as one node:
+  input gradient + ReLU mask + bias sum fused, hs_dgrad_mask), colsum (deterministic column sums), adam_clip_step
   (clip_grad_norm_ + Adam on a torch Adam's own state)
 """
 from __future__ import annotations
@@ -175,6 +176,24 @@ def relu_grad_colsum(g, y):
     return gm, part
 
 
+def dgrad_mask(g, w, x):
+    """(g @ w masked by x > 0, per-row-block column sums of it) through hs_dgrad_mask: the input
+    gradient of a Linear layer (weight w [K, 256], output gradient g [B, K]) whose input x [B, 256]
+    is a ReLU output, fused with that ReLU's backward and its bias sum's first pass."""
+    from . import _lib
+    B, K = g.shape
+    assert w.shape == (K, 256) and x.shape == (B, 256) and g.stride(1) == 1 and w.stride(1) == 1 and x.stride(1) == 1
+    L = _lib.lib()
+    gx = torch.empty(B, 256, dtype=torch.float32, device=g.device)
+    part = torch.empty(int(L.hs_dgrad_mask_partial_rows(B, K)), 256, dtype=torch.float32, device=g.device)
+    nws = int(L.hs_dgrad_mask_workspace(K))
+    ws = torch.empty(nws, dtype=torch.float32, device=g.device) if nws else None
+    _lib.check(L.hs_dgrad_mask(g.data_ptr(), g.stride(0), K, w.data_ptr(), w.stride(0), x.data_ptr(), x.stride(0), B,
+                               256, gx.data_ptr(), part.data_ptr(), None if ws is None else ws.data_ptr(),
+                               torch.cuda.current_stream(g.device).cuda_stream))
+    return gx, part
+
+
 def colsum_pair(x0, x1):
     """(column sums of x0, column sums of x1) for two short contiguous matrices, one launch."""
     from . import _lib
@@ -227,6 +246,73 @@ class _SplitKLinearReLUFn(torch.autograd.Function):
         part = torch.bmm(g.view(s, -1, g.shape[1]).transpose(1, 2), x.view(s, -1, x.shape[1]))
         gw, gb = colsum_pair(part.view(s, -1), bias_part)    # both finishes in one launch
         return gx, gw.view_as(w), gb, None
+
+
+class _MLPChainFn(torch.autograd.Function):
+    """head(relu(... relu(x W1^T + b1) ...)) for one SB3 MlpPolicy net (mlp_extractor's pi or vf
+    half + action_net / value_net, policies.py, SB3 2.3.2) with hidden widths 256, as one autograd
+    node.  Forward: each hidden layer one GEMM with the ReLU in its epilogue, the head one GEMM.
+    Backward by hand, so that a layer's input gradient, the ReLU mask of the layer below and that
+    layer's bias sum come out of one hs_dgrad_mask pass (autograd would write g @ w, read it back
+    with the ReLU output for the mask and again for the bias sum); weight gradients split-K as
+    _SplitKLinearFn, each layer's weight and bias finishes in one colsum_pair launch."""
+
+    @staticmethod
+    def forward(ctx, x, s, *params):
+        ws, bs = params[0::2], params[1::2]
+        ys, h = [], x
+        for w, b in zip(ws[:-1], bs[:-1]):
+            h = torch._addmm_activation(b, h, w.t())
+            ys.append(h)
+        out = torch.addmm(bs[-1], h, ws[-1].t())
+        ctx.save_for_backward(x, *ys, *ws)
+        ctx.s, ctx.nl = s, len(ws)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        s, nl = ctx.s, ctx.nl
+        saved = ctx.saved_tensors
+        x, ys, ws = saved[0], saved[1:nl], saved[nl:]
+        g = g.contiguous()
+        A, yl = g.shape[1], ys[-1]
+        grads = [None] * (2 * nl)
+        if A == 1:       # value head: a rank-1 weight gradient
+            grads[-2] = colsum(yl, g.view(-1)).view_as(ws[-1])
+        else:
+            part = torch.bmm(g.view(s, -1, A).transpose(1, 2), yl.view(s, -1, yl.shape[1]))
+            grads[-2] = colsum(part.view(s, -1)).view_as(ws[-1])
+        grads[-1] = colsum(g)
+        g, bias_part = dgrad_mask(g, ws[-1], yl)
+        gx = None
+        for li in range(nl - 2, -1, -1):
+            xin = ys[li - 1] if li else x
+            part = torch.bmm(g.view(s, -1, g.shape[1]).transpose(1, 2), xin.view(s, -1, xin.shape[1]))
+            gw, grads[2 * li + 1] = colsum_pair(part.view(s, -1), bias_part)
+            grads[2 * li] = gw.view_as(ws[li])
+            if li:
+                g, bias_part = dgrad_mask(g, ws[li], ys[li - 1])
+            elif ctx.needs_input_grad[0]:
+                gx = g @ ws[0]
+        return (gx, None, *grads)
+
+
+FUSED_CHAIN = True       # module switch (A/B probes)
+
+
+def mlp_head_forward(seq, head, x):
+    """head(seq(x)) for an MlpPolicy net (seq = [Linear, ReLU] * L, head a Linear); a large device
+    minibatch with hidden widths 256 and a head of <= 32 outputs runs as one _MLPChainFn node, the
+    rest through mlp_forward."""
+    mods = list(seq)
+    s = _splitk_rows(x)
+    if (FUSED_CHAIN and s and x.dtype == torch.float32 and len(mods) >= 2 and len(mods) % 2 == 0
+            and all(isinstance(m, nn.Linear) and m.out_features == 256 for m in mods[0::2])
+            and all(type(m) is nn.ReLU for m in mods[1::2]) and isinstance(head, nn.Linear)
+            and head.out_features <= 32 and x.stride(1) == 1):
+        params = [t for m in mods[0::2] + [head] for t in (m.weight, m.bias)]
+        return _MLPChainFn.apply(x, s, *params)
+    return head(mlp_forward(seq, x))
 
 
 def _splitk_rows(x):

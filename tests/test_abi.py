@@ -102,6 +102,18 @@ def test_trainer_entry_points_validate_arguments():
     assert "D <= 512" in err(mlp(600, 8, 600, 256, 256, 21))
     assert "null" in err(mlp(352, 8, 352, 256, 256, 21))
     assert mlp(352, 0, 352, 256, 256, 21) == 0
+    dg = lambda G, ldg, K, W, ldw, X, ldx, B, N: L.hs_dgrad_mask(G, ldg, K, W, ldw, X, ldx, B, N, X, W,  # noqa: E731
+                                                                 None, None)
+    assert "N == 256" in err(dg(None, 21, 21, None, 256, None, 256, 8, 128))
+    assert "K % 16" in err(dg(None, 40, 40, None, 256, None, 256, 8, 256))
+    assert "ldx >= N" in err(dg(None, 21, 21, None, 256, None, 100, 8, 256))
+    assert "null" in err(dg(None, 21, 21, None, 256, None, 256, 8, 256))
+    assert dg(None, 256, 256, None, 256, None, 256, 0, 256) == 0
+    assert "16-byte aligned" in err(L.hs_dgrad_mask(4, 256, 256, 16, 256, 16, 256, 8, 256, 16, 16, 16, None))
+    assert "workspace" in err(L.hs_dgrad_mask(16, 256, 256, 16, 256, 16, 256, 8, 256, 16, 16, None, None))
+    assert L.hs_dgrad_mask_workspace(256) == 256 * 256 and L.hs_dgrad_mask_workspace(21) == 0
+    assert L.hs_dgrad_mask_partial_rows(32768, 256) == 512 and L.hs_dgrad_mask_partial_rows(4096, 256) == 256
+    assert L.hs_dgrad_mask_partial_rows(37, 21) == 2 and L.hs_dgrad_mask_partial_rows(0, 21) == 0
     # empty problems are no-ops, not errors
     assert L.hs_ppo_loss(None, None, None, None, None, None, 0, 0.2, None, None, None, None) == 0
     assert L.hs_colsum(None, 0, 0, None, None, None, None) == 0

@@ -487,6 +487,67 @@ def test_relu_grad_colsum_and_pair():
         assert torch.allclose(s1, ref.double().sum(0).float(), rtol=1e-5, atol=1e-5 * rows ** 0.5)
 
 
+@pytest.mark.parametrize("B,K", [(32768, 256), (10000, 256), (4096, 256), (100, 256), (37, 21), (32768, 21),
+                                 (4096, 1), (5, 1)])
+def test_dgrad_mask_matches_torch(B, K):
+    """hs_dgrad_mask (ppo.hip dgrad_mask_*: the input gradient of a Linear fed by a ReLU, masked,
+    with per-row-block column sums) == (g @ w) * (x > 0) and its fp64 column sums, fp32 tolerance:
+    the MFMA instance with one / two / four row blocks (4096 / 10000 / 32768 rows), a partial last
+    tile (100, 10000), the
+    VALU instance for the heads (21 actions, 1 value) with ragged rows (37, 5)."""
+    from mujocoposelearning_amd.ppo_ops import colsum_pair, dgrad_mask
+    gen = torch.Generator(device="cuda").manual_seed(B + K)
+    g = torch.randn(B, K, device="cuda", generator=gen)
+    w = torch.randn(K, 256, device="cuda", generator=gen) * 0.06
+    x = torch.relu(torch.randn(B, 256, device="cuda", generator=gen))
+    gx, part = dgrad_mask(g, w, x)
+    ref = (g.double() @ w.double()) * (x > 0)
+    tol = 1e-5 * (1 + float(ref.abs().max()))
+    assert float((gx.double() - ref).abs().max()) < tol
+    assert torch.all(gx[x <= 0] == 0)
+    _, s1 = colsum_pair(torch.zeros(1, 1, device="cuda"), part)
+    assert torch.allclose(s1.double(), ref.sum(0), rtol=1e-5, atol=tol * B ** 0.5)
+
+
+def test_mlp_chain_node_gradients_match_autograd():
+    """_MLPChainFn (a whole pi / vf net as one autograd node, ppo_ops.py) == module-by-module torch
+    autograd of the same nn.Linear / ReLU net: outputs and every parameter gradient, fp32
+    tolerance, for the pi net (21-action head) and the vf net (value head, rank-1 gradient), with
+    and without an input gradient."""
+    from mujocoposelearning_amd import ppo_ops as O
+    torch.manual_seed(3)
+    B, D = 32768, 352
+    for A, need_gx in ((21, False), (1, True)):
+        seq = torch.nn.Sequential(O.Linear(D, 256), torch.nn.ReLU(), O.Linear(256, 256), torch.nn.ReLU()).cuda()
+        head = O.Linear(256, A).cuda()
+        x = torch.randn(B, D, device="cuda", requires_grad=need_gx)
+        gout = torch.randn(B, A, device="cuda")
+        res = {}
+        for fused in (True, False):
+            O.FUSED_CHAIN = fused
+            try:
+                for p in list(seq.parameters()) + list(head.parameters()):
+                    p.grad = None
+                x.grad = None
+                with torch.enable_grad():
+                    if fused:
+                        out = O.mlp_head_forward(seq, head, x)
+                    else:   # plain torch: F.linear / relu on the same parameters
+                        F = torch.nn.functional
+                        h = torch.relu(F.linear(torch.relu(F.linear(x, seq[0].weight, seq[0].bias)), seq[2].weight,
+                                                seq[2].bias))
+                        out = F.linear(h, head.weight, head.bias)
+                    out.backward(gout)
+                res[fused] = [out.detach()] + [p.grad.clone() for p in list(seq.parameters()) + list(head.parameters())]
+                if need_gx:
+                    res[fused].append(x.grad.clone())
+            finally:
+                O.FUSED_CHAIN = True
+        for a, b in zip(res[True], res[False]):
+            assert a.shape == b.shape
+            assert torch.allclose(a, b, rtol=1e-4, atol=1e-4 * (1 + float(b.abs().max()))), float((a - b).abs().max())
+
+
 def test_ppo_deep_net_arch_trains_on_gpu():
     """net_arch lists of any depth (main.py --net_arch_pi/--net_arch_vf): 3 + 3 hidden
     layers are 17 parameter tensors (> one 16-tensor Adam chunk); graphed training runs and

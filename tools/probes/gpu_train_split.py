@@ -1,7 +1,8 @@
 """Where a bench.py train-leg iteration goes: PPO.learn with the bench's train config (4096 fp64
 envs, 32 steps, batch 32768, 4 epochs, MLP[256,256] ReLU), per iteration the logger's rollout_s
 (collect_rollouts + warning check) and train_s (the update), synchronized.
-    python tools/probes/gpu_train_split.py [iterations]"""
+    python tools/probes/gpu_train_split.py [iterations] [nochain]
+(nochain: the nets' backward module by module, ppo_ops.FUSED_CHAIN off)"""
 import json
 import os
 import sys
@@ -20,6 +21,9 @@ XML = os.path.join(ROOT, "mujocoposelearning_amd", "assets", "humanoid.xml")
 
 def main():
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 6
+    if "nochain" in sys.argv[2:]:
+        from mujocoposelearning_amd import ppo_ops
+        ppo_ops.FUSED_CHAIN = False
     n = 4096
     env = HumanoidVecEnv({"model_path": XML, "duration": 10.0, "frame_skip": 3, "reward_config": {"type": "stand"}},
                          n_envs=n, model=HsModel(XML), seed=0, precision="fp64")
