@@ -526,36 +526,42 @@ def test_dgrad_mask_unaligned_operands(K):
     assert torch.equal(gx, ga) and torch.equal(part, pa)
 
 
-def test_mlp_chain_node_gradients_match_autograd():
+@pytest.mark.parametrize("depth", [1, 2, 3])
+def test_mlp_chain_node_gradients_match_autograd(depth):
     """_MLPChainFn (a whole pi / vf net as one autograd node, ppo_ops.py) == module-by-module torch
     autograd of the same nn.Linear / ReLU net: outputs and every parameter gradient, fp32
-    tolerance, for the pi net (21-action head) and the vf net (value head, rank-1 gradient), with
-    and without an input gradient."""
+    tolerance, for 1-3 hidden layers of 256, the pi head (21 actions) and the value head (rank-1
+    weight gradient), with and without an input gradient."""
     from mujocoposelearning_amd import ppo_ops as O
-    torch.manual_seed(3)
+    F = torch.nn.functional
+    torch.manual_seed(3 + depth)
     B, D = 32768, 352
     for A, need_gx in ((21, False), (1, True)):
-        seq = torch.nn.Sequential(O.Linear(D, 256), torch.nn.ReLU(), O.Linear(256, 256), torch.nn.ReLU()).cuda()
+        mods = []
+        for li in range(depth):
+            mods += [O.Linear(D if li == 0 else 256, 256), torch.nn.ReLU()]
+        seq = torch.nn.Sequential(*mods).cuda()
         head = O.Linear(256, A).cuda()
+        params = list(seq.parameters()) + list(head.parameters())
         x = torch.randn(B, D, device="cuda", requires_grad=need_gx)
         gout = torch.randn(B, A, device="cuda")
         res = {}
         for fused in (True, False):
             O.FUSED_CHAIN = fused
             try:
-                for p in list(seq.parameters()) + list(head.parameters()):
+                for p in params:
                     p.grad = None
                 x.grad = None
                 with torch.enable_grad():
                     if fused:
                         out = O.mlp_head_forward(seq, head, x)
                     else:   # plain torch: F.linear / relu on the same parameters
-                        F = torch.nn.functional
-                        h = torch.relu(F.linear(torch.relu(F.linear(x, seq[0].weight, seq[0].bias)), seq[2].weight,
-                                                seq[2].bias))
+                        h = x
+                        for m in seq[0::2]:
+                            h = torch.relu(F.linear(h, m.weight, m.bias))
                         out = F.linear(h, head.weight, head.bias)
                     out.backward(gout)
-                res[fused] = [out.detach()] + [p.grad.clone() for p in list(seq.parameters()) + list(head.parameters())]
+                res[fused] = [out.detach()] + [p.grad.clone() for p in params]
                 if need_gx:
                     res[fused].append(x.grad.clone())
             finally:
