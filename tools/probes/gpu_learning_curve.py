@@ -50,6 +50,9 @@ def main(iters=400, reward="stand", precision="fp32", seed=0, batch=32768, epoch
 
 
 if __name__ == "__main__":
+    if os.environ.get("HS_NOCHAIN") == "1":   # A/B: the nets' backward module by module
+        from mujocoposelearning_amd import ppo_ops
+        ppo_ops.FUSED_CHAIN = False
     main(int(sys.argv[1]) if len(sys.argv) > 1 else 400, sys.argv[2] if len(sys.argv) > 2 else "stand",
          sys.argv[3] if len(sys.argv) > 3 else "fp32", int(sys.argv[4]) if len(sys.argv) > 4 else 0,
          int(sys.argv[5]) if len(sys.argv) > 5 else 32768, int(sys.argv[6]) if len(sys.argv) > 6 else 4,
