@@ -571,6 +571,46 @@ def test_mlp_chain_node_gradients_match_autograd(depth):
             assert torch.allclose(a, b, rtol=1e-4, atol=1e-4 * (1 + float(b.abs().max()))), float((a - b).abs().max())
 
 
+def test_chain_node_in_a_real_ppo_minibatch():
+    """In context: after a real fused rollout of 4096 fp64 envs (bench train config), one 32 768-
+    sample minibatch's loss gradient for every policy parameter (log_std included) with the nets'
+    backward as _MLPChainFn nodes == the module-by-module backward, fp32 tolerance; and so does the
+    gradient norm clip_grad_norm_ sees."""
+    from mujocoposelearning_amd import ppo_ops as O
+    from mujocoposelearning_amd.model import HsModel
+    from mujocoposelearning_amd.ppo import PPO
+    from mujocoposelearning_amd.vec_env import HumanoidVecEnv
+    env = HumanoidVecEnv({"model_path": XML, "duration": 10.0, "frame_skip": 3, "reward_config": {"type": "stand"}},
+                         n_envs=4096, model=HsModel(XML), seed=0, precision="fp64")
+    ppo = PPO(env, n_steps=32, batch_size=32768, n_epochs=1, seed=0, stagger_episodes=True,
+              policy_kwargs={"activation_fn": "ReLU", "net_arch": {"pi": [256, 256], "vf": [256, 256]}})
+    adv, ret = ppo.collect_rollouts()
+    b = ppo.buf
+    M = 32 * 4096
+    obs, act, old_logp = b["obs"].reshape(M, -1), b["act"].reshape(M, -1), b["logp"].reshape(-1)
+    adv, ret = adv.reshape(-1).float().contiguous(), ret.reshape(-1).float().contiguous()
+    idx = torch.randperm(M, device="cuda", generator=torch.Generator(device="cuda").manual_seed(1))[:32768]
+    params = list(ppo.policy.parameters())
+    grads = {}
+    for fused in (True, False):
+        O.FUSED_CHAIN = fused
+        try:
+            for p in params:
+                p.grad = None
+            with torch.enable_grad():
+                loss, _, _ = ppo._minibatch_loss(obs, act, old_logp, adv, ret, idx)
+                loss.backward()
+            grads[fused] = [p.grad.clone() for p in params]
+        finally:
+            O.FUSED_CHAIN = True
+    for a, c in zip(grads[True], grads[False]):
+        assert torch.allclose(a, c, rtol=1e-3, atol=1e-4 * (1 + float(c.abs().max()))), float((a - c).abs().max())
+    n1 = torch.sqrt(sum((g.double() ** 2).sum() for g in grads[True]))
+    n0 = torch.sqrt(sum((g.double() ** 2).sum() for g in grads[False]))
+    assert abs(float(n1 / n0) - 1) < 1e-4, (float(n1), float(n0))
+    env.close()
+
+
 def test_ppo_deep_net_arch_trains_on_gpu():
     """net_arch lists of any depth (main.py --net_arch_pi/--net_arch_vf): 3 + 3 hidden
     layers are 17 parameter tensors (> one 16-tensor Adam chunk); graphed training runs and
