@@ -43,7 +43,7 @@ def main(iters=400, reward="stand", precision="fp32", seed=0, batch=32768, epoch
             rows.append((it, ppo.num_timesteps, r_step, h, ep, st["value_loss"], time.perf_counter() - t0))
             print(f"iter {it:4d} steps {ppo.num_timesteps / 1e6:6.1f}M  mean step reward {r_step:.4f}  "
                   f"mean height {h:.3f}  ep return (last 200) {ep:8.2f}  vf loss {st['value_loss']:.4f}  "
-                  f"log_std {float(ppo.policy.log_std.mean()):.3f}  fused {ppo._fused_rollout_args() is not None}  "
+                  f"log_std {float(ppo.policy.log_std.detach().mean()):.3f}  fused {ppo._fused_rollout_args() is not None}  "
                   f"{time.perf_counter() - t0:6.1f}s", flush=True)
     env.close()
     return rows
