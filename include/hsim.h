@@ -18,6 +18,8 @@
  *   hs_step_tape         <- K x HumanoidEnv.step over a given action tape (open loop), one launch
  *   hs_rollout           <- SB3 PPO.collect_rollouts' per-step loop (policy + env step + buffers), one launch
  *   hs_physics_step      <- raw `data.ctrl[:] = a; mujoco.mj_step(model, data)` custom_env.py:159-160
+ *   hs_reward_eval       <- REWARD_FUNCTIONS[type](data, params) reward_functions.py:66-269 (the device
+ *                           formulas of hs_step on supplied fields)
  *   hs_debug_lose_handoff   (test hook: mj_step's warning + mj_resetData path, custom_env.py:160)
  *   hs_state_io          <- reads/writes of data.qpos/qvel/qacc_warmstart/time/ctrl (custom_env.py:105-117)
  *   hs_get_buffers       <- data.* arrays as device buffers (obs, reward, terminated, ...)
@@ -288,6 +290,20 @@ int hs_synchronize(hs_batch* b);
  * the wide tier (64 / 256); contacts are only dropped (HS_WARN_OVERFLOW) past the wide tier. */
 int hs_batch_counters(const hs_batch* b, uint64_t* wide_reruns);
 
+/* The device reward plug-ins on supplied fields <- REWARD_FUNCTIONS[type](env_data, params)
+ * (reward_functions.py:66-269, utils.py:3-21; called at custom_env.py:263-271).  Runs the SAME device
+ * code the step kernel inlines after each env step (reward_formula + numpy-order sums), on n states
+ * given as device arrays of the `precision` type (HS_FP32 / HS_FP64): qpos [n][nq], qvel [n][nv],
+ * ctrl [n][nu], time [n], subtree_com0 / subtree_linvel0 [n][3] (subtree_com[0], subtree_linvel[0]),
+ * cfrc_ext [n][nbody][6], qfrc_actuator [n][nv]; writes out [n].  reward_id: HS_REWARD_STAND ("default",
+ * "stand"), HS_REWARD_KNEELING, HS_REWARD_WALK; kneel_params: 9 host doubles in hs_env_config's order
+ * (NULL = the reference defaults, reward_functions.py:71-81).  The step kernel itself passes zeros for
+ * cfrc_ext / subtree_linvel unless HS_FULL_STATE (mj_step leaves them uncomputed).  Asynchronous. */
+int hs_reward_eval(const hs_model* m, int precision, int reward_id, const double* kneel_params, int n,
+                   const void* qpos, const void* qvel, const void* ctrl, const void* time, const void* subtree_com0,
+                   const void* subtree_linvel0, const void* cfrc_ext, const void* qfrc_actuator, void* out,
+                   void* stream);
+
 /* GAE(gamma, lambda) reverse scan over a device rollout buffer, SB3 semantics: [T][N] float32
  * rewards, values, episode_starts; [N] last_values, last_dones; writes [T][N] advantages and
  * returns (= advantages + values).  All pointers are device memory on the current device;
@@ -342,7 +358,8 @@ int hs_gauss_logp_grad(const float* mean, int mean_ld, const float* actions, con
                        const float* g_logp, float* g_mean, float* gls_rows, int N, int A, void* stream);
 /* SB3 PPO minibatch loss over B samples gathered by idx [B] (int64) from the rollout arrays
  * advantages / returns / old_log_prob [M]: log_prob [B] and values [B] are the policy's on the
- * minibatch.  a = advantages[idx] normalised (mean, unbiased std + 1e-8; not when B == 1),
+ * minibatch.  a = advantages[idx] normalised (mean, unbiased std + 1e-8; not when B == 1, nor when
+ * normalize_advantage == 0: SB3's PPO(normalize_advantage=False)),
  * r = exp(log_prob - old_log_prob[idx]); writes policy_loss = -mean(min(a r, a clip(r, 1 -+ clip)))
  * and value_loss = mean((returns[idx] - values)^2) (device scalars).  `workspace` holds
  * hs_ppo_loss_workspace(B) floats: the forward leaves the gathered minibatch and the
@@ -351,8 +368,8 @@ int hs_gauss_logp_grad(const float* mean, int mean_ld, const float* actions, con
  * Fixed reduction order (deterministic); asynchronous on `stream`. */
 uint64_t hs_ppo_loss_workspace(int B);
 int hs_ppo_loss(const float* log_prob, const float* values, const int64_t* idx, const float* advantages,
-                const float* returns, const float* old_log_prob, int B, float clip, float* policy_loss,
-                float* value_loss, float* workspace, void* stream);
+                const float* returns, const float* old_log_prob, int B, float clip, int normalize_advantage,
+                float* policy_loss, float* value_loss, float* workspace, void* stream);
 int hs_ppo_loss_grad(const float* log_prob, const float* values, int B, float clip, const float* workspace,
                      const float* g_pg, const float* g_vf, float* g_log_prob, float* g_values, void* stream);
 /* Gradient-norm clipping + one Adam step over nt <= 1024 float32 device tensors: params[i],

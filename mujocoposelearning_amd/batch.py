@@ -24,6 +24,67 @@ def _torch():
     return torch
 
 
+# MuJoCo's own warning texts for the three bad-state resets (mjWARN_BADQPOS / QVEL / QACC)
+WARN_KINDS = ("Nan, Inf or huge value in QPOS", "Nan, Inf or huge value in QVEL", "Nan, Inf or huge value in QACC",
+              "contacts dropped past the wide contact tier", "chunk-queue hand-off lost")
+
+
+def report_warnings(new, where="step"):
+    """Surface new warning counts (include/hsim.h HS_WARN_*, one value per kind) the way the reference
+    run surfaces them: MuJoCo's mj_step prints mju_warning and resets a bad state (mj_resetData) and the
+    run goes on (custom_env.py:160) -- here one RuntimeWarning per call with the counts; a lost
+    chunk-queue hand-off is a scheduling failure of the step kernel, not physics, so it raises."""
+    new = np.asarray(new, dtype=np.int64)
+    if len(new) > 4 and new[4] > 0:
+        raise _lib.HsimError(f"{WARN_KINDS[4]} in {int(new[4])} env step(s) of this {where}: a scheduling failure of "
+                             "the step kernel (e.g. more concurrent queued batches than the GPU holds waves for), "
+                             "not physics -- those envs were reset and the results are not valid")
+    parts = [f"{WARN_KINDS[k]} in {int(new[k])} env step(s) of this {where}" for k in range(min(4, len(new)))
+             if new[k] > 0]
+    if parts:
+        import warnings
+        warnings.warn("mj_step warning: " + "; ".join(parts) + (" -- those envs were reset (mj_resetData)"
+                      if new[:3].any() else ""), RuntimeWarning, stacklevel=3)
+
+
+def reward_eval(model, name, qpos, qvel, ctrl, time, subtree_com0, subtree_linvel0, cfrc_ext, qfrc_actuator,
+                params=None, registry=None):
+    """``REWARD_FUNCTIONS[name](data, params)`` for n states at once, computed by the device reward
+    code of the step kernel (``hs_reward_eval``; reward_functions.py:66-269).  Arguments are CUDA
+    tensors of one float dtype (float64 = the fp64 engine's formulas, float32 = the fp32 engine's):
+    qpos [n][nq], qvel [n][nv], ctrl [n][nu], time [n], subtree_com0 / subtree_linvel0 [n][3],
+    cfrc_ext [n][nbody][6], qfrc_actuator [n][nv].  ``params`` are the kneeling reward's overrides
+    (merged over its defaults like reward_functions.py:83).  Returns a [n] tensor.  Unknown names raise
+    ValueError like custom_env.py:268-269; user callables have no device formula (HsimError)."""
+    from .reward_functions import device_reward_id
+    torch = _torch()
+    rid = device_reward_id(name, registry)
+    if rid is None:
+        raise _lib.HsimError(f"reward {name!r} is a host callable: no device formula")
+    args = [qpos, qvel, ctrl, time, subtree_com0, subtree_linvel0, cfrc_ext, qfrc_actuator]
+    dt = qpos.dtype
+    if dt not in (torch.float32, torch.float64):
+        raise TypeError("reward_eval: float32 or float64 tensors")
+    n = qpos.shape[0]
+    shapes = [(n, model.nq), (n, model.nv), (n, model.nu), (n,), (n, 3), (n, 3), (n, model.nbody, 6),
+              (n, model.nv)]
+    for a, s in zip(args, shapes):
+        if not a.is_cuda or a.dtype != dt or tuple(a.shape) != s or not a.is_contiguous():
+            raise ValueError(f"reward_eval: expected a contiguous CUDA {dt} tensor of shape {s}, got "
+                             f"{tuple(a.shape)} {a.dtype} on {a.device}")
+    kn = None
+    if rid == 1:
+        p = {**dict(zip(KNEEL_KEYS, KNEEL_DEFAULTS)), **(params or {})}
+        kn = (C.c_double * 9)(*[float(p[k]) for k in KNEEL_KEYS])
+    out = torch.empty(n, dtype=dt, device=qpos.device)
+    with torch.cuda.device(qpos.device):
+        st = torch.cuda.current_stream().cuda_stream
+        check(lib().hs_reward_eval(model.handle, 1 if dt == torch.float64 else 0, rid,
+                                   C.cast(kn, C.c_void_p) if kn is not None else None, n,
+                                   *[a.data_ptr() for a in args], out.data_ptr(), st))
+    return out
+
+
 class HsBatch:
     def __init__(self, model, n_envs, device=0, seed=0, precision="fp32", full_state=False, groups=1):
         """``groups`` > 1 splits the envs into that many native sub-batches (contiguous env ranges
@@ -278,28 +339,35 @@ class HsBatch:
     _HOST_COLS = ("reward", "terminated", "truncated", "total_reward", "step_count", "terminal_step_count",
                   "terminal_total_reward")
 
-    def host_outputs(self, ncols=3):
+    def host_outputs(self, ncols=3, warnings=False):
         """One step's outputs on the host in ONE device-to-host copy: the obs and the first ``ncols``
         of (reward, terminated, truncated, total_reward, step_count, terminal_step_count,
         terminal_total_reward), packed on the device into one float64 buffer, copied into pinned
         host memory and synchronized once.  Returns (obs [N, obs_dim] float64, cols [ncols, N]
         float64), views of a fresh pinned block (torch's caching host allocator recycles it once
-        both are dropped)."""
+        both are dropped).  ``warnings=True`` also packs the warning counters summed over the envs
+        (HS_NWARN values, cumulative since the batch was created) and returns them third, as int64."""
         torch = _torch()
         N, D = self.n, self.obs_dim
-        size = N * D + ncols * N
+        nw = _lib.HS_NWARN if warnings else 0
+        size = N * D + ncols * N + nw
         dev = self.__dict__.get("_pack_dev")
         if dev is None or dev.numel() != size:
             dev = self._pack_dev = torch.empty(size, dtype=torch.float64, device=self.device)
         dev[:N * D].view(N, D).copy_(self.t["obs"])
-        cols = dev[N * D:].view(ncols, N)
+        cols = dev[N * D:N * D + ncols * N].view(ncols, N)
         for k in range(ncols):
             cols[k].copy_(self.t[self._HOST_COLS[k]])
+        if nw:
+            torch.sum(self.t["warning"], 0, dtype=torch.float64, out=dev[N * D + ncols * N:])
         host = torch.empty(size, dtype=torch.float64, pin_memory=True)
         host.copy_(dev, non_blocking=True)
         torch.cuda.current_stream(self.device).synchronize()
         a = host.numpy()
-        return a[:N * D].reshape(N, D), a[N * D:].reshape(ncols, N)
+        obs, c = a[:N * D].reshape(N, D), a[N * D:N * D + ncols * N].reshape(ncols, N)
+        if not nw:
+            return obs, c
+        return obs, c, a[N * D + ncols * N:].astype(np.int64)
 
     def tape_aborts(self):
         """Tape launches replayed step by step because an env overflowed the resident tier."""

@@ -854,15 +854,15 @@ int hs_gauss_logp_grad(const float* mean, int mean_ld, const float* actions, con
 uint64_t hs_ppo_loss_workspace(int B) { return B > 0 ? hs::ppo_loss_workspace(B) : 0; }
 
 int hs_ppo_loss(const float* log_prob, const float* values, const int64_t* idx, const float* advantages,
-                const float* returns, const float* old_log_prob, int B, float clip, float* policy_loss,
-                float* value_loss, float* workspace, void* stream) {
+                const float* returns, const float* old_log_prob, int B, float clip, int normalize_advantage,
+                float* policy_loss, float* value_loss, float* workspace, void* stream) {
   if (B < 0) return fail("hs_ppo_loss: negative size");
   if (B == 0) return 0;
   if (!log_prob || !values || !idx || !advantages || !returns || !old_log_prob || !policy_loss || !value_loss ||
       !workspace)
     return fail("hs_ppo_loss: null buffer");
-  return hip_ok(hs::launch_ppo_loss_fwd(log_prob, values, idx, advantages, returns, old_log_prob, B, clip, policy_loss,
-                                        value_loss, workspace, (hipStream_t)stream),
+  return hip_ok(hs::launch_ppo_loss_fwd(log_prob, values, idx, advantages, returns, old_log_prob, B, clip,
+                                        normalize_advantage, policy_loss, value_loss, workspace, (hipStream_t)stream),
                 "ppo loss kernels")
              ? 0
              : -1;
@@ -978,6 +978,48 @@ int hs_gae(const float* rewards, const float* values, const float* episode_start
                 "gae_kernel")
              ? 0
              : -1;
+}
+
+int hs_reward_eval(const hs_model* m, int precision, int reward_id, const double* kneel_params, int n,
+                   const void* qpos, const void* qvel, const void* ctrl, const void* time, const void* subtree_com0,
+                   const void* subtree_linvel0, const void* cfrc_ext, const void* qfrc_actuator, void* out,
+                   void* stream) {
+  if (!m) return fail("hs_reward_eval: null model");
+  if (n < 0) return fail("hs_reward_eval: negative n");
+  if (reward_id != HS_REWARD_STAND && reward_id != HS_REWARD_KNEELING && reward_id != HS_REWARD_WALK)
+    return fail("hs_reward_eval: unknown reward id " + std::to_string(reward_id));
+  const int prec = precision & 0xFF;
+  if (prec != HS_FP32 && prec != HS_FP64) return fail("hs_reward_eval: precision must be HS_FP32 or HS_FP64");
+  const hs::HostModel& h = m->host;
+  if (h.nv < 6 || h.nv > 32 || h.nu > 32 || h.nbody < 2 || h.nq < 7)
+    return fail("hs_reward_eval: the model needs a free root joint, nv <= 32, nu <= 32 and >= 2 bodies");
+  if (n == 0) return 0;
+  if (!qpos || !qvel || !ctrl || !time || !subtree_com0 || !subtree_linvel0 || !cfrc_ext || !qfrc_actuator || !out)
+    return fail("hs_reward_eval: null buffer");
+  static const double kdef[9] = {1.282, 0.85, 3.14159265358979323846 / 6, 0.1, 0.3, 0.3, 0.2, 0.1, 0.1};
+  const double* kn = kneel_params ? kneel_params : kdef;
+  auto run = [&](auto zero) -> int {
+    using T = decltype(zero);
+    hs::RewardEvalArgs<T> a{};
+    a.reward_id = reward_id;
+    a.n = n;
+    a.nq = h.nq;
+    a.nv = h.nv;
+    a.nu = h.nu;
+    a.nbody = h.nbody;
+    for (int k = 0; k < 9; k++) a.kneel[k] = kn[k];
+    a.qpos = (const T*)qpos;
+    a.qvel = (const T*)qvel;
+    a.ctrl = (const T*)ctrl;
+    a.time = (const T*)time;
+    a.subtree_com0 = (const T*)subtree_com0;
+    a.subtree_linvel0 = (const T*)subtree_linvel0;
+    a.cfrc_ext = (const T*)cfrc_ext;
+    a.qfrc_actuator = (const T*)qfrc_actuator;
+    a.out = (T*)out;
+    return hip_ok(hs::launch_reward_eval<T>(a, (hipStream_t)stream), "reward_eval_kernel") ? 0 : -1;
+  };
+  return prec == HS_FP64 ? run(0.0) : run(0.0f);
 }
 
 int hs_batch_counters(const hs_batch* b, uint64_t* wide_reruns) {

@@ -182,6 +182,24 @@ constexpr int KINDIM = MAXBODY * 12 + MAXGEOM * 6 + 3;
 template <typename T>
 hipError_t launch_kinematics(const DevModel<T>* dmodel, int nv, const T* qpos, T* out, hipStream_t stream);
 
+// the step kernel's reward code (reward_formula) on caller-supplied per-env fields (hs_reward_eval)
+template <typename T>
+struct RewardEvalArgs {
+  int reward_id, n, nq, nv, nu, nbody;
+  double kneel[9];            // StepParams::kneel
+  const T* qpos;              // [n][nq]
+  const T* qvel;              // [n][nv]
+  const T* ctrl;              // [n][nu]
+  const T* time;              // [n]
+  const T* subtree_com0;      // [n][3]
+  const T* subtree_linvel0;   // [n][3]
+  const T* cfrc_ext;          // [n][nbody][6]
+  const T* qfrc_actuator;     // [n][nv]
+  T* out;                     // [n]
+};
+template <typename T>
+hipError_t launch_reward_eval(const RewardEvalArgs<T>& a, hipStream_t stream);
+
 // PPO rollout bookkeeping around the policy GEMMs and the env step (ppo.hip)
 hipError_t launch_ppo_act(const float* mean, int mean_ld, const float* value, int value_ld, const float* log_std,
                           const float* episode_start, uint64_t seed, uint64_t counter, const uint64_t* counter_base,
@@ -212,8 +230,8 @@ hipError_t launch_gauss_logp_grad(const float* mean, int mean_ld, const float* a
 // of ppo_loss_workspace(B) floats, written by the forward and read by the backward
 size_t ppo_loss_workspace(int B);
 hipError_t launch_ppo_loss_fwd(const float* logp, const float* v, const int64_t* idx, const float* adv,
-                               const float* ret, const float* old_logp, int B, float clip, float* pg, float* vf,
-                               float* ws, hipStream_t stream);
+                               const float* ret, const float* old_logp, int B, float clip, int normalize, float* pg,
+                               float* vf, float* ws, hipStream_t stream);
 hipError_t launch_ppo_loss_bwd(const float* logp, const float* v, int B, float clip, const float* ws,
                                const float* g_pg, const float* g_vf, float* g_logp, float* g_v, hipStream_t stream);
 // clip_grad_norm_ + Adam over up to 1024 tensors (ppo.hip); part: adam_partials(total numel) floats

@@ -144,6 +144,13 @@ __device__ __forceinline__ double rows_sum(double v) {
   return __longlong_as_double((long long)(((uint64_t)h.lo << 32) | l.lo)) +
          __longlong_as_double((long long)(((uint64_t)h.hi << 32) | l.hi));
 }
+// the value of the same position in the half's high 16-lane row (valid on the low row's lanes)
+__device__ __forceinline__ float up_row(float v) { return __uint_as_float(rowswap(__float_as_uint(v)).hi); }
+__device__ __forceinline__ double up_row(double v) {
+  uint64_t x = (uint64_t)__double_as_longlong(v);
+  const uint64_t lo = rowswap((uint32_t)x).hi, hi = rowswap((uint32_t)(x >> 32)).hi;
+  return __longlong_as_double((long long)((hi << 32) | lo));
+}
 // sum over each 32-lane half (result in every lane of the half); all-VALU, no LDS permute
 template <typename T>
 __device__ __forceinline__ T hsum(T v) {
@@ -2132,51 +2139,133 @@ __device__ __forceinline__ void foot_forces(MPtr<T> m, const Scratch<T, C>& s, T
   for (int k = 0; k < 6; k++) { lf += fabs(s.u.n.cfrc[nb - 2][k]); rf += fabs(s.u.n.cfrc[nb - 1][k]); }
 }
 
-template <typename T, typename C>
-__device__ __forceinline__ T compute_reward(MPtr<T> m, const Scratch<T, C>& s, KPtr<T> k, T time,
-                            T energy_sum, T ctrl_sq) {
-  // quaternion_to_euler (utils.py:3-21): pitch = arcsin(2(wy - zx)), not clamped
-  T w = s.qpos[3], x = s.qpos[4], y = s.qpos[5], z = s.qpos[6];
-  T roll = atan2(2 * (w * x + y * z), 1 - 2 * (x * x + y * y));
-  T pitch = asin(2 * (w * y - z * x));
-  T h = s.qpos[2];
-  if (k->p.reward_id == REWARD_STAND || k->p.reward_id == REWARD_WALK) {
-    T torque = exp(T(-0.05) * ctrl_sq);     // sum(ctrl^2), reduced across the half-wave by the caller
-    T post = T(0.5) * exp(T(-2) * (h - T(1.282)) * (h - T(1.282))) + T(0.5) * exp(T(-3) * (roll * roll + pitch * pitch));
-    if (k->p.reward_id == REWARD_STAND) {
-      // cfrc_ext is never computed by mj_step without sensors -> both "feet" forces are 0 (full_state:
-      // the real wrenches of the last two bodies, reward_functions.py:176-177)
-      T lf = 0, rf = 0;
-      if (k->p.full_state) foot_forces(m, s, lf, rf);
-      T foot = 1 - fmin(lf, rf) / (lf + rf + T(1e-8));
-      T vr = exp(T(-2) * (s.qvel[0] - 1) * (s.qvel[0] - 1));
-      T r = T(0.4) * vr + T(0.3) * post + T(0.2) * foot + T(0.1) * torque;
-      return h < T(0.8) ? T(0) : r;
+// The reward plug-ins' inputs, gathered per env.  The step kernel fills them from its scratch
+// (compute_reward below); hs_reward_eval (reward_eval_kernel) from caller-supplied fields.  Both run
+// the same reward_formula, so the device formulas are pinned directly by the reference's golden vectors.
+template <typename T>
+struct RewardIn {
+  T h, qw, qx, qy, qz;   // qpos[2], qpos[3:7]
+  T vx;                  // qvel[0]
+  T time;
+  T com0, com1;          // subtree_com[0][0:2]
+  T comv;                // sum(subtree_linvel[0]^2), numpy order (sequential: 3 < 8 terms)
+  T lf, rf;              // sum |cfrc_ext[-2]|, sum |cfrc_ext[-1]| (numpy order: sequential over 6)
+  T energy;              // sum((qfrc_actuator[-nj:] * qvel[6:])^2), numpy's pairwise order (np_sum_half)
+  T ctrl_sq;             // sum(ctrl^2), numpy's pairwise order
+};
+
+// reward_functions.py:66-261 + utils.py:3-21, each expression in the reference's own association
+// and without FMA contraction, so the only difference to numpy is the device libm (exp / atan2 / asin).
+// The reference's Python min(a, b) is `b if b < a else a` (a NaN first operand is returned as is).
+template <typename T, typename KP>
+__device__ __forceinline__ T reward_formula(int reward_id, KP kn, const RewardIn<T>& in) {
+#pragma clang fp contract(off)
+  const T w = in.qw, x = in.qx, y = in.qy, z = in.qz;
+  const T roll = atan2(T(2) * (w * x + y * z), T(1) - T(2) * (x * x + y * y));
+  const T pitch = asin(T(2) * (w * y - z * x));   // not clamped: |sinp| > 1 -> NaN, as np.arcsin
+  const T h = in.h;
+  auto pymin = [](T a, T b) { return b < a ? b : a; };
+  if (reward_id == REWARD_STAND || reward_id == REWARD_WALK) {
+    const T hd = h - T(1.282);
+    const T height_reward = exp(T(-2.0) * (hd * hd));
+    const T orientation_reward = exp(T(-3.0) * (roll * roll + pitch * pitch));
+    const T posture = T(0.5) * height_reward + T(0.5) * orientation_reward;
+    const T torque = exp(T(-0.05) * in.ctrl_sq);
+    if (reward_id == REWARD_STAND) {                       // :156-211
+      if (h < T(0.8)) return T(0);
+      const T vd = in.vx - T(1.0);
+      const T vr = exp(T(-2.0) * (vd * vd));
+      const T total = in.lf + in.rf + T(1e-8);
+      const T foot = T(1.0) - pymin(in.lf, in.rf) / total;
+      return T(0.4) * vr + T(0.3) * posture + T(0.2) * foot + T(0.1) * torque;
     }
-    T vr = exp(T(-0.5) * (s.qvel[0] - 10) * (s.qvel[0] - 10));
-    return h < T(0.8) ? T(0.1) * h / T(0.8) : vr + post * torque;
+    if (h < T(0.8)) return T(0.1) * h / T(0.8);           // :213-261
+    const T vd = in.vx - T(10.0);
+    const T vr = exp(T(-0.5) * (vd * vd));
+    return vr + posture * torque;
   }
-  if (k->p.reward_id == REWARD_KNEELING) {
-    CPtr<double> kn = k->p.kneel;   // target_height, min_height, max_roll_pitch, com_radius, energy_w, posture_w, com_w, foot_w, alive_w
+  if (reward_id == REWARD_KNEELING) {                      // :66-154
+    // kn: target_height, min_height, max_roll_pitch, com_radius, energy_w, posture_w, com_w, foot_w, alive_w
     if (h < T(kn[1])) return h * h;
-    T mrp = T(kn[2]);
-    T posture = T(0.7) * exp(T(-5) * (roll * roll + pitch * pitch) / (mrp * mrp)) +
-                T(0.3) * exp(T(-5) * (h - T(kn[0])) * (h - T(kn[0])));
-    T dist = sqrt(s.com[0] * s.com[0] + s.com[1] * s.com[1]);
-    T comv = T(0);   // subtree_linvel is lazy in MuJoCo -> 0 (full_state: |subtree_linvel[0]|^2)
-    T foot = T(0);   // min(0,0)/(0+0+1e-8)
-    if (k->p.full_state) {
-      for (int q = 0; q < 3; q++) comv += s.u.n.linv[0][q] * s.u.n.linv[0][q];
-      T lf, rf;
-      foot_forces(m, s, lf, rf);
-      foot = fmin(lf, rf) / (lf + rf + T(1e-8));
-    }
-    T com = T(0.7) * exp(T(-10) * (dist / T(kn[3]))) + T(0.3) * exp(T(-0.1) * comv);
-    T energy = exp(T(-0.01) * energy_sum);
-    T alive = 1 - exp(T(-0.5) * time);
+    const T mrp = T(kn[2]);
+    const T orientation_error = (roll * roll + pitch * pitch) / (mrp * mrp);
+    const T posture_reward = exp(T(-5.0) * orientation_error);
+    const T hd = h - T(kn[0]);
+    const T height_reward = exp(T(-5.0) * (hd * hd));
+    const T posture = T(0.7) * posture_reward + T(0.3) * height_reward;
+    const T dist = sqrt(in.com0 * in.com0 + in.com1 * in.com1);
+    const T com = T(0.7) * exp(T(-10.0) * (dist / T(kn[3]))) + T(0.3) * exp(T(-0.1) * in.comv);
+    const T total = in.lf + in.rf + T(1e-8);
+    const T foot = pymin(in.lf, in.rf) / total;
+    const T energy = exp(T(-0.01) * in.energy);
+    const T alive = T(1.0) - exp(T(-0.5) * in.time);
     return T(kn[5]) * posture + T(kn[6]) * com + T(kn[7]) * foot + T(kn[4]) * energy + T(kn[8]) * alive;
   }
   return T(0);
+}
+
+// the step kernel's reward: inputs from the env's scratch.  cfrc_ext and subtree_linvel are never
+// computed by mj_step without sensors (lazy), so the reference's reward reads zeros for them; with
+// full_state, the real wrenches / velocity of post_constraint.
+template <typename T, typename C>
+__device__ __forceinline__ T compute_reward(MPtr<T> m, const Scratch<T, C>& s, KPtr<T> k, T time,
+                                            T energy_sum, T ctrl_sq) {
+  RewardIn<T> in;
+  in.h = s.qpos[2];
+  in.qw = s.qpos[3];
+  in.qx = s.qpos[4];
+  in.qy = s.qpos[5];
+  in.qz = s.qpos[6];
+  in.vx = s.qvel[0];
+  in.time = time;
+  in.com0 = s.com[0];
+  in.com1 = s.com[1];
+  in.comv = T(0);
+  in.lf = T(0);
+  in.rf = T(0);
+  if (k->p.full_state) {
+#pragma clang fp contract(off)
+    for (int q = 0; q < 3; q++) in.comv += s.u.n.linv[0][q] * s.u.n.linv[0][q];
+    foot_forces(m, s, in.lf, in.rf);
+  }
+  in.energy = energy_sum;
+  in.ctrl_sq = ctrl_sq;
+  return reward_formula(k->p.reward_id, k->p.kneel, in);
+}
+
+// np.sum's order (numpy pairwise_sum, n <= 128) over the values x_i held by sub-lanes off + i,
+// i < n, of each 32-lane half: n < 8 -> ((0 + x0) + x1) + ...; else eight accumulators r_j = x_j +
+// x_{j+8} + ... over the whole blocks of 8, combined ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)),
+// then the rest added in order.  The block stage and the tree are DPP (row_ror:8, permlane16 swap,
+// the quad / half-mirror steps of hsum); the tail is a few lane reads.  off + n <= 32; the result is
+// in every lane of the half.  (hsum's butterfly order differs from numpy's by an ulp of the sum,
+// which the exp() of a reward term can amplify to several ulp of the reward.)
+template <typename T>
+__device__ __forceinline__ T np_sum_half(T v, int off, int n, int lane) {
+#pragma clang fp contract(off)
+  const int base = (lane & HL) + off;
+  auto at = [&](int i) { return __shfl(v, base + i, WAVE); };
+  T res;
+  int i;
+  if (n < 8) {
+    res = T(0);
+    i = 0;
+  } else {
+    T x = off == 0 ? v : __shfl(v, base + (lane & (HL - 1)), WAVE);   // x_j on sub-lane j
+    const int nb = n - n % 8;
+    T r = x;
+    const T x8 = dpp<0x128>(x);                           // row_ror:8 -> x_{j+8} on sub-lanes 0..7
+    if (nb >= 16) r += x8;
+    if (nb >= 24) { const T t = x; r += up_row(t); }       // x_{j+16}
+    if (nb >= 32) r += up_row(x8);                         // x_{j+24}
+    r += dpp<0xB1>(r);                                     // r0 + r1, r2 + r3, ...
+    r += dpp<0x4E>(r);                                     // (r0 + r1) + (r2 + r3), ...
+    r += dpp<0x141>(r);                                    // ... + ((r4 + r5) + (r6 + r7)) on sub-lane 0
+    res = bcast<0>(r);
+    i = nb;
+  }
+  for (; i < n; i++) res += at(i);
+  return res;
 }
 
 // custom_env.py:232-261 layout; qfrc_actuator comes from registers (sub-lane i holds dof i)
@@ -2545,10 +2634,11 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
         if (k->p.mode == MODE_ENV_STEP) {
           step_count += 1;
           bool trunc = step_count >= k->p.max_steps;
-          T e = (sl >= 6 && sl < nv) ? st.qfa * s.qvel[sl] : T(0);
-          T esum = hsum(e * e);
+          // np.sum(np.square(qfrc_actuator[-nj:] * qvel[6:])) and np.sum(np.square(ctrl)) in numpy's order
+          const T e = sl < nv ? st.qfa * s.qvel[sl] : T(0);
+          const T esum = np_sum_half(e * e, 6, nv - 6, lane);
           const T cu = sl < st.m->nu ? s.ctrl[sl] : T(0);
-          const T csum = hsum(cu * cu);                 // sum ctrl^2 as one half-wave sum
+          const T csum = np_sum_half(cu * cu, 0, st.m->nu, lane);
           HS_STAMP(st.clk, 24);
           T r = trunc ? T(0) : compute_reward(st.m, s, k, time, esum, csum);
           HS_STAMP(st.clk, 25);
@@ -2904,7 +2994,58 @@ __global__ __launch_bounds__(64) void kin_kernel(MPtr<T> m, const T* __restrict_
   if (sl < 3) out[sl] = s.com[sl];
 }
 
+// hs_reward_eval: the step kernel's reward code (np_sum_half + reward_formula) on caller-supplied
+// fields, one env per 32-lane half as in the step kernel.  Not on the step path: it exists so the
+// device formulas can be checked against the reference's own outputs on arbitrary states.
+template <typename T>
+__global__ __launch_bounds__(256) void reward_eval_kernel(RewardEvalArgs<T> a) {
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int sl = lane & (HL - 1);
+  const long long env = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / HL;
+  const bool ok = env < a.n;
+  const int nv = a.nv, nu = a.nu;
+  T e = T(0), cu = T(0);
+  if (ok && sl < nv) e = a.qfrc_actuator[env * nv + sl] * a.qvel[env * nv + sl];
+  if (ok && sl < nu) cu = a.ctrl[env * nu + sl];
+  const T esum = np_sum_half(e * e, 6, nv - 6, lane);   // every lane of the wave takes part
+  const T csum = np_sum_half(cu * cu, 0, nu, lane);
+  if (!ok || sl != 0) return;
+  const T* q = a.qpos + env * a.nq;
+  RewardIn<T> in;
+  in.h = q[2];
+  in.qw = q[3];
+  in.qx = q[4];
+  in.qy = q[5];
+  in.qz = q[6];
+  in.vx = a.qvel[env * nv];
+  in.time = a.time[env];
+  in.com0 = a.subtree_com0[env * 3];
+  in.com1 = a.subtree_com0[env * 3 + 1];
+  {
+#pragma clang fp contract(off)
+    in.comv = T(0);
+    for (int d = 0; d < 3; d++) in.comv += a.subtree_linvel0[env * 3 + d] * a.subtree_linvel0[env * 3 + d];
+  }
+  const T* cf = a.cfrc_ext + (env * a.nbody + a.nbody - 2) * 6;
+  in.lf = T(0);
+  in.rf = T(0);
+  for (int d = 0; d < 6; d++) { in.lf += fabs(cf[d]); in.rf += fabs(cf[6 + d]); }
+  in.energy = esum;
+  in.ctrl_sq = csum;
+  a.out[env] = reward_formula(a.reward_id, a.kneel, in);
+}
+
 }  // namespace
+
+template <typename T>
+hipError_t launch_reward_eval(const RewardEvalArgs<T>& a, hipStream_t stream) {
+  if (a.n <= 0) return hipSuccess;
+  if (a.nv < 6 || a.nv > HL || a.nu < 0 || a.nu > HL || a.nbody < 2 || a.nq < 7) return hipErrorInvalidValue;
+  const long long threads = (long long)a.n * HL;
+  const unsigned blocks = (unsigned)((threads + 255) / 256);
+  hipLaunchKernelGGL((reward_eval_kernel<T>), dim3(blocks), dim3(256), 0, stream, a);
+  return hipGetLastError();
+}
 
 // waves of the resident step-kernel instance the current device holds at once (occupancy x CUs),
 // cached per device (a racing first call computes the same value twice: benign)
@@ -3018,6 +3159,7 @@ template hipError_t launch_step<float>(const DevModel<float>*, int, const EnvBuf
                                        hipStream_t, const TapeOut<float>*, const RolloutArgs*);
 template int resident_waves<float>(bool);
 template hipError_t launch_kinematics<float>(const DevModel<float>*, int, const float*, float*, hipStream_t);
+template hipError_t launch_reward_eval<float>(const RewardEvalArgs<float>&, hipStream_t);
 #endif
 #if !defined(HS_DEV_F32_ONLY) && !defined(HS_ONLY_F32)
 template hipError_t launch_step<double>(const DevModel<double>*, int, const EnvBuffers<double>&, const float*,
@@ -3028,6 +3170,7 @@ template hipError_t launch_step<double>(const DevModel<double>*, int, const EnvB
 #if !defined(HS_DEV_F32_ONLY) && !defined(HS_ONLY_F32)
 template int resident_waves<double>(bool);
 template hipError_t launch_kinematics<double>(const DevModel<double>*, int, const double*, double*, hipStream_t);
+template hipError_t launch_reward_eval<double>(const RewardEvalArgs<double>&, hipStream_t);
 #endif
 
 }  // namespace hs

@@ -228,10 +228,11 @@ __device__ inline float wave_part_sum(const float* part, int nblk, int c) {
 }
 
 // mean and 1 / (std + 1e-8) from the per-block shifted sums (called by a whole wave)
-__device__ inline void loss_stats(const float* ws, int B, int nblk, float a0, float& mean, float& inv) {
+// (norm == 0: SB3's normalize_advantage=False -- mean 0, scale 1)
+__device__ inline void loss_stats(const float* ws, int B, int nblk, float a0, int norm, float& mean, float& inv) {
   const float* part = ws + 3 * (size_t)B;
   const float s1 = wave_part_sum(part, nblk, 0), s2 = wave_part_sum(part, nblk, 1);
-  if (B > 1) {
+  if (B > 1 && norm) {
     mean = a0 + s1 / (float)B;
     float var = (s2 - s1 * s1 / (float)B) / (float)(B - 1);
     inv = 1.f / (sqrtf(fmaxf(var, 0.f)) + 1e-8f);
@@ -243,7 +244,7 @@ __device__ inline void loss_stats(const float* ws, int B, int nblk, float a0, fl
 
 __global__ __launch_bounds__(LOSS_TPB) void loss_terms_kernel(const float* __restrict__ logp,
                                                               const float* __restrict__ v, int B, float clip,
-                                                              float* __restrict__ ws, int nblk) {
+                                                              int norm, float* __restrict__ ws, int nblk) {
   __shared__ float red[LOSS_TPB / 64];
   __shared__ float st[2];
   const float* a_g = ws;
@@ -252,7 +253,7 @@ __global__ __launch_bounds__(LOSS_TPB) void loss_terms_kernel(const float* __res
   float* part = ws + 3 * (size_t)B;
   if (threadIdx.x < 64) {
     float mu, iv;
-    loss_stats(ws, B, nblk, a_g[0], mu, iv);
+    loss_stats(ws, B, nblk, a_g[0], norm, mu, iv);
     if (threadIdx.x == 0) { st[0] = mu; st[1] = iv; }
   }
   __syncthreads();
@@ -953,12 +954,13 @@ size_t ppo_loss_workspace(int B) {
 }
 
 hipError_t launch_ppo_loss_fwd(const float* logp, const float* v, const int64_t* idx, const float* adv,
-                               const float* ret, const float* old_logp, int B, float clip, float* pg, float* vf,
-                               float* ws, hipStream_t stream) {
+                               const float* ret, const float* old_logp, int B, float clip, int normalize, float* pg,
+                               float* vf, float* ws, hipStream_t stream) {
   if (B <= 0) return hipSuccess;
   const int nblk = (B + LOSS_TPB - 1) / LOSS_TPB;
   hipLaunchKernelGGL(loss_gather_kernel, dim3(nblk), dim3(LOSS_TPB), 0, stream, idx, adv, ret, old_logp, B, ws);
-  hipLaunchKernelGGL(loss_terms_kernel, dim3(nblk), dim3(LOSS_TPB), 0, stream, logp, v, B, clip, ws, nblk);
+  hipLaunchKernelGGL(loss_terms_kernel, dim3(nblk), dim3(LOSS_TPB), 0, stream, logp, v, B, clip, normalize, ws,
+                     nblk);
   hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(64), 0, stream, (const float*)ws, B, nblk, pg, vf);
   return hipGetLastError();
 }

@@ -19,7 +19,7 @@ import numpy as np
 from . import _lib
 from . import reward_functions as _rf
 from ._lib import HsimError
-from .batch import HsBatch
+from .batch import HsBatch, report_warnings
 from .model import HsModel
 from .render import Renderer, write_video
 from .spaces import Box, Env
@@ -228,7 +228,13 @@ class HumanoidEnv(Env):
         self.step_count += 1
         a = torch.as_tensor(np.asarray(action, dtype=np.float32).reshape(1, -1), device=self._batch.device)
         self._batch.step(a)
-        obs, cols = self._batch.host_outputs(ncols=3)      # obs, reward and done flags in one copy
+        # obs, reward, done flags and the warning counters in one copy; a bad-state reset warns as
+        # mj_step's mju_warning does, a lost hand-off raises (batch.report_warnings)
+        obs, cols, warn = self._batch.host_outputs(ncols=3, warnings=True)
+        new = warn - self.__dict__.get("_warn_seen", 0)     # counters start at 0 with the batch
+        self._warn_seen = warn
+        if new.any():
+            report_warnings(new, "step")
         state = obs[0]
         height = state[0]
         truncated = bool(cols[2, 0])

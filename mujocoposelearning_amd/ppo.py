@@ -25,6 +25,7 @@ import torch
 import torch.nn as nn
 
 
+from . import batch as _batch_mod
 from .ppo_ops import (Linear, _GaussLogpFn, _PPOLossFn, _SplitKLinearFn, _SplitKLinearReLUFn,  # noqa: F401
                       _SPLITK_ROWS, adam_clip_step, colsum, gae_device, mlp2_forward, mlp_forward,
                       mlp_head_forward, ppo_act, ppo_loss, ppo_post)
@@ -243,7 +244,8 @@ class PPO:
 
     def __init__(self, env, learning_rate=3e-4, n_steps=2048, batch_size=64, n_epochs=10, gamma=0.99,
                  gae_lambda=0.95, clip_range=0.2, ent_coef=0.0, vf_coef=0.5, max_grad_norm=0.5,
-                 policy_kwargs=None, seed=0, world_size=None, rank=None, sync_grads=None, stagger_episodes=False):
+                 policy_kwargs=None, seed=0, world_size=None, rank=None, sync_grads=None, stagger_episodes=False,
+                 normalize_advantage=True):
         import torch.distributed as dist
         if world_size is None:
             world_size = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
@@ -280,6 +282,9 @@ class PPO:
         self.n_steps, self.batch_size, self.n_epochs = n_steps, batch_size, n_epochs
         self.gamma, self.gae_lambda, self.clip_range = gamma, gae_lambda, clip_range
         self.ent_coef, self.vf_coef, self.max_grad_norm = ent_coef, vf_coef, max_grad_norm
+        # SB3 PPO's normalize_advantage (default True): per-minibatch mean / std; with world > 1 each
+        # rank normalises its own chunk of the global minibatch (tests/test_ppo.py equal-result test)
+        self.normalize_advantage = bool(normalize_advantage)
         self.world_size, self.rank = world_size, rank
         N, T, D, A = env.num_envs, n_steps, env.obs_dim, env.act_dim
         self._plan_minibatches(N)
@@ -579,14 +584,14 @@ class PPO:
         mean, v = self.policy(obs[idx])
         logp = self.policy._logp(mean, act[idx])
         if logp.is_cuda:                            # fused HIP loss (same formulas as below)
-            pg, vf = ppo_loss(logp, v, idx, adv, ret, old_logp, self.clip_range)
+            pg, vf = ppo_loss(logp, v, idx, adv, ret, old_logp, self.clip_range, self.normalize_advantage)
             loss = torch.add(pg, vf, alpha=self.vf_coef)
             if self.ent_coef:                       # SB3's default ent_coef 0: no term, no launches
                 loss = loss - self.ent_coef * self.policy.entropy()
             return loss, pg, vf
         ent_mean = self.policy.entropy()            # = evaluate()'s per-sample entropy, averaged
         a = adv[idx]
-        if a.numel() > 1:
+        if self.normalize_advantage and a.numel() > 1:
             a = (a - a.mean()) / (a.std() + 1e-8)
         ratio = torch.exp(logp - old_logp[idx])
         pg = -torch.min(a * ratio, a * ratio.clamp(1 - self.clip_range, 1 + self.clip_range)).mean()
@@ -752,16 +757,14 @@ class PPO:
         pg, vf = (self._g_stats / n).tolist()
         return dict(policy_loss=pg, value_loss=vf)
 
-    WARN_KINDS = ("Nan, Inf or huge value in QPOS", "Nan, Inf or huge value in QVEL",
-                  "Nan, Inf or huge value in QACC", "contacts dropped past the wide contact tier",
-                  "chunk-queue hand-off lost")
+    WARN_KINDS = _batch_mod.WARN_KINDS
 
     def _check_env_warnings(self):
         """Once per rollout: the env's warning counters (include/hsim.h HS_WARN_*) since the last
         check, summed over ranks.  Bad-state resets are reported the way MuJoCo's mj_step reports
         them (mju_warning: the state was reset with mj_resetData and the run goes on; custom_env.py:160);
         a lost chunk-queue hand-off is a scheduling failure, not physics, so it raises on every
-        rank.  Returns the new counts (also in ``logger["env_warnings"]``)."""
+        rank (batch.report_warnings).  Returns the new counts (also in ``logger["env_warnings"]``)."""
         fn = getattr(self.env, "warning_counts", None)
         if fn is None:
             return None
@@ -775,17 +778,7 @@ class PPO:
             dist.all_reduce(t)
             new = t.cpu().numpy()
         self._warn_new = new
-        if len(new) > 4 and new[4] > 0:
-            from ._lib import HsimError
-            raise HsimError(f"{self.WARN_KINDS[4]} in {int(new[4])} env step(s) of this rollout: a scheduling "
-                            "failure of the step kernel (e.g. more concurrent queued batches than the GPU holds "
-                            "waves for), not physics -- those envs were reset and the rollout is not valid")
-        for k in range(min(4, len(new))):
-            if new[k] > 0:
-                import warnings
-                warnings.warn(f"mj_step warning: {self.WARN_KINDS[k]} in {int(new[k])} env step(s) of this "
-                              "rollout" + (" -- those envs were reset (mj_resetData)" if k < 3 else ""),
-                              RuntimeWarning, stacklevel=3)
+        _batch_mod.report_warnings(new, "rollout")
         return new
 
     def learn(self, total_timesteps, callback=None, log_interval=1):

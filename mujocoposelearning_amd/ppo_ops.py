@@ -87,7 +87,7 @@ class _PPOLossFn(torch.autograd.Function):
     hs_ppo_loss_grad launch backward (dL/dlog_prob, dL/dvalues)."""
 
     @staticmethod
-    def forward(ctx, logp, v, idx, adv, ret, old_logp, clip):
+    def forward(ctx, logp, v, idx, adv, ret, old_logp, clip, normalize=True):
         from . import _lib
         logp, v = logp.contiguous(), v.contiguous()
         B = logp.shape[0]
@@ -98,7 +98,8 @@ class _PPOLossFn(torch.autograd.Function):
         ws = torch.empty(int(L.hs_ppo_loss_workspace(B)), dtype=torch.float32, device=dev)
         st = torch.cuda.current_stream(dev).cuda_stream
         _lib.check(L.hs_ppo_loss(logp.data_ptr(), v.data_ptr(), idx.data_ptr(), adv.data_ptr(), ret.data_ptr(),
-                                 old_logp.data_ptr(), B, float(clip), pg.data_ptr(), vf.data_ptr(), ws.data_ptr(), st))
+                                 old_logp.data_ptr(), B, float(clip), 1 if normalize else 0, pg.data_ptr(), vf.data_ptr(),
+                                 ws.data_ptr(), st))
         ctx.save_for_backward(logp, v, ws)
         ctx.clip = float(clip)
         return pg, vf
@@ -118,15 +119,16 @@ class _PPOLossFn(torch.autograd.Function):
         _lib.check(_lib.lib().hs_ppo_loss_grad(logp.data_ptr(), v.data_ptr(), B, ctx.clip, ws.data_ptr(),
                                                g_pg.data_ptr(), g_vf.data_ptr(), g_logp.data_ptr(), g_v.data_ptr(),
                                                st))
-        return g_logp, g_v, None, None, None, None, None
+        return g_logp, g_v, None, None, None, None, None, None
 
 
-def ppo_loss(logp, v, idx, adv, ret, old_logp, clip):
-    """(policy_loss, value_loss) of one minibatch on a device (hs_ppo_loss / hs_ppo_loss_grad)."""
+def ppo_loss(logp, v, idx, adv, ret, old_logp, clip, normalize=True):
+    """(policy_loss, value_loss) of one minibatch on a device (hs_ppo_loss / hs_ppo_loss_grad);
+    ``normalize``: SB3's normalize_advantage."""
     for t in (adv, ret, old_logp):
         assert t.dtype == torch.float32 and t.is_contiguous() and t.dim() == 1
     assert idx.dtype == torch.int64 and idx.is_contiguous()
-    return _PPOLossFn.apply(logp, v, idx, adv, ret, old_logp, clip)
+    return _PPOLossFn.apply(logp, v, idx, adv, ret, old_logp, clip, normalize)
 
 
 def adam_clip_step(opt, params, max_norm, workspace=None):

@@ -22,7 +22,9 @@ def robust_kneeling_reward(env_data, params=None):
     if h < params['min_height']:
         return h ** 2
     roll, pitch, _ = quaternion_to_euler(qpos[3:7])
-    posture = 0.7 * np.exp(-5.0 * (roll ** 2 + pitch ** 2) / params['max_roll_pitch'] ** 2) + \
+    # same association as the reference (:97-98): the error is divided before it is scaled
+    orientation_error = (roll ** 2 + pitch ** 2) / (params['max_roll_pitch'] ** 2)
+    posture = 0.7 * np.exp(-5.0 * orientation_error) + \
         0.3 * np.exp(-5.0 * np.square(h - params['target_height']))
     com_pos, com_vel = env_data.subtree_com[0], env_data.subtree_linvel[0]
     dist = np.sqrt(com_pos[0] ** 2 + com_pos[1] ** 2)

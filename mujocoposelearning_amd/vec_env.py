@@ -29,7 +29,7 @@ from . import _hsinfo
 from . import _lib
 from . import reward_functions as _rf
 from ._lib import HsimError
-from .batch import HsBatch
+from .batch import HsBatch, report_warnings
 from .model import HsModel
 from .spaces import Box
 
@@ -269,7 +269,8 @@ class HumanoidVecEnv(_Base):
         if not isinstance(a, torch.Tensor):
             a = torch.as_tensor(a, device=self.batch.device)
         self.step_tensors(a)
-        obs_np, cols = self.batch.host_outputs(ncols=7)
+        obs_np, cols, warn = self.batch.host_outputs(ncols=7, warnings=True)
+        self._report_new_warnings(warn)
         rew_np = cols[0].copy()
         term_np, trunc_np = cols[1] != 0, cols[2] != 0
         dones = term_np | trunc_np
@@ -284,6 +285,16 @@ class HumanoidVecEnv(_Base):
             step_count = np.where(dones, cols[5], step_count)
             tot = np.where(dones, cols[6], tot)
         return obs_np, rew_np, dones, StepInfos(obs_np, term_np, trunc_np, step_count, tot, idx, term_obs)
+
+    def _report_new_warnings(self, tot):
+        """The warning counters this step added (the packed copy carries their sums): bad-state resets
+        warn as MuJoCo's mj_step does, a lost hand-off raises HsimError (batch.report_warnings), so
+        SB3's own PPO on this VecEnv sees them too."""
+        prev = self.__dict__.get("_warn_seen")
+        self._warn_seen = tot
+        new = tot - prev if prev is not None else tot
+        if new.any():
+            report_warnings(new, "step")
 
     def warning_counts(self):
         """The per-env warning counters (include/hsim.h HS_WARN_*: bad qpos / qvel / qacc resets,

@@ -42,7 +42,7 @@ def kneeling(qpos, qvel, time, subtree_com0, subtree_linvel0, cfrc_ext, qfrc_act
     p = {**KNEEL_DEFAULTS, **(params or {})}
     h = qpos[:, 2]
     roll, pitch, _ = quaternion_to_euler(qpos[:, 3:7])
-    post = np.exp(-5.0 * (roll ** 2 + pitch ** 2) / p['max_roll_pitch'] ** 2)
+    post = np.exp(-5.0 * ((roll ** 2 + pitch ** 2) / (p['max_roll_pitch'] ** 2)))   # :97-98 association
     hr = np.exp(-5.0 * np.square(h - p['target_height']))
     posture = 0.7 * post + 0.3 * hr
     dist = np.sqrt(subtree_com0[:, 0] ** 2 + subtree_com0[:, 1] ** 2)

@@ -86,7 +86,7 @@ def test_trainer_entry_points_validate_arguments():
                                          8, 33, None))
     assert "null" in err(L.hs_ppo_post(None, None, None, None, None, None, None, 0, 0.9, None, None, 0, None, None,
                                        None, None, None, 4, None))
-    assert "null" in err(L.hs_ppo_loss(None, None, None, None, None, None, 8, 0.2, None, None, None, None))
+    assert "null" in err(L.hs_ppo_loss(None, None, None, None, None, None, 8, 0.2, 1, None, None, None, None))
     assert "null" in err(L.hs_ppo_loss_grad(None, None, 8, 0.2, None, None, None, None, None, None))
     assert "nt" in err(L.hs_adam_clip(17, None, None, None, None, None, None, None, 0.5, 3e-4, 0.9, 0.999, 1e-5,
                                       None))
@@ -115,7 +115,7 @@ def test_trainer_entry_points_validate_arguments():
     assert L.hs_dgrad_mask_partial_rows(32768, 256) == 512 and L.hs_dgrad_mask_partial_rows(4096, 256) == 256
     assert L.hs_dgrad_mask_partial_rows(37, 21) == 2 and L.hs_dgrad_mask_partial_rows(0, 21) == 0
     # empty problems are no-ops, not errors
-    assert L.hs_ppo_loss(None, None, None, None, None, None, 0, 0.2, None, None, None, None) == 0
+    assert L.hs_ppo_loss(None, None, None, None, None, None, 0, 0.2, 1, None, None, None, None) == 0
     assert L.hs_colsum(None, 0, 0, None, None, None, None) == 0
     # workspace sizes: loss 3B + 4 blocks + 2; colsum partial rows bounded; Adam one partial per 1024 elements
     assert L.hs_ppo_loss_workspace(32768) == 3 * 32768 + 4 * 128 + 2
