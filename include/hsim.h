@@ -53,7 +53,13 @@
  * claim counters, so pairs could be stepped twice or skipped).  A call on another stream than the
  * batch's previous call first makes its stream wait for everything already issued on the old one
  * (an event; counted by hs_stream_orders).  Streams in graph capture are not joined this way: the
- * capturing framework orders a capture against its origin stream.
+ * capturing framework orders a capture against its origin stream.  The library keeps the handle of a
+ * batch's last stream to record that event, so a stream a batch was launched on must stay alive until
+ * the batch's next call (or hs_batch_destroy).
+ * Uncached memory (the chunk queue's hand-off rows and sync words, ~1.2 KB per fp64 env) is recycled
+ * within the process as uncached memory only, in power-of-two size classes >= 64 KB: the process keeps
+ * at most the peak of concurrently live uncached memory of each class, each block up to twice its
+ * request, until it exits.
  */
 #ifndef HSIM_H
 #define HSIM_H
@@ -307,8 +313,9 @@ int hs_reward_eval(const hs_model* m, int precision, int reward_id, const double
 /* GAE(gamma, lambda) reverse scan over a device rollout buffer, SB3 semantics: [T][N] float32
  * rewards, values, episode_starts; [N] last_values, last_dones; writes [T][N] advantages and
  * returns (= advantages + values).  All pointers are device memory on the current device;
- * asynchronous on `stream`.  advantages / returns must not overlap the inputs: for T >= 256 the scan
- * runs as three launches that keep their per-chunk maps and carries in those output rows. */
+ * asynchronous on `stream`.  advantages / returns must not overlap the inputs or each other (checked:
+ * an error, not wrong advantages): for T >= 256 the scan runs as three launches that keep their
+ * per-chunk maps and carries in those output rows. */
 int hs_gae(const float* rewards, const float* values, const float* episode_starts, const float* last_values,
            const float* last_dones, float* advantages, float* returns, int T, int N, float gamma, float gae_lambda,
            void* stream);

@@ -973,6 +973,22 @@ int hs_gae(const float* rewards, const float* values, const float* episode_start
   if (T == 0 || N == 0) return 0;
   if (!rewards || !values || !episode_starts || !last_values || !last_dones || !advantages || !returns)
     return fail("hs_gae: null buffer");
+  {  // the T >= 256 path keeps per-chunk maps / carries in the output rows: outputs must not overlap inputs
+    const size_t tn = (size_t)T * (size_t)N * sizeof(float);
+    auto overlap = [](const void* a, size_t na, const void* b, size_t nb) {
+      const char *pa = (const char*)a, *pb = (const char*)b;
+      return pa < pb + nb && pb < pa + na;
+    };
+    const void* outs[2] = {advantages, returns};
+    const void* ins[3] = {rewards, values, episode_starts};
+    if (overlap(advantages, tn, returns, tn)) return fail("hs_gae: advantages and returns overlap");
+    for (const void* o : outs) {
+      for (const void* in : ins)
+        if (overlap(o, tn, in, tn)) return fail("hs_gae: an output ([T][N] advantages / returns) overlaps an input");
+      if (overlap(o, tn, last_values, (size_t)N * sizeof(float)) || overlap(o, tn, last_dones, (size_t)N * sizeof(float)))
+        return fail("hs_gae: an output overlaps last_values / last_dones");
+    }
+  }
   return hip_ok(hs::launch_gae(rewards, values, episode_starts, last_values, last_dones, advantages, returns, T, N,
                                gamma, gae_lambda, (hipStream_t)stream),
                 "gae_kernel")

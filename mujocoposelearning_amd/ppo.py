@@ -301,6 +301,8 @@ class PPO:
         # stagger_episodes: spread the envs' episode clocks after this first reset (not an SB3 option;
         # HumanoidVecEnv.stagger_episode_clocks) so that short rollouts see every episode phase
         if stagger_episodes:
+            if not hasattr(env, "stagger_episode_clocks"):
+                raise ValueError("stagger_episodes=True needs an env with stagger_episode_clocks() (HumanoidVecEnv)")
             env.stagger_episode_clocks()
         elif hasattr(env, "episode_length") and N > 1 and 2 * n_steps < env.episode_length():
             import warnings

@@ -25,7 +25,6 @@ from collections.abc import Sequence
 
 import numpy as np
 
-from . import _hsinfo
 from . import _lib
 from . import reward_functions as _rf
 from ._lib import HsimError
@@ -384,8 +383,12 @@ class StepInfos(Sequence):
         if self._cache is None:
             h, sc, tr, te, tot = self._cols
             pos = {int(i): k for k, i in enumerate(self._idx)}
-            self._cache = _hsinfo.build(h.tolist(), sc.astype(np.int64).tolist(), tr.tolist(), te.tolist(),
-                                        tot.tolist(), pos, self._tobs, 0, self._n)
+            args = (h.tolist(), sc.astype(np.int64).tolist(), tr.tolist(), te.tolist(), tot.tolist(), pos, self._tobs)
+            try:        # the native builder (csrc/hs_infos.c, built for the interpreter of the Makefile)
+                from . import _hsinfo
+                self._cache = _hsinfo.build(*args, 0, self._n)
+            except ImportError:
+                self._cache = _build_infos_py(*args)
         return self._cache
 
     def __getitem__(self, i):
@@ -396,6 +399,22 @@ class StepInfos(Sequence):
 
     def __repr__(self):
         return f"StepInfos({len(self)} envs)"
+
+
+def _build_infos_py(h, sc, tr, te, tot, pos, tobs):
+    """The info dicts in Python (what csrc/hs_infos.c builds): custom_env.py:216-224 keys, plus
+    SB3's terminal_observation / TimeLimit.truncated for the envs that finished this step."""
+    out = []
+    for i in range(len(h)):
+        d = {"height": h[i], "step_count": sc[i], "truncated": tr[i],
+             "truncation_info": {"reason": "timeout"} if tr[i] else {}, "terminated": te[i], "total_reward": tot[i],
+             "reward_components": {}}
+        k = pos.get(i)
+        if k is not None:
+            d["terminal_observation"] = tobs[k]
+            d["TimeLimit.truncated"] = bool(tr[i] and not te[i])
+        out.append(d)
+    return out
 
 
 def _config_of_factory(fn):

@@ -94,6 +94,14 @@ def test_trainer_entry_points_validate_arguments():
     assert "null" in err(L.hs_relu_grad_colsum(None, None, 4, 4, None, None, None))
     assert "null" in err(L.hs_colsum_pair(None, 4, 4, None, None, 4, 4, None, None))
     assert "negative" in err(L.hs_gae(None, None, None, None, None, None, None, -1, 4, 0.99, 0.95, None))
+    # outputs overlapping inputs are rejected (the long-rollout path keeps its carries in the outputs);
+    # fake, never-dereferenced addresses: [T][N] = 4 x 8 floats = 128 B each
+    gae = lambda r, v, s, lv, ld, a, ret: L.hs_gae(r, v, s, lv, ld, a, ret, 4, 8, 0.99, 0.95, None)  # noqa: E731
+    base = 1 << 20
+    r, v, s, lv, ld = base, base + 128, base + 256, base + 384, base + 416
+    assert "overlaps an input" in err(gae(r, v, s, lv, ld, v + 64, base + 4096))
+    assert "advantages and returns overlap" in err(gae(r, v, s, lv, ld, base + 4096, base + 4096 + 64))
+    assert "last_values" in err(gae(r, v, s, lv, ld, base + 4096, lv + 16))
     # the fused policy forward: nn.Linear layouts (ld1 >= D, ld2 / ld3 >= 256), A <= 32, D <= 512
     mlp = lambda D, N, ld1, ld2, ld3, A: L.hs_mlp2_forward(None, D, D, N, None, ld1, None, None, ld2, None,  # noqa: E731
                                                            None, ld3, None, A, None, A, None)

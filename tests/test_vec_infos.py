@@ -38,8 +38,23 @@ def _case(n, seed):
     return obs, term, trunc, sc, tot, idx, tobs_full
 
 
-def test_step_infos_equal_the_eager_dicts():
+import pytest
+
+
+@pytest.mark.parametrize("builder", ["native", "python"])
+def test_step_infos_equal_the_eager_dicts(builder, monkeypatch):
+    """Both builders: the native one, and the Python fallback taken when the extension cannot be
+    imported (not built, or built for another interpreter)."""
+    import sys
     from mujocoposelearning_amd.vec_env import StepInfos
+    if builder == "python":
+        import mujocoposelearning_amd as pkg
+        import mujocoposelearning_amd.vec_env as ve
+        monkeypatch.setitem(sys.modules, "mujocoposelearning_amd._hsinfo", None)   # import -> ImportError
+        monkeypatch.delattr(pkg, "_hsinfo", raising=False)
+        calls = []
+        real = ve._build_infos_py
+        monkeypatch.setattr(ve, "_build_infos_py", lambda *a: calls.append(1) or real(*a))
     for n, seed in ((8, 0), (4096, 1), (1, 2)):
         obs, term, trunc, sc, tot, idx, tobs_full = _case(n, seed)
         infos = StepInfos(obs, term, trunc, sc, tot, idx, tobs_full[idx])
@@ -59,6 +74,8 @@ def test_step_infos_equal_the_eager_dicts():
         assert infos[0]["episode"] == {"r": 1.0}
         if n > 1:
             assert infos[0]["truncation_info"] is not infos[1]["truncation_info"]   # fresh dicts per env
+    if builder == "python":
+        assert len(calls) == 3
 
 
 def test_step_infos_build_4096_in_about_a_millisecond():
