@@ -63,6 +63,26 @@ def algo_bytes_per_env_step(es):
     return 83 * es + 21 * 4 + 436 * es + 2
 
 
+L2_PEAK_GBS = 18800.0      # MI355X_MICROARCH.md "Indexed rows": rows shared by every workgroup, served by the XCD L2s
+PROFILE_ROLLOUT_TRAFFIC = os.path.join(ROOT, "profiles", "traffic_rollout_kernel.json")
+
+
+def rollout_algo_bytes(D, A, k, es=8, nq=28, nv=27, H=256):
+    """Algorithmic bytes per env step of the fused rollout kernel (hs_rollout) over a
+    launch of k env steps.  HBM: per env step the rollout rows written -- obs row (f32 D), actions
+    (f32 A), log-prob, episode start, reward (f32 each), done (1 B), episode return (f64), bootstrap
+    flag (1 B) -- plus, once per launch and env (amortised over k): the state read and written
+    (qpos / qvel / warm start / time in es bytes, step count / episode / 5 warning ints / return),
+    the obs_last row (f32 D), the batch's obs row (es D), the clipped action in and out (f32 A),
+    ep_acc in and out (f64) and episode_start (f32).  L2: the pi net's weights and biases (f32),
+    streamed once per wave and env step for the wave's two envs."""
+    rows = 4 * D + 4 * A + 4 + 4 + 4 + 1 + 8 + 1
+    per_launch = 2 * ((nq + 2 * nv + 1) * es + 7 * 4 + es) + 4 * D + es * D + 2 * 4 * A + 2 * 8 + 4
+    hbm = rows + per_launch / k
+    weights = 4 * (D * H + H * H + H * A + H + H + A)
+    return hbm, weights / 2
+
+
 # ----------------------------------------------------------------------------- CPU baseline
 def _cpu_worker(conn, seed):
     """SubprocVecEnv._worker equivalent around the fp64 oracle env (train_sb3.py:203)."""
@@ -616,15 +636,49 @@ def main():
                   policy_kwargs={"net_arch": {"pi": [256, 256], "vf": [256, 256]}, "activation_fn": "ReLU"})
         ppo = PPO(e, seed=0, world_size=world, rank=rank, **tk)
         ppo.learn(ppo.num_timesteps + n * tk["n_steps"] * world)          # warm-up iteration
+        ppo.rollout_launches = []
         barrier()
         t_tr = time.perf_counter()
         ppo.learn(ppo.num_timesteps + args.train_iters * n * tk["n_steps"] * world)
         barrier()
         ts = max_over_ranks(time.perf_counter() - t_tr)
+        # roofline of the train leg's dominant kernel: the fused rollout launch (hs_rollout), its mean
+        # duration from HIP events recorded around it on its stream (hs_last_tape_ms)
+        rl = getattr(ppo, "rollout_launches", [])
+        train_roof = None
+        if rl:
+            env_steps = sum(s for s, _ in rl) / len(rl)
+            kms = max_over_ranks(sum(ms for _, ms in rl) / len(rl))
+            ksteps = env_steps / n
+            hbm_b, l2_b = rollout_algo_bytes(e.batch.obs_dim, model.nu, ksteps)
+            ach = hbm_b * env_steps / (kms * 1e-3) / 1e9
+            l2a = l2_b * env_steps / (kms * 1e-3) / 1e9
+            rtr = None
+            if os.path.exists(PROFILE_ROLLOUT_TRAFFIC):
+                rtr = json.load(open(PROFILE_ROLLOUT_TRAFFIC))
+            train_roof = dict(
+                bound="hbm", achieved=ach, peak=HBM_PEAK_GBS, unit="GB/s", frac=ach / HBM_PEAK_GBS,
+                traffic=(rtr["hbm_bytes_per_launch"] * env_steps / rtr["env_steps_per_launch"]) if rtr else None,
+                kernel="step_kernel_queue<double,27,false,true> (fused rollout, hs_rollout)",
+                kernel_ms_per_launch=kms, env_steps_per_launch=env_steps, launches=len(rl),
+                algo_bytes_per_env_step=hbm_b,
+                l2_weight_stream=dict(bytes_per_env_step=l2_b, achieved=l2a, peak=L2_PEAK_GBS, unit="GB/s",
+                                      frac=l2a / L2_PEAK_GBS,
+                                      note="pi-net weights (f32) each wave streams per env step for its two envs; "
+                                           "peak: MI355X_MICROARCH.md shared-row L2 rate"),
+                profile=rtr.get("source") if rtr else None,
+                note="HIP events around each hs_rollout kernel launch (hs_last_tape_ms), timed iterations; "
+                     "algorithmic bytes: bench.rollout_algo_bytes (rollout rows per env step + the state, obs and "
+                     "action rows once per launch and env); traffic: 2*FETCH+WRITE of the committed profile scaled "
+                     "to this launch size")
         train_res = dict(value=args.train_iters * n * tk["n_steps"] * ranks / ts, unit="env_steps/s",
                          iterations=args.train_iters, ms_per_iteration=ts / args.train_iters * 1e3,
                          env_precision=args.precision,
                          config={k: v for k, v in tk.items() if k != "policy_kwargs"} | {"net_arch": "[256,256] ReLU"},
+                         roofline=train_roof,
+                         roofline_frac=train_roof["frac"] if train_roof else None,
+                         l2_weight_frac=train_roof["l2_weight_stream"]["frac"] if train_roof else None,
+                         kernel_ms_per_launch=train_roof["kernel_ms_per_launch"] if train_roof else None,
                          note="rollout (policy forward + env step) + GAE + 4 epochs of minibatch updates, "
                               "one gradient all-reduce per optimizer step")
         e.close()

@@ -18,6 +18,8 @@
  *   hs_step_tape         <- K x HumanoidEnv.step over a given action tape (open loop), one launch
  *   hs_rollout           <- SB3 PPO.collect_rollouts' per-step loop (policy + env step + buffers), one launch
  *   hs_physics_step      <- raw `data.ctrl[:] = a; mujoco.mj_step(model, data)` custom_env.py:159-160
+ *   hs_pack_outputs      <- the worker -> main-process pipe transfer of SubprocVecEnv.step_wait (obs,
+ *                           rewards, dones, info values; train_sb3.py:203): one packed device buffer
  *   hs_reward_eval       <- REWARD_FUNCTIONS[type](data, params) reward_functions.py:66-269 (the device
  *                           formulas of hs_step on supplied fields)
  *   hs_debug_lose_handoff   (test hook: mj_step's warning + mj_resetData path, custom_env.py:160)
@@ -207,6 +209,9 @@ typedef struct hs_tape_out {
 int hs_step_tape(hs_batch* b, const float* actions, int n_steps, const hs_tape_out* out, void* stream);
 /* tape launches of this batch that were replayed step by step (resident-tier overflow) */
 int hs_tape_aborts(const hs_batch* b, uint64_t* n);
+/* duration in ms of the last tape / rollout kernel launch of this batch (hs_step_tape, hs_rollout), from
+ * HIP events recorded around it on its stream; -1 before the first one (diagnostics: the bench's roofline) */
+int hs_last_tape_ms(const hs_batch* b, double* ms);
 /* cross-stream waits the library inserted to keep this batch's launches ordered (diagnostics) */
 int hs_stream_orders(const hs_batch* b, uint64_t* n);
 
@@ -263,6 +268,12 @@ int hs_rollout_max_steps(const hs_batch* b);
  * SubprocVecEnv-exact mode where worker i continues its own np.random stream seeded with
  * seed + i (custom_env.py:99-110, SB3 VecEnv.seed).  The arrays stay owned by the caller. */
 int hs_set_autoreset_noise(hs_batch* b, const void* qpos_noise, const void* qvel_noise);
+/* One step's host-bound outputs in ONE launch, for a single device-to-host copy (the SubprocVecEnv
+ * step_wait / Gym step() return values, custom_env.py:216-230, train_sb3.py:203): writes the float64
+ * device buffer out = [obs N x obs_dim][ncols x N columns of reward, terminated, truncated,
+ * total_reward, step_count, terminal_step_count, terminal_total_reward (first ncols of them)]
+ * [warnings ? HS_NWARN x N warning counters (kind-major) : nothing].  Asynchronous on `stream`. */
+int hs_pack_outputs(hs_batch* b, double* out, int ncols, int warnings, void* stream);
 /* ctrl: [N][nu] float32 device (NULL = keep current ctrl).  nsub raw mj_step's, obs refreshed.
  * Resets and raw physics calls always write data.ctrl; env steps (hs_step) only with HS_OUT_CTRL.
  * After an hs_step with HS_OUT_CTRL off the ctrl buffer no longer holds data.ctrl, and until it is

@@ -346,34 +346,45 @@ class HsBatch:
         host memory and synchronized once.  Returns (obs [N, obs_dim] float64, cols [ncols, N]
         float64), views of a fresh pinned block (torch's caching host allocator recycles it once
         both are dropped).  ``warnings=True`` also packs the warning counters summed over the envs
-        (HS_NWARN values, cumulative since the batch was created) and returns them third, as int64."""
+        (HS_NWARN values, cumulative since the batch was created) and returns them third, as int64.
+        One native pack launch (hs_pack_outputs) for a single-group batch."""
         torch = _torch()
         N, D = self.n, self.obs_dim
-        nw = _lib.HS_NWARN if warnings else 0
-        size = N * D + ncols * N + nw
+        nwr = N * _lib.HS_NWARN if warnings else 0          # per-env warning rows (summed on the host)
+        size = N * D + ncols * N + nwr
         dev = self.__dict__.get("_pack_dev")
         if dev is None or dev.numel() != size:
             dev = self._pack_dev = torch.empty(size, dtype=torch.float64, device=self.device)
-        dev[:N * D].view(N, D).copy_(self.t["obs"])
-        cols = dev[N * D:N * D + ncols * N].view(ncols, N)
-        for k in range(ncols):
-            cols[k].copy_(self.t[self._HOST_COLS[k]])
-        if nw:
-            torch.sum(self.t["warning"], 0, dtype=torch.float64, out=dev[N * D + ncols * N:])
+        st = torch.cuda.current_stream(self.device)
+        if len(self._groups) == 1:   # one pack launch (hs_pack_outputs)
+            check(lib().hs_pack_outputs(self._h, dev.data_ptr(), int(ncols), 1 if warnings else 0, st.cuda_stream))
+        else:
+            dev[:N * D].view(N, D).copy_(self.t["obs"])
+            cols = dev[N * D:N * D + ncols * N].view(ncols, N)
+            for k in range(ncols):
+                cols[k].copy_(self.t[self._HOST_COLS[k]])
+            if nwr:
+                dev[N * D + ncols * N:].view(_lib.HS_NWARN, N).copy_(self.t["warning"].t())
         host = torch.empty(size, dtype=torch.float64, pin_memory=True)
         host.copy_(dev, non_blocking=True)
-        torch.cuda.current_stream(self.device).synchronize()
+        st.synchronize()
         a = host.numpy()
         obs, c = a[:N * D].reshape(N, D), a[N * D:N * D + ncols * N].reshape(ncols, N)
-        if not nw:
+        if not nwr:
             return obs, c
-        return obs, c, a[N * D + ncols * N:].astype(np.int64)
+        return obs, c, a[N * D + ncols * N:].reshape(_lib.HS_NWARN, N).sum(1).astype(np.int64)
 
     def tape_aborts(self):
         """Tape launches replayed step by step because an env overflowed the resident tier."""
         v = C.c_uint64(0)
         check(lib().hs_tape_aborts(self._groups[0][0], C.byref(v)))
         return int(v.value)
+
+    def last_tape_ms(self):
+        """Duration (ms, HIP events on its stream) of the last tape / fused-rollout kernel launch."""
+        v = C.c_double(0)
+        check(lib().hs_last_tape_ms(self._groups[0][0], C.byref(v)))
+        return float(v.value)
 
     def stream_orders(self):
         """Cross-stream waits the library inserted because calls of this batch came on different

@@ -43,6 +43,8 @@ struct hs_batch {
   bool last_valid = false;
   hipEvent_t order_ev = nullptr;
   unsigned long long stream_orders = 0;      // cross-stream waits inserted (diagnostics)
+  hipEvent_t tape_ev[2] = {nullptr, nullptr};   // around the last tape / rollout kernel launch
+  float last_tape_ms = -1.f;                 // its duration (hs_last_tape_ms)
 };
 
 namespace {
@@ -258,13 +260,20 @@ int guarded_tape(hs_batch* b, const std::vector<Region>& regs, hipStream_t st, F
     off += (r.bytes + 255) & ~(size_t)255;
   }
   if (!hip_ok(hipMemsetAsync(b->qsync + hs::QS_ABORT, 0, sizeof(int), st), "tape abort word")) return -1;
+  // HIP events right around the kernel launch on its stream (hs_last_tape_ms: the bench's roofline of
+  // the fused rollout kernel); one pair per tape launch, which is one per several env steps
+  for (auto& e : b->tape_ev)
+    if (!e && !hip_ok(hipEventCreate(&e), "hipEventCreate")) return -1;
+  if (!hip_ok(hipEventRecord(b->tape_ev[0], st), "tape event")) return -1;
   int rc = go();
   if (rc) return rc < 0 ? rc : -1;
+  if (!hip_ok(hipEventRecord(b->tape_ev[1], st), "tape event")) return -1;
   int aborted = 0;
   if (!hip_ok(hipMemcpyAsync(&aborted, b->qsync + hs::QS_ABORT, sizeof(int), hipMemcpyDeviceToHost, st),
               "tape abort word") ||
       !hip_ok(hipStreamSynchronize(st), "tape launch"))
     return -1;
+  if (!hip_ok(hipEventElapsedTime(&b->last_tape_ms, b->tape_ev[0], b->tape_ev[1]), "tape event time")) return -1;
   if (!aborted) return 0;
   off = 0;
   for (auto& r : regs) {
@@ -506,6 +515,8 @@ void hs_batch_destroy(hs_batch* b) {
   if (b->qsync) uc_release(b->device, hs::qsync_words(b->n) * sizeof(int), b->qsync);
   if (b->tape_backup) (void)hipFree(b->tape_backup);
   if (b->order_ev) (void)hipEventDestroy(b->order_ev);
+  for (auto& e : b->tape_ev)
+    if (e) (void)hipEventDestroy(e);
   delete b;
 }
 
@@ -1038,6 +1049,34 @@ int hs_reward_eval(const hs_model* m, int precision, int reward_id, const double
   return prec == HS_FP64 ? run(0.0) : run(0.0f);
 }
 
+int hs_pack_outputs(hs_batch* b, double* out, int ncols, int warnings, void* stream) {
+  if (!b || !out) return fail("hs_pack_outputs: null argument");
+  if (ncols < 0 || ncols > 7) return fail("hs_pack_outputs: ncols must be in [0, 7]");
+  DeviceGuard g(b->device);
+  if (order_streams(b, (hipStream_t)stream)) return -1;
+  auto run = [&](auto zero) -> int {
+    using T = decltype(zero);
+    hs::PackArgs<T> a{};
+    a.n = b->n;
+    a.obs_dim = b->obs_dim;
+    a.ncols = ncols;
+    a.nwarn = warnings ? HS_NWARN : 0;
+    a.nwarn_stride = HS_NWARN;
+    a.obs = (const T*)b->buf.obs;
+    a.reward = (const T*)b->buf.reward;
+    a.terminated = b->buf.terminated;
+    a.truncated = b->buf.truncated;
+    a.total_reward = (const T*)b->buf.total_reward;
+    a.step_count = b->buf.step_count;
+    a.term_step_count = b->buf.terminal_step_count;
+    a.term_total_reward = (const T*)b->buf.terminal_total_reward;
+    a.warning = b->buf.warning;
+    a.out = out;
+    return hip_ok(hs::launch_pack<T>(a, (hipStream_t)stream), "pack_kernel") ? 0 : -1;
+  };
+  return b->precision == HS_FP64 ? run(0.0) : run(0.0f);
+}
+
 int hs_batch_counters(const hs_batch* b, uint64_t* wide_reruns) {
   if (!b || !wide_reruns) return fail("null argument");
   DeviceGuard g(b->device);
@@ -1046,6 +1085,12 @@ int hs_batch_counters(const hs_batch* b, uint64_t* wide_reruns) {
       !hip_ok(hipMemcpy(&v, b->redo_total, sizeof v, hipMemcpyDeviceToHost), "counters"))
     return -1;
   *wide_reruns = v;
+  return 0;
+}
+
+int hs_last_tape_ms(const hs_batch* b, double* ms) {
+  if (!b || !ms) return fail("null argument");
+  *ms = (double)b->last_tape_ms;
   return 0;
 }
 

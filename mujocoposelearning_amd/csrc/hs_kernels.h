@@ -200,6 +200,24 @@ struct RewardEvalArgs {
 template <typename T>
 hipError_t launch_reward_eval(const RewardEvalArgs<T>& a, hipStream_t stream);
 
+// one step's host-bound outputs packed into one float64 buffer (hs_pack_outputs)
+template <typename T>
+struct PackArgs {
+  int n, obs_dim, ncols, nwarn, nwarn_stride;
+  const T* obs;
+  const T* reward;
+  const uint8_t* terminated;
+  const uint8_t* truncated;
+  const T* total_reward;
+  const int* step_count;
+  const int* term_step_count;
+  const T* term_total_reward;
+  const int* warning;
+  double* out;
+};
+template <typename T>
+hipError_t launch_pack(const PackArgs<T>& a, hipStream_t stream);
+
 // PPO rollout bookkeeping around the policy GEMMs and the env step (ppo.hip)
 hipError_t launch_ppo_act(const float* mean, int mean_ld, const float* value, int value_ld, const float* log_std,
                           const float* episode_start, uint64_t seed, uint64_t counter, const uint64_t* counter_base,

@@ -3035,7 +3035,50 @@ __global__ __launch_bounds__(256) void reward_eval_kernel(RewardEvalArgs<T> a) {
   a.out[env] = reward_formula(a.reward_id, a.kneel, in);
 }
 
+// hs_pack_outputs: one step's host-bound outputs as ONE float64 buffer in one launch (the drop-in's
+// single device-to-host copy): obs rows, then ncols columns of N values, then the warning rows
+// (column-major: kind k of env i at k * N + i).  Grid-stride over the whole buffer: coalesced writes.
+template <typename T>
+__global__ __launch_bounds__(256) void pack_kernel(PackArgs<T> a) {
+  const size_t nobs = (size_t)a.n * a.obs_dim, ncol = (size_t)a.ncols * a.n, nw = (size_t)a.nwarn * a.n;
+  const size_t total = nobs + ncol + nw;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    double v;
+    if (i < nobs) {
+      v = (double)a.obs[i];
+    } else if (i < nobs + ncol) {
+      const size_t j = i - nobs;
+      const int c = (int)(j / a.n);
+      const size_t e = j - (size_t)c * a.n;
+      switch (c) {
+        case 0: v = (double)a.reward[e]; break;
+        case 1: v = (double)a.terminated[e]; break;
+        case 2: v = (double)a.truncated[e]; break;
+        case 3: v = (double)a.total_reward[e]; break;
+        case 4: v = (double)a.step_count[e]; break;
+        case 5: v = a.term_step_count ? (double)a.term_step_count[e] : 0.0; break;
+        default: v = a.term_total_reward ? (double)a.term_total_reward[e] : 0.0; break;
+      }
+    } else {
+      const size_t j = i - nobs - ncol;
+      const int kind = (int)(j / a.n);
+      const size_t e = j - (size_t)kind * a.n;
+      v = (double)a.warning[e * a.nwarn_stride + kind];
+    }
+    a.out[i] = v;
+  }
+}
+
 }  // namespace
+
+template <typename T>
+hipError_t launch_pack(const PackArgs<T>& a, hipStream_t stream) {
+  const size_t total = (size_t)a.n * (a.obs_dim + a.ncols + a.nwarn);
+  if (total == 0) return hipSuccess;
+  const unsigned blocks = (unsigned)std::min<size_t>((total + 255) / 256, 2048);
+  hipLaunchKernelGGL((pack_kernel<T>), dim3(blocks), dim3(256), 0, stream, a);
+  return hipGetLastError();
+}
 
 template <typename T>
 hipError_t launch_reward_eval(const RewardEvalArgs<T>& a, hipStream_t stream) {
@@ -3160,6 +3203,7 @@ template hipError_t launch_step<float>(const DevModel<float>*, int, const EnvBuf
 template int resident_waves<float>(bool);
 template hipError_t launch_kinematics<float>(const DevModel<float>*, int, const float*, float*, hipStream_t);
 template hipError_t launch_reward_eval<float>(const RewardEvalArgs<float>&, hipStream_t);
+template hipError_t launch_pack<float>(const PackArgs<float>&, hipStream_t);
 #endif
 #if !defined(HS_DEV_F32_ONLY) && !defined(HS_ONLY_F32)
 template hipError_t launch_step<double>(const DevModel<double>*, int, const EnvBuffers<double>&, const float*,
@@ -3171,6 +3215,7 @@ template hipError_t launch_step<double>(const DevModel<double>*, int, const EnvB
 template int resident_waves<double>(bool);
 template hipError_t launch_kinematics<double>(const DevModel<double>*, int, const double*, double*, hipStream_t);
 template hipError_t launch_reward_eval<double>(const RewardEvalArgs<double>&, hipStream_t);
+template hipError_t launch_pack<double>(const PackArgs<double>&, hipStream_t);
 #endif
 
 }  // namespace hs

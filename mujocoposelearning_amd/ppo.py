@@ -410,6 +410,10 @@ class PPO:
         while t0 < T:
             k = min(L, T - t0)
             rc = _lib.check(_lib.lib().hs_rollout(handle, C.byref(cpol), C.byref(rb), t0, k, T, stream))
+            if rc == 0:                       # (env steps, kernel ms by HIP events) of the last launches
+                ms = C.c_double(0)
+                _lib.check(_lib.lib().hs_last_tape_ms(handle, C.byref(ms)))
+                self.rollout_launches = (getattr(self, "rollout_launches", []) + [(k * self.env.num_envs, ms.value)])[-64:]
             if rc == 1:                       # resident-tier overflow: state restored, step by step from t0
                 self.fused_fallbacks = getattr(self, "fused_fallbacks", 0) + 1
                 self._rollout_body(t_from=t0)

@@ -61,3 +61,26 @@ def test_gym_step_warns_on_a_bad_state_reset():
     with pytest.warns(RuntimeWarning, match="QVEL"):
         state, reward, terminated, truncated, info = env.step(a)
     assert np.isfinite(state).all()
+
+
+@pytest.mark.parametrize("precision", ["fp64", "fp32"])
+def test_pack_outputs_equals_the_buffers(precision):
+    """hs_pack_outputs (one launch) writes exactly the obs, the seven host columns and the per-env
+    warning counters that step_wait reads, converted to float64."""
+    import torch
+    from mujocoposelearning_amd.batch import HsBatch
+    from mujocoposelearning_amd.model import HsModel
+    b = HsBatch(HsModel(XML), 37, precision=precision, seed=1)
+    b.configure(frame_skip=3, duration=0.05, reward_id=0, autoreset=1)
+    b.reset()
+    b.t["warning"].copy_(torch.arange(37 * 5, dtype=torch.int32, device=b.device).view(37, 5))
+    for _ in range(9):                                   # past a termination: terminal columns written
+        b.step(torch.zeros(37, 21, device=b.device))
+    obs, cols, warn = b.host_outputs(ncols=7, warnings=True)
+    assert np.array_equal(obs, b.t["obs"].double().cpu().numpy())
+    for k, name in enumerate(b._HOST_COLS):
+        assert np.array_equal(cols[k], b.t[name].double().cpu().numpy()), name
+    assert np.array_equal(warn, b.t["warning"].sum(0).cpu().numpy().astype(np.int64))
+    o2, c2 = b.host_outputs(ncols=3)
+    assert np.array_equal(o2, obs) and np.array_equal(c2, cols[:3])
+    b.close()
