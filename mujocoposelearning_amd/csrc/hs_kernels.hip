@@ -532,6 +532,80 @@ __device__ __forceinline__ T chol_fwd(const T (&L)[NV], T dinv, T b, int sl) {
   chol_fwd_multi<NV, 1>(L, dinv, bb, sl);
   return bb[0];
 }
+// Gauss-Jordan solve of an SPD system A x = b held row-per-lane (sub-lane i: row i in A[], b_i in b),
+// without pivoting (SPD: positive pivot blocks), two pivots per LDS round trip -- the Newton direction
+// of the HS_NEWTON_GJ A/B build (12 % fewer VALU instructions than chol_rows + chol_solve,
+// 8 % slower: the kernel is latency-bound, and the solve needs the Hessian's upper triangle).  No
+// substitutions: every other lane eliminates the pivot columns from its own row, rows above the pivots
+// included.  Step s eliminates columns k = 2s, k + 1 with the 2 x 2 pivot
+// block P (rows k, k + 1 of the current matrix; its trailing block is symmetric, but the two
+// off-diagonal entries are used as computed, so every row's update is exact Gauss-Jordan):
+//   (f0, f1) = (a_ik, a_i,k+1) P^-1,   a_ij -= f0 a_kj + f1 a_k+1,j  (j > k + 1),   b_i likewise.
+// Rows k and k + 1 keep only their block at the end; each lane records its block's entries at its
+// own step and takes its partner's right-hand side by DPP (lanes k, k + 1 are a quad pair): x from
+// the 2 x 2 solve.  `buf` >= 64 T: row k at [0, NV), row k + 1 at [32, 32 + NV), their b at 28 / 60.
+template <int NV, typename T>
+__device__ __forceinline__ T gj_solve2(T (&A)[NV], T b, int sl, T* buf) {
+  static_assert(NV + 1 <= 28, "two pivot rows + their b in 64 slots");
+  using V2 = HIP_vector_type<T, 2>;
+  T qd = T(0), qo = T(0), qr = T(0);     // own block: the other row's diagonal, own off-diagonal, 1 / det
+  T dinv1 = T(0);                        // (a trailing single column, NV odd)
+  static_for<0, NV / 2>([&](auto sc) {
+    constexpr int k = 2 * decltype(sc)::value;
+    const int sl_k = opaque_v(sl);
+    const bool piv = sl_k == k || sl_k == k + 1;
+    if (piv) {                           // lanes k, k + 1 publish their rows' columns >= k and b
+      T* row = buf + (sl_k == k ? 0 : 32);
+      static_for<k / 2, (NV + 1) / 2>([&](auto pc) {
+        constexpr int p = decltype(pc)::value;
+        if constexpr (2 * p + 1 < NV) *reinterpret_cast<V2*>(row + 2 * p) = V2(A[2 * p], A[2 * p + 1]);
+        else row[2 * p] = A[2 * p];
+      });
+      *reinterpret_cast<V2*>(row + 28) = V2(b, T(0));
+    }
+    WSYNC();
+    const V2 r0 = *reinterpret_cast<const V2*>(buf + k), r1 = *reinterpret_cast<const V2*>(buf + 32 + k);
+    const T p00 = r0.x, p01 = r0.y, p10 = r1.x, p11 = r1.y;
+    const T det = p00 * p11 - p01 * p10;
+    const T rdet = recip(det > T(1e-30) ? det : T(1e-30));
+    qd = (sl_k == k) ? p11 : (sl_k == k + 1) ? p00 : qd;
+    qo = (sl_k == k) ? p01 : (sl_k == k + 1) ? p10 : qo;
+    qr = piv ? rdet : qr;
+    const T f0 = piv ? T(0) : (A[k] * p11 - A[k + 1] * p10) * rdet;
+    const T f1 = piv ? T(0) : (A[k + 1] * p00 - A[k] * p01) * rdet;
+    const T b0 = buf[28], b1 = buf[60];
+    static_for<(k + 2) / 2, (NV + 1) / 2>([&](auto pc) {
+      constexpr int p = decltype(pc)::value;
+      if constexpr (2 * p + 1 < NV) {
+        const V2 u = *reinterpret_cast<const V2*>(buf + 2 * p), w = *reinterpret_cast<const V2*>(buf + 32 + 2 * p);
+        A[2 * p] = fma(-f1, w.x, fma(-f0, u.x, A[2 * p]));
+        A[2 * p + 1] = fma(-f1, w.y, fma(-f0, u.y, A[2 * p + 1]));
+      } else {
+        A[2 * p] = fma(-f1, buf[32 + 2 * p], fma(-f0, buf[2 * p], A[2 * p]));
+      }
+    });
+    b = fma(-f1, b1, fma(-f0, b0, b));
+    WSYNC();
+  });
+  if constexpr (NV % 2 == 1) {           // the last column: a single pivot
+    constexpr int k = NV - 1;
+    const int sl_k = opaque_v(sl);
+    const T piv = A[k] > T(1e-30) ? A[k] : T(1e-30);
+    const T r = recip(piv);
+    dinv1 = (sl_k == k) ? r : T(0);
+    if (sl_k == k) *reinterpret_cast<V2*>(buf + 28) = V2(b, r);
+    WSYNC();
+    const V2 br = *reinterpret_cast<const V2*>(buf + 28);
+    const T f = (sl_k == k) ? T(0) : A[k] * br.y;
+    b = fma(-f, br.x, b);
+    WSYNC();
+  }
+  const T bp = dpp<0xB1>(b);             // the pair partner's right-hand side (quad_perm [1,0,3,2])
+  const int sl_e = opaque_v(sl);
+  const T x2 = qr * (qd * b - qo * bp);
+  return (NV % 2 == 1 && sl_e == NV - 1) ? b * dinv1 : x2;
+}
+
 // (A v)_i for a row-per-lane matrix and a vector in LDS (broadcast ds_reads)
 template <int NV, typename T>
 __device__ __forceinline__ T matvec_lds(const T (&A)[NV], const T* v) {
@@ -586,8 +660,11 @@ struct Scratch {
     struct { T crb[MAXBODY][10]; T buf[MAXDOF][6]; } c;          // composite rigid body
     struct { T cdofdot[MAXDOF][6]; T cfrc[MAXBODY][6]; T csub[MAXBODY][6]; } r;   // RNE
     struct { T bvel[MAXBODY][6];                                  // J x mapping (rows, Newton)
-             alignas(16) T cb[MAXDOF][2];                         // Cholesky column pairs
-             T cfrc[MAXBODY][6], linv[MAXBODY][3], mv[MAXBODY][3]; } n;   // full_state (after solve)
+             alignas(16) T cb[MAXDOF][2];                         // Cholesky column pairs / Gauss-Jordan pivot row
+             union {
+               struct { T cfrc[MAXBODY][6], linv[MAXBODY][3], mv[MAXBODY][3]; };   // full_state (after solve)
+               alignas(16) T aug[MAXDOF][6];   // Newton: each dof's contact Hessian aggregate (upper triangle)
+             }; } n;
     // fused rollout's policy forward (fp64 engine only: inside the union's 4 KB there; the fp32
     // engine's union is smaller and must not grow, so its member is a stub)
     struct { alignas(16) float x[sizeof(T) == 8 ? 512 : 4]; alignas(16) float h[sizeof(T) == 8 ? 256 : 4]; } pol;
@@ -1546,7 +1623,9 @@ struct Stepper {
       HS_STAMP(clk, 8);
       if (__ballot(!done) == 0) break;       // both envs of the wave converged
       T H[NV];
+#ifndef HS_NEWTON_GJ
       T hdinv = 0, hdiag = 0;
+#endif
       // Hessian lower rows: M + contact (tree form) + joint limits (diag) + dense rank-1 rows
       {
         T aug[6] = {0, 0, 0, 0, 0, 0};
@@ -1578,6 +1657,33 @@ struct Stepper {
           if (hi >= 0 && s.row_f[hi] != T(0)) dadd += s.row_D[hi];
         }
         HS_STAMP(clk, 27);
+#ifdef HS_NEWTON_GJ
+        // the full symmetric rows (gj_solve2 needs the upper triangle too): H_ij = cdof_j . aug_i for an
+        // ancestor j of dof i, = cdof_i . aug_j for a descendant j (H_ji, with lane j's aggregate read
+        // from LDS), as mass_matrix() builds M's full rows
+        if (sl < NV)
+          for (int k = 0; k < 6; k++) s.u.n.aug[sl][k] = aug[k];
+        WSYNC();
+        {
+          // software-pipelined like the lower-only rows: column j + 1's cdof and aug rows are read
+          // before column j's arithmetic (fenced), so each LDS round trip overlaps the FMAs
+          const uint32_t relm = sl < NV ? m->dof_relmask[sl] : 0u;
+          T cbuf[2][12];
+          auto load = [&](auto jc, T (&dst)[12]) {
+            constexpr int j = decltype(jc)::value;
+            for (int k = 0; k < 6; k++) { dst[k] = s.cdof[j][k]; dst[6 + k] = s.u.n.aug[j][k]; }
+          };
+          load(std::integral_constant<int, 0>{}, cbuf[0]);
+          static_for<0, NV>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            if constexpr (j + 1 < NV) load(std::integral_constant<int, j + 1>{}, cbuf[(j + 1) & 1]);
+            SCHED_FENCE();
+            const T* cj = cbuf[j & 1];
+            const T v = (j <= sl) ? dot6(cj, aug) : dot6(cd, cj + 6);
+            H[j] = Mr[j] + (bit(relm, j) ? v : T(0)) + ((j == sl) ? dadd : T(0));
+          });
+        }
+#else
         // HESS_G columns per scheduling group: their cdof rows are read from LDS together, so one
         // LDS round trip is exposed per group instead of per column
         constexpr int HESS_G = sizeof(T) == 8 ? 2 : 1;
@@ -1614,6 +1720,7 @@ struct Stepper {
             });
           });
         }
+#endif
         HS_STAMP(clk, 28);
         // dense rank-1 rows (tendon limits, body-body contacts): only the rows flagged in
         // dense_mask; the loop runs max(#rows of either half) times (wave-uniform control)
@@ -1659,9 +1766,14 @@ struct Stepper {
         }
       }
       HS_STAMP(clk, 9);
+#ifndef HS_NEWTON_GJ   // the factor + substitutions (HS_NEWTON_GJ: the Gauss-Jordan A/B build)
       chol_rows<NV, T, LDLF>(H, hdinv, sl, s.u.n.cb, &hdiag);   // (LDLF: as L D L')
       HS_STAMP(clk, 15);
       T sdir = -chol_solve<NV, T, LDLF>(H, hdinv, g, sl);
+#else
+      T sdir = -gj_solve2<NV>(H, g, sl, &s.u.n.cb[0][0]);
+      HS_STAMP(clk, 15);
+#endif
       if (sl >= NV) sdir = 0;
       HS_STAMP(clk, 10);
       // exact line search along sdir (piecewise-quadratic cost)

@@ -73,6 +73,7 @@ struct DevModel {
   T jnt_solref[MAXJNT][2], jnt_solimp[MAXJNT][SOLIMP], jnt_margin[MAXJNT];
   int dof_bodyid[MAXDOF], dof_jntid[MAXDOF], dof_qposadr[MAXDOF];   // qposadr: hinge dofs, else -1
   uint32_t dof_ancmask[MAXDOF];       // dof ancestors incl. self (dof_parentid chain)
+  uint32_t dof_relmask[MAXDOF];       // dof ancestors and descendants incl. self (nonzeros of a row of M)
   uint32_t dof_dotmask[MAXDOF];       // dofs whose motion precedes this dof in mj_comVel
   T dof_armature[MAXDOF], dof_damping[MAXDOF], dof_invweight0[MAXDOF];
   T dof_stiffness[MAXDOF], dof_springref[MAXDOF];

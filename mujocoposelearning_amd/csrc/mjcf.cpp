@@ -1080,6 +1080,9 @@ bool build_dev_model(const HostModel& m, DevModel<T>& d, std::string& err) {
     uint32_t anc = 0;
     for (int k = i; k >= 0; k = m.dof_parentid[k]) anc |= 1u << k;
     d.dof_ancmask[i] = anc;
+    d.dof_relmask[i] = anc;
+    for (int k = 0; k < i; k++)      // i is a descendant of each of its ancestors k
+      if ((anc >> k) & 1u) d.dof_relmask[k] |= 1u << i;
     // mj_comVel: a hinge sees the velocity of all its dof ancestors; the 3 rotational dofs of
     // a free joint all see the velocity after its 3 translational dofs; translations see none.
     uint32_t dot = 0;

@@ -165,4 +165,6 @@ if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[2] == "predict":
         predict(prec=sys.argv[1])
         sys.exit(0)
-    main(prec=sys.argv[1] if len(sys.argv) > 1 else "fp32", staggered="staggered" in sys.argv[2:])
+    kw = dict(a.split("=", 1) for a in sys.argv[2:] if "=" in a)
+    main(n=int(kw.get("n", 4096)), prec=sys.argv[1] if len(sys.argv) > 1 else "fp32",
+         staggered="staggered" in sys.argv[2:])
