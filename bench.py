@@ -512,7 +512,7 @@ def main():
         from mujocoposelearning_amd.env import HumanoidEnv
         dropin = {}
         rng_np = np.random.default_rng(3 + rank)
-        for n_x, ks in ((8, 400), (n, 30)):
+        for n_x, ks in ((8, 400), (16, 400), (64, 200), (256, 100), (n, 30)):
             e = make_env(args.precision, 9000, n_x=n_x)
             precondition(e, tape[:, :n_x])
             acts_np = rng_np.uniform(-1, 1, (ks + 5, n_x, model.nu)).astype(np.float32)
@@ -552,8 +552,8 @@ def main():
         dropin["humanoid_env_step"] = dict(ms_per_step=hl * 1e3, value=1.0 / hl, unit="env_steps/s", n_envs=1)
         dropin["note"] = ("numpy surfaces of the reference's call sites, PCIe-inclusive: HumanoidVecEnv.step_async / "
                           "step_wait (SB3 VecEnv API, SubprocVecEnv semantics; obs / rewards / dones / final-step info "
-                          "in one packed pinned copy, infos built lazily) at configs[0]'s 8 envs and configs[1]'s "
-                          "4096, from staggered episode clocks; with_sb3_info_reads also touches every info as SB3's "
+                          "in one packed pinned copy, infos built lazily) at configs[0]'s 8 envs, 16 / 64 / 256 (where the GPU "
+                          "passes the 8-process CPU baseline) and configs[1]'s 4096, from staggered episode clocks; with_sb3_info_reads also touches every info as SB3's "
                           "collect_rollouts does; humanoid_env_step: the single-env Gym step() latency")
 
     # ---- extra sim-only leg: free-running stream groups (opt-in)
