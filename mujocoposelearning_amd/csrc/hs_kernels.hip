@@ -2753,10 +2753,13 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
           const T cu = sl < st.m->nu ? s.ctrl[sl] : T(0);
           const T csum = hsum(cu * cu);
 #else
+          // (each sum only for the reward that reads it: kneeling the energy, stand / walk the torque;
+          // the launch's reward id is wave-uniform)
+          const int rid = opaque(k)->p.reward_id;
           const T e = sl < nv ? st.qfa * s.qvel[sl] : T(0);
-          const T esum = np_sum_half(e * e, 6, nv - 6, lane);
+          const T esum = rid == REWARD_KNEELING ? np_sum_half(e * e, 6, nv - 6, lane) : T(0);
           const T cu = sl < st.m->nu ? s.ctrl[sl] : T(0);
-          const T csum = np_sum_half(cu * cu, 0, st.m->nu, lane);
+          const T csum = (rid == REWARD_STAND || rid == REWARD_WALK) ? np_sum_half(cu * cu, 0, st.m->nu, lane) : T(0);
 #endif
           HS_STAMP(st.clk, 24);
           T r = trunc ? T(0) : compute_reward(st.m, s, k, time, esum, csum);
