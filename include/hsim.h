@@ -22,6 +22,7 @@
  *                           rewards, dones, info values; train_sb3.py:203): one packed device buffer
  *   hs_reward_eval       <- REWARD_FUNCTIONS[type](data, params) reward_functions.py:66-269 (the device
  *                           formulas of hs_step on supplied fields)
+ *   hs_reward            <- the same on the batch's current states (custom_env.py:263-271 _compute_reward)
  *   hs_debug_lose_handoff   (test hook: mj_step's warning + mj_resetData path, custom_env.py:160)
  *   hs_state_io          <- reads/writes of data.qpos/qvel/qacc_warmstart/time/ctrl (custom_env.py:105-117)
  *   hs_get_buffers       <- data.* arrays as device buffers (obs, reward, terminated, ...)
@@ -320,6 +321,16 @@ int hs_reward_eval(const hs_model* m, int precision, int reward_id, const double
                    const void* qpos, const void* qvel, const void* ctrl, const void* time, const void* subtree_com0,
                    const void* subtree_linvel0, const void* cfrc_ext, const void* qfrc_actuator, void* out,
                    void* stream);
+
+/* The reward of every env's current state under any built-in reward <- REWARD_FUNCTIONS[type](data, params)
+ * on each env's data (custom_env.py:263-271): hs_reward_eval on the batch's own buffers (qpos, qvel,
+ * data.ctrl, time, the aux row's subtree com, subtree_linvel / cfrc_ext -- zeros unless HS_FULL_STATE,
+ * as mj_step leaves them -- and the obs row's qfrc_actuator), so it needs HS_OUT_AUX | HS_OUT_CTRL written
+ * by the last step.  out: [N] of the batch precision (device).  kneel_params NULL = the batch's.  After an
+ * hs_step with reward_id r it equals the step's reward buffer bitwise, except for truncated envs (which
+ * the step rewards 0, custom_env.py:201-211) and envs that auto-reset (whose buffers hold the reset
+ * state).  Asynchronous. */
+int hs_reward(hs_batch* b, int reward_id, const double* kneel_params, void* out, void* stream);
 
 /* GAE(gamma, lambda) reverse scan over a device rollout buffer, SB3 semantics: [T][N] float32
  * rewards, values, episode_starts; [N] last_values, last_dones; writes [T][N] advantages and

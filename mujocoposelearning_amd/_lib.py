@@ -108,6 +108,7 @@ def lib():
         "hs_gae": (i, [vp, vp, vp, vp, vp, vp, vp, i, i, C.c_float, C.c_float, vp]),
         "hs_reward_eval": (i, [vp, i, i, vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
         "hs_pack_outputs": (i, [vp, vp, i, i, vp]),
+        "hs_reward": (i, [vp, i, vp, vp, vp]),
         "hs_ppo_act": (i, [vp, i, vp, i, vp, vp, u64, u64, vp, i, vp, vp, vp, vp, vp, i, i, vp]),
         "hs_ppo_post": (i, [vp, vp, vp, vp, vp, vp, vp, i, C.c_float, vp, vp, u64, vp, vp, vp, vp, vp, i, vp]),
         "hs_gauss_logp": (i, [vp, i, vp, vp, vp, i, i, vp]),
@@ -141,7 +142,7 @@ def lib():
 EXPORTED = ("hs_model_load", "hs_model_free", "hs_model_field", "hs_batch_create", "hs_batch_destroy",
             "hs_batch_get_info", "hs_get_buffers", "hs_set_config", "hs_set_seed", "hs_get_config", "hs_reset", "hs_step", "hs_step_tape", "hs_tape_aborts", "hs_last_tape_ms", "hs_stream_orders", "hs_rollout", "hs_rollout_max_steps", "hs_set_autoreset_noise",
             "hs_physics_step", "hs_state_io", "hs_kinematics", "hs_set_debug", "hs_debug_lose_handoff", "hs_get_debug", "hs_synchronize", "hs_batch_counters", "hs_gae",
-            "hs_reward_eval", "hs_pack_outputs",
+            "hs_reward_eval", "hs_reward", "hs_pack_outputs",
             "hs_ppo_act", "hs_ppo_post", "hs_gauss_logp", "hs_gauss_logp_grad",
             "hs_ppo_loss_workspace", "hs_ppo_loss", "hs_ppo_loss_grad", "hs_adam_workspace", "hs_adam_clip",
             "hs_mlp2_forward", "hs_colsum_partial_rows", "hs_relu_grad_colsum", "hs_dgrad_mask_partial_rows",

@@ -380,6 +380,28 @@ class HsBatch:
         check(lib().hs_tape_aborts(self._groups[0][0], C.byref(v)))
         return int(v.value)
 
+    def reward(self, name, params=None, registry=None):
+        """``REWARD_FUNCTIONS[name](data_i, params)`` for every env's current state on the device
+        (``hs_reward``: the step kernel's reward code on the batch's own buffers; custom_env.py:263-271).
+        Needs the aux row and the data.ctrl copy (``configure(aux=True, ctrl=True)``, the default).
+        Returns an [N] tensor of the batch precision."""
+        from .reward_functions import device_reward_id
+        torch = _torch()
+        rid = device_reward_id(name, registry)
+        if rid is None:
+            raise _lib.HsimError(f"reward {name!r} is a host callable: no device formula")
+        kn = None
+        if params is not None:
+            p = {**dict(zip(KNEEL_KEYS, KNEEL_DEFAULTS)), **params}
+            kn = (C.c_double * 9)(*[float(p[k]) for k in KNEEL_KEYS])
+        out = torch.empty(self.n, dtype=self.dtype, device=self.device)
+
+        def go(h, lo, hi, st):
+            check(lib().hs_reward(h, rid, C.cast(kn, C.c_void_p) if kn is not None else None,
+                                  out.data_ptr() + lo * out.element_size(), st))
+        self._launch(go, out)
+        return out
+
     def last_tape_ms(self):
         """Duration (ms, HIP events on its stream) of the last tape / fused-rollout kernel launch."""
         v = C.c_double(0)

@@ -1049,6 +1049,45 @@ int hs_reward_eval(const hs_model* m, int precision, int reward_id, const double
   return prec == HS_FP64 ? run(0.0) : run(0.0f);
 }
 
+int hs_reward(hs_batch* b, int reward_id, const double* kneel_params, void* out, void* stream) {
+  if (!b || !out) return fail("hs_reward: null argument");
+  if (reward_id != HS_REWARD_STAND && reward_id != HS_REWARD_KNEELING && reward_id != HS_REWARD_WALK)
+    return fail("hs_reward: unknown reward id " + std::to_string(reward_id));
+  if (!(b->cfg.outputs & HS_OUT_AUX) || !(b->cfg.outputs & HS_OUT_CTRL) || b->ctrl_stale)
+    return fail("hs_reward: needs the aux row (subtree com) and the data.ctrl copy (HS_OUT_AUX | HS_OUT_CTRL) "
+                "written by the last step");
+  const hs::HostModel& h = b->model->host;
+  DeviceGuard g(b->device);
+  if (order_streams(b, (hipStream_t)stream)) return -1;
+  const int o4 = (h.nq - 2) + h.nv + 16 * h.nbody;   // qfrc_actuator's offset in the obs row (custom_env.py:250)
+  const double* kn = kneel_params ? kneel_params : b->cfg.kneel_params;
+  auto run = [&](auto zero) -> int {
+    using T = decltype(zero);
+    hs::RewardEvalArgs<T> a{};
+    a.reward_id = reward_id;
+    a.n = b->n;
+    a.nq = h.nq;
+    a.nv = h.nv;
+    a.nu = h.nu;
+    a.nbody = h.nbody;
+    for (int k = 0; k < 9; k++) a.kneel[k] = kn[k];
+    a.qpos = (const T*)b->buf.qpos;
+    a.qvel = (const T*)b->buf.qvel;
+    a.ctrl = (const T*)b->buf.ctrl;
+    a.time = (const T*)b->buf.time;
+    a.subtree_com0 = (const T*)b->buf.aux + hs::MAXDOF;   // aux row: qacc[MAXDOF], com[3], ...
+    a.ld_com = hs::AUXDIM;
+    a.subtree_linvel0 = (const T*)b->buf.subtree_linvel;   // zeros unless HS_FULL_STATE (mj_step leaves it)
+    a.ld_linv = 3 * h.nbody;
+    a.cfrc_ext = (const T*)b->buf.cfrc_ext;
+    a.qfrc_actuator = (const T*)b->buf.obs + o4;
+    a.ld_qfrc = b->obs_dim;
+    a.out = (T*)out;
+    return hip_ok(hs::launch_reward_eval<T>(a, (hipStream_t)stream), "reward_eval_kernel") ? 0 : -1;
+  };
+  return b->precision == HS_FP64 ? run(0.0) : run(0.0f);
+}
+
 int hs_pack_outputs(hs_batch* b, double* out, int ncols, int warnings, void* stream) {
   if (!b || !out) return fail("hs_pack_outputs: null argument");
   if (ncols < 0 || ncols > 7) return fail("hs_pack_outputs: ncols must be in [0, 7]");

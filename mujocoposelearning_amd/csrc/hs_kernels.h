@@ -196,6 +196,9 @@ struct RewardEvalArgs {
   const T* cfrc_ext;          // [n][nbody][6]
   const T* qfrc_actuator;     // [n][nv]
   T* out;                     // [n]
+  // row strides (elements) of subtree_com0 / subtree_linvel0 / qfrc_actuator; 0 = packed (3, 3, nv) --
+  // hs_reward reads the batch's own buffers in place (aux row, subtree_linvel rows, obs rows)
+  int ld_com, ld_linv, ld_qfrc;
 };
 template <typename T>
 hipError_t launch_reward_eval(const RewardEvalArgs<T>& a, hipStream_t stream);

@@ -3126,8 +3126,9 @@ __global__ __launch_bounds__(256) void reward_eval_kernel(RewardEvalArgs<T> a) {
   const long long env = ((long long)blockIdx.x * blockDim.x + threadIdx.x) / HL;
   const bool ok = env < a.n;
   const int nv = a.nv, nu = a.nu;
+  const long long ldc = a.ld_com ? a.ld_com : 3, ldl = a.ld_linv ? a.ld_linv : 3, ldq = a.ld_qfrc ? a.ld_qfrc : nv;
   T e = T(0), cu = T(0);
-  if (ok && sl < nv) e = a.qfrc_actuator[env * nv + sl] * a.qvel[env * nv + sl];
+  if (ok && sl < nv) e = a.qfrc_actuator[env * ldq + sl] * a.qvel[env * nv + sl];
   if (ok && sl < nu) cu = a.ctrl[env * nu + sl];
   const T esum = np_sum_half(e * e, 6, nv - 6, lane);   // every lane of the wave takes part
   const T csum = np_sum_half(cu * cu, 0, nu, lane);
@@ -3141,12 +3142,12 @@ __global__ __launch_bounds__(256) void reward_eval_kernel(RewardEvalArgs<T> a) {
   in.qz = q[6];
   in.vx = a.qvel[env * nv];
   in.time = a.time[env];
-  in.com0 = a.subtree_com0[env * 3];
-  in.com1 = a.subtree_com0[env * 3 + 1];
+  in.com0 = a.subtree_com0[env * ldc];
+  in.com1 = a.subtree_com0[env * ldc + 1];
   {
 #pragma clang fp contract(off)
     in.comv = T(0);
-    for (int d = 0; d < 3; d++) in.comv += a.subtree_linvel0[env * 3 + d] * a.subtree_linvel0[env * 3 + d];
+    for (int d = 0; d < 3; d++) in.comv += a.subtree_linvel0[env * ldl + d] * a.subtree_linvel0[env * ldl + d];
   }
   const T* cf = a.cfrc_ext + (env * a.nbody + a.nbody - 2) * 6;
   in.lf = T(0);
