@@ -261,3 +261,25 @@ def test_step_tape_longer_than_511_steps(model):
     assert info_a["aborts"] == 0
     _same("final", fin_a, fin_b)
     _same("after", aft_a, aft_b)
+
+
+def test_last_tape_ms_times_the_tape_launch(model):
+    """hs_last_tape_ms (the bench's train-leg roofline reads it for hs_rollout): -1 before any tape
+    launch, then the last tape kernel's duration from HIP events on its stream -- positive, and no
+    longer than the host-timed call around it."""
+    import time
+
+    import torch
+    from mujocoposelearning_amd.batch import HsBatch
+    b = HsBatch(model, 256, precision="fp64", seed=2)
+    b.configure(frame_skip=3, duration=10.0, reward_id=0, autoreset=1)
+    b.reset()
+    assert b.last_tape_ms() == -1.0
+    acts = torch.zeros(8, 256, 21, device="cuda")
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    b.step_tape(acts, outputs=False)
+    host_ms = (time.perf_counter() - t0) * 1e3
+    ms = b.last_tape_ms()
+    assert 0.0 < ms <= host_ms, (ms, host_ms)
+    b.close()
