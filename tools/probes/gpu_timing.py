@@ -87,7 +87,7 @@ def main(n=4096, steps=20, prec="fp32", staggered=False):
         for a_, e_ in zip(qs, qe):
             busy[int(a_ / span * 199):int(e_ / span * 199) + 1] += 1
         print("  busy waves over the launch (20 bins): " + " ".join(f"{v:.0f}" for v in busy.reshape(20, 10).mean(1)))
-    np.savez(os.path.join(ROOT, "gpurun_out", f"timing_{prec}.npz"), life=life, st=st, en=en,
+    np.savez(os.path.join(ROOT, "gpurun_out", f"timing_{prec}_{n}.npz"), life=life, st=st, en=en,
              it=dbg[11100:11100 + 2 * len(life)], q0=q0, qw=qw)
     it = b.get_debug()[11100:11100 + 2 * len(life)].reshape(-1, 2)
     wmax, wsum = it.max(1), it.sum(1)
