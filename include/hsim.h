@@ -24,6 +24,7 @@
  *                           formulas of hs_step on supplied fields)
  *   hs_reward            <- the same on the batch's current states (custom_env.py:263-271 _compute_reward)
  *   hs_debug_lose_handoff   (test hook: mj_step's warning + mj_resetData path, custom_env.py:160)
+ *   hs_last_tape_ms, hs_tape_aborts, hs_stream_orders, hs_batch_counters   (diagnostics)
  *   hs_state_io          <- reads/writes of data.qpos/qvel/qacc_warmstart/time/ctrl (custom_env.py:105-117)
  *   hs_get_buffers       <- data.* arrays as device buffers (obs, reward, terminated, ...)
  *   hs_last_error        <- mujoco's error callback / MjModel load error string
