@@ -2747,12 +2747,6 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
           step_count += 1;
           bool trunc = step_count >= k->p.max_steps;
           // np.sum(np.square(qfrc_actuator[-nj:] * qvel[6:])) and np.sum(np.square(ctrl)) in numpy's order
-#ifdef HS_REWARD_HSUM   // (A/B build: round 5's butterfly sums)
-          const T e = (sl >= 6 && sl < nv) ? st.qfa * s.qvel[sl] : T(0);
-          const T esum = hsum(e * e);
-          const T cu = sl < st.m->nu ? s.ctrl[sl] : T(0);
-          const T csum = hsum(cu * cu);
-#else
           // (each sum only for the reward that reads it: kneeling the energy, stand / walk the torque;
           // the launch's reward id is wave-uniform)
           const int rid = opaque(k)->p.reward_id;
@@ -2760,7 +2754,6 @@ __device__ __forceinline__ void step_pair(KPtr<T> ka, Scratch<T, C>* smem, PgsCa
           const T esum = rid == REWARD_KNEELING ? np_sum_half(e * e, 6, nv - 6, lane) : T(0);
           const T cu = sl < st.m->nu ? s.ctrl[sl] : T(0);
           const T csum = (rid == REWARD_STAND || rid == REWARD_WALK) ? np_sum_half(cu * cu, 0, st.m->nu, lane) : T(0);
-#endif
           HS_STAMP(st.clk, 24);
           T r = trunc ? T(0) : compute_reward(st.m, s, k, time, esum, csum);
           HS_STAMP(st.clk, 25);
