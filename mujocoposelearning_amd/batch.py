@@ -380,9 +380,10 @@ class HsBatch:
         check(lib().hs_tape_aborts(self._groups[0][0], C.byref(v)))
         return int(v.value)
 
-    def reward(self, name, params=None, registry=None):
+    def compute_reward(self, name, params=None, registry=None):
         """``REWARD_FUNCTIONS[name](data_i, params)`` for every env's current state on the device
-        (``hs_reward``: the step kernel's reward code on the batch's own buffers; custom_env.py:263-271).
+        (``hs_reward``: the step kernel's reward code on the batch's own buffers; custom_env.py:263-271
+        ``_compute_reward``; ``self.reward`` stays the last step's reward buffer).
         Needs the aux row and the data.ctrl copy (``configure(aux=True, ctrl=True)``, the default).
         Returns an [N] tensor of the batch precision."""
         from .reward_functions import device_reward_id

@@ -176,3 +176,13 @@ def test_struct_layouts_match_the_c_compiler(tmp_path):
         assert got[(name, "size")] == C.sizeof(cls), name
         for f, _ in cls._fields_:
             assert got[(name, f)] == getattr(cls, f).offset, (name, f)
+
+
+def test_batch_buffer_views_are_not_shadowed_by_methods():
+    """HsBatch serves its device buffers (b.obs, b.reward, ...) through __getattr__, which a class
+    attribute of the same name would shadow silently (a method named ``reward`` once did)."""
+    from mujocoposelearning_amd import _lib
+    from mujocoposelearning_amd.batch import HsBatch
+    names = [f[0] for f in _lib.hs_buffers._fields_]
+    assert "reward" in names and "obs" in names
+    assert [n for n in names if hasattr(HsBatch, n)] == []
