@@ -34,13 +34,14 @@ static PyObject* build_one(PyObject* h, PyObject* sc, PyObject* tr, PyObject* te
   PyObject* tinfo = PyDict_New();
   if (!tinfo) goto fail;
   if (is_trunc && PyDict_SetItem(tinfo, k_reason, v_timeout) < 0) { Py_DECREF(tinfo); goto fail; }
+  if (set_new(d, k_reward_components, PyDict_New()) < 0) { Py_DECREF(tinfo); goto fail; }
+  /* keys in custom_env.py:216-224's order */
   if (PyDict_SetItem(d, k_height, PyList_GET_ITEM(h, i)) < 0 ||
       PyDict_SetItem(d, k_step_count, PyList_GET_ITEM(sc, i)) < 0 ||
       PyDict_SetItem(d, k_truncated, trunc) < 0 ||
       set_new(d, k_truncation_info, tinfo) < 0 ||
       PyDict_SetItem(d, k_terminated, term) < 0 ||
-      PyDict_SetItem(d, k_total_reward, PyList_GET_ITEM(tot, i)) < 0 ||
-      set_new(d, k_reward_components, PyDict_New()) < 0)
+      PyDict_SetItem(d, k_total_reward, PyList_GET_ITEM(tot, i)) < 0)
     goto fail;
   if ((is_trunc || is_term) && done_pos != Py_None) {
     PyObject* key = PyLong_FromSsize_t(i);

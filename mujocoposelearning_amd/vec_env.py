@@ -406,9 +406,8 @@ def _build_infos_py(h, sc, tr, te, tot, pos, tobs):
     SB3's terminal_observation / TimeLimit.truncated for the envs that finished this step."""
     out = []
     for i in range(len(h)):
-        d = {"height": h[i], "step_count": sc[i], "truncated": tr[i],
-             "truncation_info": {"reason": "timeout"} if tr[i] else {}, "terminated": te[i], "total_reward": tot[i],
-             "reward_components": {}}
+        d = {"reward_components": {}, "height": h[i], "step_count": sc[i], "truncated": tr[i],
+             "truncation_info": {"reason": "timeout"} if tr[i] else {}, "terminated": te[i], "total_reward": tot[i]}
         k = pos.get(i)
         if k is not None:
             d["terminal_observation"] = tobs[k]

@@ -427,9 +427,9 @@ def _reference_step_wait(env, actions):
     tot = np.where(dones, env.batch.terminal_total_reward.double().cpu().numpy(), tot)
     infos = []
     for i in range(env.num_envs):
-        info = {"height": None, "step_count": int(step_count[i]), "truncated": bool(trunc_np[i]),
-                "truncation_info": {"reason": "timeout"} if trunc_np[i] else {}, "terminated": bool(term_np[i]),
-                "total_reward": float(tot[i]), "reward_components": {}}
+        info = {"reward_components": {}, "height": None, "step_count": int(step_count[i]),   # custom_env.py:216-224
+                "truncated": bool(trunc_np[i]), "truncation_info": {"reason": "timeout"} if trunc_np[i] else {},
+                "terminated": bool(term_np[i]), "total_reward": float(tot[i])}
         if dones[i]:
             info["terminal_observation"] = term_obs[i]
             info["TimeLimit.truncated"] = bool(trunc_np[i] and not term_np[i])

@@ -11,9 +11,9 @@ def _eager(obs, term, trunc, step_count, total, term_obs_full):
     dones = term | trunc
     out = []
     for i in range(len(term)):
-        info = {"height": None, "step_count": int(step_count[i]), "truncated": bool(trunc[i]),
-                "truncation_info": {"reason": "timeout"} if trunc[i] else {}, "terminated": bool(term[i]),
-                "total_reward": float(total[i]), "reward_components": {}}
+        info = {"reward_components": {}, "height": None, "step_count": int(step_count[i]),   # custom_env.py:216-224 order
+                "truncated": bool(trunc[i]), "truncation_info": {"reason": "timeout"} if trunc[i] else {},
+                "terminated": bool(term[i]), "total_reward": float(total[i])}
         if dones[i]:
             info["terminal_observation"] = term_obs_full[i]
             info["TimeLimit.truncated"] = bool(trunc[i] and not term[i])
