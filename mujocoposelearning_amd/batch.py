@@ -339,7 +339,7 @@ class HsBatch:
     _HOST_COLS = ("reward", "terminated", "truncated", "total_reward", "step_count", "terminal_step_count",
                   "terminal_total_reward")
 
-    def host_outputs(self, ncols=3, warnings=False, during=None):
+    def host_outputs(self, ncols=3, warnings=False):
         """One step's outputs on the host in ONE device-to-host copy: the obs and the first ``ncols``
         of (reward, terminated, truncated, total_reward, step_count, terminal_step_count,
         terminal_total_reward), packed on the device into one float64 buffer, copied into pinned
@@ -347,10 +347,7 @@ class HsBatch:
         float64), views of a fresh pinned block (torch's caching host allocator recycles it once
         both are dropped).  ``warnings=True`` also packs the warning counters summed over the envs
         (HS_NWARN values, cumulative since the batch was created) and returns them third, as int64.
-        One native pack launch (hs_pack_outputs) for a single-group batch.
-        ``during(cols, warn, height, obs_landed)``: the columns, the warning sums and every env's
-        obs[:, 0] are copied FIRST; the callback runs on the host while the obs block is still in
-        flight (``obs_landed()`` polls its arrival) and its result is returned last."""
+        One native pack launch (hs_pack_outputs) for a single-group batch."""
         torch = _torch()
         N, D = self.n, self.obs_dim
         nwr = N * _lib.HS_NWARN if warnings else 0          # per-env warning rows (summed on the host)
@@ -368,8 +365,6 @@ class HsBatch:
                 cols[k].copy_(self.t[self._HOST_COLS[k]])
             if nwr:
                 dev[N * D + ncols * N:].view(_lib.HS_NWARN, N).copy_(self.t["warning"].t())
-        if during is not None:
-            return self._host_outputs_overlapped(dev, ncols, nwr, st, during)
         host = torch.empty(size, dtype=torch.float64, pin_memory=True)
         host.copy_(dev, non_blocking=True)
         st.synchronize()
@@ -378,30 +373,6 @@ class HsBatch:
         if not nwr:
             return obs, c
         return obs, c, a[N * D + ncols * N:].reshape(_lib.HS_NWARN, N).sum(1).astype(np.int64)
-
-    def _host_outputs_overlapped(self, dev, ncols, nwr, st, during):
-        torch = _torch()
-        N, D = self.n, self.obs_dim
-        tail = ncols * N + nwr
-        h0 = self.__dict__.get("_h0_dev")
-        if h0 is None or h0.numel() != N:
-            h0 = self._h0_dev = torch.empty(N, dtype=torch.float64, device=self.device)
-        h0.copy_(dev[:N * D].view(N, D)[:, 0])
-        small = torch.empty(tail + N, dtype=torch.float64, pin_memory=True)
-        small[:tail].copy_(dev[N * D:], non_blocking=True)
-        small[tail:].copy_(h0, non_blocking=True)
-        ev_small, ev_obs = torch.cuda.Event(), torch.cuda.Event()
-        ev_small.record(st)
-        host = torch.empty(N * D, dtype=torch.float64, pin_memory=True)
-        host.copy_(dev[:N * D], non_blocking=True)
-        ev_obs.record(st)
-        ev_small.synchronize()
-        a = small.numpy()
-        c = a[:ncols * N].reshape(ncols, N)
-        warn = a[ncols * N:tail].reshape(_lib.HS_NWARN, N).sum(1).astype(np.int64) if nwr else None
-        r = during(c, warn, a[tail:], ev_obs.query)
-        ev_obs.synchronize()
-        return host.numpy().reshape(N, D), c, warn, r
 
     def tape_aborts(self):
         """Tape launches replayed step by step because an env overflowed the resident tier."""

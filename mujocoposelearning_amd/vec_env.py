@@ -21,7 +21,6 @@ seed + i and the worker's global numpy stream continues across auto-resets).
 from __future__ import annotations
 
 import copy
-import os
 from collections.abc import Sequence
 
 import numpy as np
@@ -269,23 +268,22 @@ class HumanoidVecEnv(_Base):
         if not isinstance(a, torch.Tensor):
             a = torch.as_tensor(a, device=self.batch.device)
         self.step_tensors(a)
-        # the scalar columns land first; the info dicts are built while the obs block is in flight
-        if _OVERLAP_INFOS:
-            obs_np, cols, warn, pre = self.batch.host_outputs(ncols=7, warnings=True, during=_prebuild_infos)
-        else:   # A/B: one copy, then the infos lazily on first access
-            obs_np, cols, warn = self.batch.host_outputs(ncols=7, warnings=True)
-            pre = _prebuild_infos(cols, warn, obs_np[:, 0], lambda: True)
+        obs_np, cols, warn = self.batch.host_outputs(ncols=7, warnings=True)
         self._report_new_warnings(warn)
         rew_np = cols[0].copy()
-        term_np, trunc_np, dones, idx, step_count, tot, height, built = pre
+        term_np, trunc_np = cols[1] != 0, cols[2] != 0
+        dones = term_np | trunc_np
+        idx = np.flatnonzero(dones)
         term_obs = None
+        step_count, tot = cols[4], cols[3]
         if idx.size:
             # the finished episodes' final info (SubprocVecEnv returns the last step's info before
             # the worker resets: step_count 667 / 750, the episode's total_reward; custom_env.py:216-224)
             rows = torch.as_tensor(idx, device=self.batch.device)
             term_obs = self.batch.terminal_obs.index_select(0, rows).double().cpu().numpy()
-        return obs_np, rew_np, dones, StepInfos(obs_np, term_np, trunc_np, step_count, tot, idx, term_obs,
-                                                height=height, prefix=built)
+            step_count = np.where(dones, cols[5], step_count)
+            tot = np.where(dones, cols[6], tot)
+        return obs_np, rew_np, dones, StepInfos(obs_np, term_np, trunc_np, step_count, tot, idx, term_obs)
 
     def _report_new_warnings(self, tot):
         """The warning counters this step added (the packed copy carries their sums): bad-state resets
@@ -357,43 +355,6 @@ class HumanoidVecEnv(_Base):
         return indices
 
 
-# envs per native-builder call while the obs copy is in flight (one call ~0.05 ms at 512)
-_PREBUILD_CHUNK = 512
-# HSIM_INFO_OVERLAP=0: no info building during the obs copy (A/B switch, profiles/LOG.md)
-_OVERLAP_INFOS = os.environ.get("HSIM_INFO_OVERLAP", "1") != "0"
-
-
-def _prebuild_infos(cols, warn, height, obs_landed):
-    """host_outputs' ``during`` hook of step_wait: from the scalar columns (reward, terminated,
-    truncated, total_reward, step_count, terminal_step_count, terminal_total_reward) and obs[:, 0],
-    the done flags and the info columns, and the info dicts of a prefix of the envs, built chunk by
-    chunk until the obs block has landed (a consumer that reads no info never waits for them).
-    Finished envs get their terminal keys once the terminal obs are fetched (StepInfos)."""
-    term_np, trunc_np = cols[1] != 0, cols[2] != 0
-    dones = term_np | trunc_np
-    idx = np.flatnonzero(dones)
-    step_count, tot = cols[4], cols[3]
-    if idx.size:
-        step_count = np.where(dones, cols[5], step_count)
-        tot = np.where(dones, cols[6], tot)
-    built = []
-    n = len(term_np)
-    if not obs_landed():
-        try:
-            from . import _hsinfo
-        except ImportError:
-            _hsinfo = None
-        if _hsinfo is not None:
-            lists = (height.tolist(), step_count.astype(np.int64).tolist(), trunc_np.tolist(), term_np.tolist(),
-                     tot.tolist())
-            k = 0
-            while k < n and not obs_landed():
-                hi = min(n, k + _PREBUILD_CHUNK)
-                built += _hsinfo.build(*lists, None, None, k, hi)
-                k = hi
-    return term_np, trunc_np, dones, idx, step_count, tot, height, built
-
-
 class StepInfos(Sequence):
     """The ``infos`` of one ``step_wait``: a read-only sequence of the per-env info dicts
     SubprocVecEnv returns (custom_env.py:216-230 keys; for a finished env also
@@ -402,10 +363,10 @@ class StepInfos(Sequence):
     annotate one, as SB3's VecMonitor does with ``episode``); a consumer that reads none pays
     nothing.  Building 4096 dicts in Python costs ~5 ms per step, more than the physics."""
 
-    __slots__ = ("_cols", "_idx", "_tobs", "_cache", "_n", "_pre")
+    __slots__ = ("_cols", "_idx", "_tobs", "_cache", "_n")
 
-    def __init__(self, obs, term, trunc, step_count, total, done_idx, term_obs, height=None, prefix=None):
-        h = (obs[:, 0] if height is None else height).copy()
+    def __init__(self, obs, term, trunc, step_count, total, done_idx, term_obs):
+        h = obs[:, 0].copy()
         if done_idx.size:
             h[done_idx] = term_obs[:, 0]
         self._n = len(term)
@@ -414,18 +375,6 @@ class StepInfos(Sequence):
         self._idx = done_idx
         self._tobs = term_obs
         self._cache = None
-        # dicts already built for envs [0, len(prefix)) without their terminal keys (step_wait builds
-        # them while the obs copy is in flight): the finished envs among them are completed here
-        self._pre = prefix or None
-        if self._pre:
-            m = len(self._pre)
-            for k, i in enumerate(done_idx):
-                if i >= m:
-                    break
-                d = self._pre[i]
-                d["height"] = float(term_obs[k, 0])
-                d["terminal_observation"] = term_obs[k]
-                d["TimeLimit.truncated"] = bool(trunc[i] and not term[i])
 
     def __len__(self):
         return self._n
@@ -435,16 +384,11 @@ class StepInfos(Sequence):
             h, sc, tr, te, tot = self._cols
             pos = {int(i): k for k, i in enumerate(self._idx)}
             args = (h.tolist(), sc.astype(np.int64).tolist(), tr.tolist(), te.tolist(), tot.tolist(), pos, self._tobs)
-            pre = self._pre or []
-            if len(pre) == self._n:
-                self._cache = pre
-            else:
-                try:    # the native builder (csrc/hs_infos.c, built for the interpreter of the Makefile)
-                    from . import _hsinfo
-                    self._cache = pre + _hsinfo.build(*args, len(pre), self._n)
-                except ImportError:
-                    self._cache = _build_infos_py(*args)
-            self._pre = None
+            try:        # the native builder (csrc/hs_infos.c, built for the interpreter of the Makefile)
+                from . import _hsinfo
+                self._cache = _hsinfo.build(*args, 0, self._n)
+            except ImportError:
+                self._cache = _build_infos_py(*args)
         return self._cache
 
     def __getitem__(self, i):

@@ -91,36 +91,3 @@ def test_step_infos_build_4096_in_about_a_millisecond():
     _eager(obs, term, trunc, sc, tot, tobs_full)
     eager = time.perf_counter() - t0
     assert best < 0.5 * eager, (best, eager)
-
-
-@pytest.mark.parametrize("landed_after", [0, 2, 10 ** 9], ids=["landed", "partial", "never"])
-def test_infos_prebuilt_while_the_obs_copy_is_in_flight(landed_after):
-    """step_wait's overlap: _prebuild_infos builds a prefix of the dicts from the scalar columns
-    while the obs block is in flight (polled: landed at once, after two chunks, or never), StepInfos
-    completes the finished envs among them and builds the rest on access -- equal to the eager dicts."""
-    from mujocoposelearning_amd.vec_env import StepInfos, _prebuild_infos
-    n = 4096
-    obs, term, trunc, sc, tot, idx, tobs_full = _case(n, 4)
-    cols = np.zeros((7, n))
-    cols[1], cols[2] = term, trunc
-    cols[3], cols[6] = tot + 1.0, tot         # running total (post-reset) vs the finished episode's total
-    cols[4], cols[5] = sc + 1, sc
-    dones = term | trunc
-    tot_ref = np.where(dones, cols[6], cols[3])
-    sc_ref = np.where(dones, cols[5], cols[4])
-    polls = []
-    pre = _prebuild_infos(cols, None, obs[:, 0].copy(), lambda: polls.append(1) or len(polls) > landed_after)
-    te, tr, dn, ix, step_count, total, height, built = pre
-    assert np.array_equal(ix, idx) and np.array_equal(step_count, sc_ref) and np.array_equal(total, tot_ref)
-    assert len(built) == {0: 0, 2: 512, 10 ** 9: n}[landed_after]   # (the first poll gates the whole build)
-    infos = StepInfos(obs, te, tr, step_count, total, ix, tobs_full[ix], height=height, prefix=built)
-    ref = _eager(obs, term, trunc, sc_ref, tot_ref, tobs_full)
-    got = list(infos)
-    for i in range(n):
-        x, y = got[i], ref[i]
-        assert list(x.keys()) == list(y.keys()), i
-        for k in y:
-            if k == "terminal_observation":
-                np.testing.assert_array_equal(x[k], y[k])
-            else:
-                assert x[k] == y[k] and type(x[k]) is type(y[k]), (i, k, x[k], y[k])
