@@ -247,3 +247,37 @@ def test_launches_on_two_streams_are_ordered(model):
     for name in ("qpos", "qvel", "qacc_warmstart", "time", "reward", "warning", "step_count"):
         assert torch.equal(getattr(a, name), getattr(ref, name)), name
     assert ref.stream_orders() == 0
+
+
+@pytest.mark.parametrize("prec", ["fp64", "fp32"])
+def test_largest_per_gpu_batch_queue_bitwise_equals_direct(model, prec):
+    """The largest batch the configs hold in one place (configs[2]'s whole 32768-env node on ONE
+    GPU: 16384 env pairs, 16x the resident waves of the fp64 engine), staggered episode clocks so
+    auto-resets happen inside the window: the chunk queue ('auto') and one wave per pair ('direct')
+    give bitwise the same states and outputs, with no warning."""
+    import torch
+    from mujocoposelearning_amd.batch import HsBatch
+    n, K = 32768, 3
+    g = torch.Generator(device="cuda").manual_seed(23)
+    acts = torch.rand(K, n, 21, device="cuda", generator=g) * 2 - 1
+    t0 = np.floor(np.arange(n) * 667 / n) * 0.015 + 0.005
+    outs = []
+    for sched in ("auto", "direct"):
+        b = HsBatch(model, n, precision=prec, seed=9)
+        b.configure(frame_skip=3, duration=10.0, reward_id=0, autoreset=1, max_steps=750, schedule=sched)
+        b.reset()
+        b.set_state(time=t0 + 9.9 * (np.arange(n) % 97 == 0))    # some envs finish inside the window
+        o = []
+        for k in range(K):
+            b.step(acts[k])
+            o += [b.obs.clone(), b.reward.clone(), b.terminated.clone(), b.truncated.clone()]
+        torch.cuda.synchronize()
+        if sched == "auto" and prec == "fp64":
+            assert b.queued()
+        o += [b.qpos.clone(), b.qvel.clone(), b.qacc_warmstart.clone(), b.time.clone(), b.episode.clone()]
+        assert b.warning.sum().item() == 0
+        outs.append(o)
+        b.close()
+    assert bool(outs[0][2].any() or outs[0][6].any() or outs[0][10].any())    # an env terminated
+    for k, (x, y) in enumerate(zip(*outs)):
+        assert torch.equal(x, y), k
